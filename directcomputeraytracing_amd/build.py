@@ -1,0 +1,115 @@
+"""Build the in-tree native libraries.
+
+* ``libdcrt.so``  -- the product: host scene/BVH/loader C++ and the gfx950 HIP
+  kernels + tracer, one shared object behind the C ABI of ``include/dcrt.h``.
+* ``oracle/build/libdcrt_oracle.so`` -- the CPU restatement used only by tests
+  and the bench's ``cpu_baseline`` leg (test infrastructure, never the product).
+
+Both compile with IEEE single precision and no floating-point contraction so the
+GPU path and the oracle produce the same bits ("Numerics").
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+ROOT = PKG_DIR.parent
+CSRC = PKG_DIR / "csrc"
+LIB_PATH = PKG_DIR / "libdcrt.so"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "build" / "libdcrt_oracle.so"
+
+HOST_SOURCES = sorted((CSRC / "host").glob("*.cpp"))
+DEVICE_SOURCES = [CSRC / "device" / "tracer.hip"]
+HEADERS = sorted((CSRC / "host").glob("*.h")) + sorted((CSRC / "device").glob("*.h")) + [ROOT / "include" / "dcrt.h"]
+
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-ffp-contract=off",      # no FMA contraction: bit-identical to the oracle
+    "-fno-fast-math",
+    "-fno-gpu-rdc",
+    "-Wall",
+    "-Wno-unused-function",
+    "-Wno-unused-variable",
+    "-Wno-unused-but-set-variable",
+]
+
+
+def _hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the MI355X build needs ROCm's hipcc")
+
+
+def _digest(paths) -> str:
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(str(p).encode())
+        h.update(Path(p).read_bytes())
+    h.update(" ".join(HIPCC_FLAGS).encode())
+    return h.hexdigest()
+
+
+def build_native(force: bool = False, verbose: bool = False) -> Path:
+    sources = HOST_SOURCES + DEVICE_SOURCES
+    digest = _digest(sources + HEADERS)
+    stamp = LIB_PATH.with_suffix(".so.sha256")
+    if not force and LIB_PATH.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+        return LIB_PATH
+    objdir = PKG_DIR / "_build"
+    objdir.mkdir(exist_ok=True)
+    objs = []
+    procs = []
+    for src in sources:
+        obj = objdir / (src.stem + (".dev.o" if src.suffix == ".hip" else ".o"))
+        cmd = [_hipcc(), *HIPCC_FLAGS, "-c", str(src), "-o", str(obj)]
+        if src.suffix == ".cpp":
+            cmd = [_hipcc(), *[f for f in HIPCC_FLAGS if f not in ("--offload-arch=gfx950", "-fno-gpu-rdc")],
+                   "-x", "c++", "-c", str(src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        objs.append(obj)
+    failed = []
+    for src, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            failed.append((src, out.decode(errors="replace")))
+        elif verbose and out:
+            print(out.decode(errors="replace"), file=sys.stderr)
+    if failed:
+        msg = "\n".join(f"--- {s} ---\n{o}" for s, o in failed)
+        raise RuntimeError(f"native build failed:\n{msg}")
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    stamp.write_text(digest)
+    return LIB_PATH
+
+
+def build_oracle(force: bool = False) -> Path:
+    """TEST INFRASTRUCTURE: compile the CPU restatement (gcc, no contraction)."""
+    src = [ORACLE_DIR / "dcrt_oracle.c", ORACLE_DIR / "dcrt_oracle.h", ROOT / "include" / "dcrt.h"]
+    digest = _digest(src)
+    stamp = ORACLE_LIB.with_suffix(".so.sha256")
+    if not force and ORACLE_LIB.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+        return ORACLE_LIB
+    subprocess.run(["make", "-C", str(ORACLE_DIR), f"OUT={ORACLE_LIB.parent}"], check=True,
+                   stdout=subprocess.DEVNULL)
+    stamp.write_text(digest)
+    return ORACLE_LIB
+
+
+if __name__ == "__main__":
+    print(build_native(force="--force" in sys.argv, verbose=True))
+    print(build_oracle(force="--force" in sys.argv))

@@ -1,0 +1,515 @@
+// dscene.h -- HBM-resident scene and its device-side accessors: two-level BVH
+// traversal (BVHAccel.inc.hlsl:85-369), ray/box and ray/triangle tests
+// (RayPrimitiveIntersect.inc.hlsl), hit reconstruction (HitShader.inc.hlsl,
+// RayTracingCommon.inc.hlsl:88-116), lights (Light.inc.hlsl) and texture
+// emulation (BxDFTextures.inc.hlsl, D3D12 SampleLevel at LOD 0).
+#pragma once
+
+#include "../../../include/dcrt.h"
+#include "dmath.h"
+
+namespace dcrt {
+namespace dev {
+
+struct TextureDesc {
+    uint32_t width, height, format, offset;   // offset into the texel blob (bytes)
+};
+
+// Everything a kernel needs about the scene, passed by value (kernel argument).
+struct DeviceScene {
+    const float4* nodes;          // 2 x float4 per BVHNode (min.xyz,max.x | max.yz,right,misc)
+    const float4* triVerts;       // 3 x float4 per triangle: world-independent BLAS positions
+    const dcrt_vertex* vertices;
+    const uint32_t* triangles;
+    const uint32_t* materialIds;
+    const float4* transforms;     // 3 x float4 per matrix, 2N matrices (forward, inverse)
+    const uint32_t* instanceLightIndices;
+    const uint32_t* instanceFlags;
+    const uint32_t* overrides;
+    const dcrt_material* materials;
+    const dcrt_light* lights;
+    const TextureDesc* textures;
+    const uint8_t* texels;
+    const float* srgbTable;       // 256 entries
+    const float* envCube;         // 6 * n * n * 3, or nullptr
+    const uint16_t* lutBrdf;
+    const uint16_t* lutBrdfAvg;
+    const uint16_t* lutBrdfDielectric;
+    const uint16_t* lutBrdfDielectricAvg;
+    const uint16_t* lutBsdf;
+    const uint16_t* lutBsdfAvg;
+    uint32_t instanceCount;
+    uint32_t nodeCount;
+    uint32_t triangleCount;
+    uint32_t envCubeSize;
+    uint32_t stackSize;           // per-lane traversal stack entries
+};
+
+// ---- ray / primitive tests ----------------------------------------------------
+DEV bool ray_aabb(V3 o, V3 inv, float tMin, float tMax, float4 a, float4 b)
+{
+    const float tx0 = (a.x - o.x) * inv.x;
+    const float tx1 = (a.w - o.x) * inv.x;
+    float t0 = fminf(tx0, tx1);
+    float t1 = fmaxf(tx0, tx1);
+    const float ty0 = (a.y - o.y) * inv.y;
+    const float ty1 = (b.x - o.y) * inv.y;
+    t0 = fmaxf(t0, fminf(ty0, ty1));
+    t1 = fminf(t1, fmaxf(ty0, ty1));
+    const float tz0 = (a.z - o.z) * inv.z;
+    const float tz1 = (b.y - o.z) * inv.z;
+    t0 = fmaxf(t0, fminf(tz0, tz1));
+    t1 = fminf(t1, fmaxf(tz0, tz1));
+    return t1 >= t0 && (t0 < tMax && t1 >= tMin);
+}
+
+struct Shear {
+    int kx, ky, kz;
+    float sx, sy, sz;
+};
+DEV Shear make_shear(V3 d)   // BVHAccel.inc.hlsl:72-83
+{
+    Shear s;
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    int z = ax >= ay ? 0 : 1;
+    z = (z == 0 ? ax : ay) >= az ? z : 2;
+    int x = z + 1; x = x == 3 ? 0 : x;
+    int y = x + 1; y = y == 3 ? 0 : y;
+    s.kx = x; s.ky = y; s.kz = z;
+    const float dz = comp(d, z);
+    const float invZ = 1.0f / dz;
+    s.sx = -comp(d, x) * invZ;
+    s.sy = -comp(d, y) * invZ;
+    s.sz = invZ;
+    return s;
+}
+
+// Watertight test (RayPrimitiveIntersect.inc.hlsl:8-70).
+DEV bool tri_watertight(V3 o, const Shear& sh, float tMin, float tMax, V3 v0, V3 v1, V3 v2,
+                        float* t, float* u, float* v, bool* backface)
+{
+    *t = 0.0f; *u = 0.0f; *v = 0.0f; *backface = false;
+    const V3 cp = cross(v1 - v0, v2 - v0);
+    if (dot(cp, cp) == 0.0f) return false;
+    const V3 a = v0 - o, b = v1 - o, c = v2 - o;
+    float p0x = comp(a, sh.kx), p0y = comp(a, sh.ky), p0z = comp(a, sh.kz);
+    float p1x = comp(b, sh.kx), p1y = comp(b, sh.ky), p1z = comp(b, sh.kz);
+    float p2x = comp(c, sh.kx), p2y = comp(c, sh.ky), p2z = comp(c, sh.kz);
+    p0x = p0x + sh.sx * p0z; p0y = p0y + sh.sy * p0z;
+    p1x = p1x + sh.sx * p1z; p1y = p1y + sh.sy * p1z;
+    p2x = p2x + sh.sx * p2z; p2y = p2y + sh.sy * p2z;
+    const float e0 = p1x * p2y - p2x * p1y;
+    const float e1 = p2x * p0y - p0x * p2y;
+    const float e2 = p0x * p1y - p1x * p0y;
+    if ((e0 < 0.0f || e1 < 0.0f || e2 < 0.0f) && (e0 > 0.0f || e1 > 0.0f || e2 > 0.0f)) return false;
+    const float det = e0 + e1 + e2;
+    p0z = p0z * sh.sz; p1z = p1z * sh.sz; p2z = p2z * sh.sz;
+    const float tScaled = e0 * p0z + e1 * p1z + e2 * p2z;
+    const float invDet = 1.0f / det;
+    *t = tScaled * invDet;
+    *u = e1 * invDet;
+    *v = e2 * invDet;
+    *backface = (fsign(sh.sz) * det) < 0.0f;
+    return det != 0.0f && *t >= tMin && *t < tMax;
+}
+
+// Moller-Trumbore (RayPrimitiveIntersect.inc.hlsl:72-103).
+DEV bool tri_moller(V3 o, V3 d, float tMin, float tMax, V3 v0, V3 v1, V3 v2, float* t, float* u, float* v, bool* backface)
+{
+    const V3 v0v1 = v1 - v0, v0v2 = v2 - v0;
+    const V3 pvec = cross(d, v0v2);
+    const float det = dot(v0v1, pvec);
+    const float invDet = 1.0f / det;
+    const V3 tvec = o - v0;
+    *u = dot(tvec, pvec) * invDet;
+    const V3 qvec = cross(tvec, v0v1);
+    *v = dot(d, qvec) * invDet;
+    *t = dot(v0v2, qvec) * invDet;
+    *backface = det > -1e-10f;
+    return fabsf(det) >= 1e-10f && *u >= 0.0f && *u <= 1.0f && *v >= 0.0f && *u + *v <= 1.0f && *t >= tMin && *t < tMax;
+}
+
+DEV V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
+
+struct HitRecord {
+    float t, u, v;
+    uint32_t tri;        // bit 31 = backface
+    uint32_t inst;
+};
+
+// Two-level traversal with a per-lane stack in LDS (column `lane` of a
+// [stackSize][blockDim] array: consecutive lanes hit consecutive banks).
+// ANY_HIT = BVHIntersect (shadow), else BVHIntersectNoInterp (closest hit).
+// Traversal counters (SRayTraversalCounters semantics) go to *stats when non-null.
+struct TraversalStats {
+    uint32_t nodes;   // iterationCounter (BVHAccel.inc.hlsl:121)
+    uint32_t tris;    // triangle tests
+    uint32_t blas;    // TLAS -> BLAS entries
+};
+
+template <bool ANY_HIT>
+DEV bool traverse_stats(const DeviceScene& sc, V3 origin, V3 dir, float tMin, float tMaxIn, uint32_t features,
+                        uint32_t* lds, uint32_t stride, HitRecord* hit, TraversalStats* stats)
+{
+    uint32_t tris = 0, blas = 0;
+    const bool watertight = (features & DCRT_FEATURE_WATERTIGHT) != 0;
+    const bool f2b = (features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
+    float tMax = tMaxIn;
+    uint32_t count = 0;
+    uint32_t node = 0, inst = 0;
+    bool inBlas = false;
+    V3 lo = origin, ld = dir;
+    V3 inv = inv_dir(ld);
+    Shear sh;
+    bool shearValid = false;
+    uint32_t n = 0;
+    for (;;) {
+        ++n;
+        const float4 a = sc.nodes[node * 2];
+        const float4 b = sc.nodes[node * 2 + 1];
+        bool pop = false;
+        if (ray_aabb(lo, inv, tMin, tMax, a, b)) {
+            const uint32_t misc = asu(b.w);
+            const uint32_t primOrInst = (misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
+            if (misc & 0x4u) {
+                const float4* M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
+                lo = mul43(origin, 1.0f, M);
+                ld = mul43(dir, 0.0f, M);
+                inv = inv_dir(ld);
+                shearValid = false;
+                inBlas = true;
+                inst = primOrInst;
+                node = asu(b.z);
+                ++blas;
+            } else if (primOrInst == 0) {
+                const uint32_t axis = misc & 0x3u;
+                bool neg = false;
+                if (f2b) neg = axis == 0 ? ld.x < 0.0f : (axis == 1 ? ld.y < 0.0f : ld.z < 0.0f);
+                const uint32_t right = asu(b.z);
+                const uint32_t push = neg ? node + 1 : right;
+                node = neg ? right : node + 1;
+                if (count < sc.stackSize) lds[count * stride] = (push & 0x7FFFFFFFu) | (inBlas ? 0x80000000u : 0u);
+                ++count;
+            } else {
+                if (watertight && !shearValid) { sh = make_shear(ld); shearValid = true; }
+                const uint32_t begin = asu(b.z);
+                const uint32_t end = begin + primOrInst;
+                for (uint32_t p = begin; p < end; ++p) {
+                    ++tris;
+                    const float4 q0 = sc.triVerts[(size_t)p * 3];
+                    const float4 q1 = sc.triVerts[(size_t)p * 3 + 1];
+                    const float4 q2 = sc.triVerts[(size_t)p * 3 + 2];
+                    const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+                    float t, u, v; bool bf;
+                    const bool h = watertight ? tri_watertight(lo, sh, tMin, tMax, v0, v1, v2, &t, &u, &v, &bf)
+                                              : tri_moller(lo, ld, tMin, tMax, v0, v1, v2, &t, &u, &v, &bf);
+                    if (h) {
+                        if (ANY_HIT) {
+                            if (stats) { stats->nodes = n; stats->tris = tris; stats->blas = blas; }
+                            return true;
+                        }
+                        tMax = t;
+                        hit->t = t; hit->u = u; hit->v = v;
+                        hit->tri = (p & 0x7FFFFFFFu) | (bf ? 0x80000000u : 0u);
+                        hit->inst = inst;
+                    }
+                }
+                pop = true;
+            }
+        } else {
+            pop = true;
+        }
+        if (pop) {
+            if (count == 0) break;
+            --count;
+            const uint32_t packed = count < sc.stackSize ? lds[count * stride] : 0u;
+            const bool wasBlas = inBlas;
+            node = packed & 0x7FFFFFFFu;
+            inBlas = (packed & 0x80000000u) != 0;
+            if (wasBlas != inBlas) { lo = origin; ld = dir; inv = inv_dir(ld); shearValid = false; }
+        }
+    }
+    if (stats) { stats->nodes = n; stats->tris = tris; stats->blas = blas; }
+    if (ANY_HIT) return false;
+    return !isinf(tMax);
+}
+
+// ---- texture emulation ----------------------------------------------------------
+DEV float u16tex(const uint16_t* t, int x, int y, int w) { return (float)t[y * w + x] / 65535.0f; }
+DEV int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+DEV float bilinear_u16(const uint16_t* tex, int w, int h, float u, float v)
+{
+    const float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    const float fx = x - fx0, fy = y - fy0;
+    const int x0 = clampi((int)fx0, 0, w - 1), x1 = clampi((int)fx0 + 1, 0, w - 1);
+    const int y0 = clampi((int)fy0, 0, h - 1), y1 = clampi((int)fy0 + 1, 0, h - 1);
+    const float a = u16tex(tex, x0, y0, w) * (1.0f - fx) + u16tex(tex, x1, y0, w) * fx;
+    const float c = u16tex(tex, x0, y1, w) * (1.0f - fx) + u16tex(tex, x1, y1, w) * fx;
+    return a * (1.0f - fy) + c * fy;
+}
+DEV int array_slice(float s, int slices)
+{
+    const float r = floorf(s + 0.5f);
+    if (!(r > 0.0f)) return 0;
+    if (r > (float)(slices - 1)) return slices - 1;
+    return (int)r;
+}
+DEV float remap(uint32_t dim, float u) { return u * ((float)(dim - 1) / (float)dim) + 0.5f / (float)dim; }
+DEV float sample_array(const uint16_t* tex, uint32_t w, uint32_t h, uint32_t slices, float uu, float vv, float ww, uint32_t dz, uint32_t off)
+{
+    const float slicePos = ww * ((float)dz - 1.0f);
+    const float fraction = slicePos - floorf(slicePos);
+    const float u = remap(w, uu), v = remap(h, vv);
+    const uint32_t s0 = (uint32_t)(int32_t)slicePos + off;
+    const uint32_t s1 = (uint32_t)(int32_t)slicePos + 1u + off;
+    const int i0 = array_slice((float)s0, (int)slices), i1 = array_slice((float)s1, (int)slices);
+    const float a = bilinear_u16(tex + (size_t)i0 * w * h, (int)w, (int)h, u, v);
+    const float b = bilinear_u16(tex + (size_t)i1 * w * h, (int)w, (int)h, u, v);
+    return lerp(a, b, fraction);
+}
+DEV float lut_brdf(const DeviceScene& s, float cosThetaO, float alpha)
+{
+    return bilinear_u16(s.lutBrdf, 32, 32, remap(32, cosThetaO), remap(32, alpha));
+}
+DEV float lut_brdf_avg(const DeviceScene& s, float alpha)
+{
+    const float u = remap(32, alpha);
+    return bilinear_u16(s.lutBrdfAvg, 32, 1, u, u);
+}
+DEV float lut_brdf_dielectric(const DeviceScene& s, float cosThetaO, float alpha, float eta, bool entering)
+{
+    return sample_array(s.lutBrdfDielectric, 32, 16, 32, cosThetaO, alpha, (eta - 1.0f) / 2.0f, 16, entering ? 16u : 0u);
+}
+DEV float lut_brdf_dielectric_avg(const DeviceScene& s, float alpha, float eta, bool entering)
+{
+    return sample_array(s.lutBrdfDielectricAvg, 16, 16, 2, alpha, (eta - 1.0f) / 2.0f, 0.0f, 1, entering ? 1u : 0u);
+}
+DEV float lut_bsdf(const DeviceScene& s, float cosThetaO, float alpha, float eta, bool entering)
+{
+    return sample_array(s.lutBsdf, 32, 16, 32, cosThetaO, alpha, (eta - 1.0f) / 2.0f, 16, entering ? 16u : 0u);
+}
+DEV float lut_bsdf_avg(const DeviceScene& s, float alpha, float eta, bool entering)
+{
+    return sample_array(s.lutBsdfAvg, 16, 16, 2, alpha, (eta - 1.0f) / 2.0f, 0.0f, 1, entering ? 1u : 0u);
+}
+
+DEV int wrapi(int i, int n) { const int r = i % n; return r < 0 ? r + n : r; }
+DEV void texel(const DeviceScene& s, const TextureDesc& t, int x, int y, float* o)
+{
+    if (t.format == DCRT_TEXTURE_FORMAT_R8_UNORM) {
+        o[0] = (float)s.texels[t.offset + (size_t)y * t.width + x] / 255.0f; o[1] = 0.0f; o[2] = 0.0f; o[3] = 1.0f;
+    } else {
+        const uint8_t* p = s.texels + t.offset + ((size_t)y * t.width + x) * 4;
+        o[0] = s.srgbTable[p[0]]; o[1] = s.srgbTable[p[1]]; o[2] = s.srgbTable[p[2]]; o[3] = (float)p[3] / 255.0f;
+    }
+}
+DEV void sample_texture_wrap(const DeviceScene& s, uint32_t index, float u, float v, float* out)
+{
+    const TextureDesc t = s.textures[index];
+    if (t.width == 0 || t.height == 0) { out[0] = out[1] = out[2] = out[3] = 0.0f; return; }   // null SRV reads 0
+    const int w = (int)t.width, h = (int)t.height;
+    const float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    const float fx = x - fx0, fy = y - fy0;
+    const int x0 = wrapi((int)fx0, w), x1 = wrapi((int)fx0 + 1, w);
+    const int y0 = wrapi((int)fy0, h), y1 = wrapi((int)fy0 + 1, h);
+    float a[4], b[4], c[4], d[4];
+    texel(s, t, x0, y0, a); texel(s, t, x1, y0, b); texel(s, t, x0, y1, c); texel(s, t, x1, y1, d);
+    for (int i = 0; i < 4; ++i) {
+        const float top = a[i] * (1.0f - fx) + b[i] * fx;
+        const float bot = c[i] * (1.0f - fx) + d[i] * fx;
+        out[i] = top * (1.0f - fy) + bot * fy;
+    }
+}
+DEV V3 sample_env(const DeviceScene& s, V3 d)
+{
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    int face; float sc, tc, ma;
+    if (ax >= ay && ax >= az) { ma = ax; if (d.x >= 0.0f) { face = 0; sc = -d.z; tc = -d.y; } else { face = 1; sc = d.z; tc = -d.y; } }
+    else if (ay >= az) { ma = ay; if (d.y >= 0.0f) { face = 2; sc = d.x; tc = d.z; } else { face = 3; sc = d.x; tc = -d.z; } }
+    else { ma = az; if (d.z >= 0.0f) { face = 4; sc = d.x; tc = -d.y; } else { face = 5; sc = -d.x; tc = -d.y; } }
+    const float u = (sc / ma + 1.0f) * 0.5f, v = (tc / ma + 1.0f) * 0.5f;
+    const int n = (int)s.envCubeSize;
+    const float x = u * (float)n - 0.5f, y = v * (float)n - 0.5f;
+    const float fx0 = floorf(x), fy0 = floorf(y);
+    const float fx = x - fx0, fy = y - fy0;
+    const int x0 = clampi((int)fx0, 0, n - 1), x1 = clampi((int)fx0 + 1, 0, n - 1);
+    const int y0 = clampi((int)fy0, 0, n - 1), y1 = clampi((int)fy0 + 1, 0, n - 1);
+    const float* base = s.envCube + (size_t)face * n * n * 3;
+    float o[3];
+    for (int i = 0; i < 3; ++i) {
+        const float a = base[((size_t)y0 * n + x0) * 3 + i], b = base[((size_t)y0 * n + x1) * 3 + i];
+        const float c = base[((size_t)y1 * n + x0) * 3 + i], e = base[((size_t)y1 * n + x1) * 3 + i];
+        const float top = a * (1.0f - fx) + b * fx;
+        const float bot = c * (1.0f - fx) + e * fx;
+        o[i] = top * (1.0f - fy) + bot * fy;
+    }
+    return mk(o[0], o[1], o[2]);
+}
+
+// ---- hit reconstruction --------------------------------------------------------
+struct Intersection {
+    V3 albedo; float alpha;
+    V3 position, normal, tangent, geometryNormal, ior;
+    bool isTwoSided, backface, multiscattering;
+    uint32_t internalScatteringMode, materialType, lightIndex, triangleIndex;
+};
+
+DEV V3 bary3(V3 p0, V3 p1, V3 p2, float u, float v)   // Math.inc.hlsl:35-43
+{
+    V3 r1 = p1 - p0, r2 = p2 - p0;
+    r1 = r1 * u; r2 = r2 * v;
+    r1 = r1 + p0; r1 = r1 + r2;
+    return r1;
+}
+
+DEV void hit_to_intersection(const DeviceScene& s, const HitRecord& h, Intersection& it)
+{
+    const uint32_t inst = h.inst, tri = h.tri & 0x7FFFFFFFu;
+    it.lightIndex = s.instanceLightIndices[inst];
+    it.triangleIndex = tri;
+    const uint32_t ov = s.overrides[inst];
+    const dcrt_vertex& V0 = s.vertices[s.triangles[tri * 3]];
+    const dcrt_vertex& V1 = s.vertices[s.triangles[tri * 3 + 1]];
+    const dcrt_vertex& V2 = s.vertices[s.triangles[tri * 3 + 2]];
+    const float u = h.u, v = h.v;
+    const V3 p0 = ld3(V0.position), p1 = ld3(V1.position), p2 = ld3(V2.position);
+    it.position = bary3(p0, p1, p2, u, v);
+    it.normal = normalize(bary3(ld3(V0.normal), ld3(V1.normal), ld3(V2.normal), u, v));
+    V3 tangent = bary3(ld3(V0.tangent), ld3(V1.tangent), ld3(V2.tangent), u, v);
+    float tl = length(tangent);
+    if (tl >= 0.000001f) {
+        tangent = tangent - it.normal * dot(tangent, it.normal);
+        tl = length(tangent);
+    }
+    if (tl < 0.000001f) {
+        tangent = cross(it.normal, mk(0.0f, 1.0f, 0.0f));
+        tl = length(tangent);
+        tangent = tl >= 0.000001f ? tangent : mk(1.0f, 0.0f, 0.0f);
+    }
+    it.tangent = tangent / tl;
+    it.geometryNormal = normalize(cross(p2 - p0, p1 - p0));
+    const uint32_t mid = ov != DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE ? ov : s.materialIds[tri];
+    const dcrt_material& m = s.materials[mid];
+    // VectorBaryCentric2 (Math.inc.hlsl:23-33)
+    float r1x = V1.texcoord[0] - V0.texcoord[0], r1y = V1.texcoord[1] - V0.texcoord[1];
+    float r2x = V2.texcoord[0] - V0.texcoord[0], r2y = V2.texcoord[1] - V0.texcoord[1];
+    r1x = r1x * u; r1y = r1y * u; r2x = r2x * v; r2y = r2y * v;
+    r1x = r1x + V0.texcoord[0]; r1y = r1y + V0.texcoord[1];
+    float tcx = r1x + r2x, tcy = r1y + r2y;
+    tcx = tcx * m.tex_tiling[0]; tcy = tcy * m.tex_tiling[1];
+    V3 albedo = ld3(m.albedo);
+    if (m.albedo_texture_index != -1) {
+        float rgba[4];
+        sample_texture_wrap(s, (uint32_t)m.albedo_texture_index, tcx, tcy, rgba);
+        albedo = albedo * mk(rgba[0], rgba[1], rgba[2]);
+    }
+    const float checker = ((f2u_sat(tcx * 2.0f) + f2u_sat(tcy * 2.0f)) & 0x1u) != 0 ? 1.0f : 0.0f;
+    float roughness = m.roughness;
+    roughness = roughness * ((m.flags & DCRT_MATERIAL_FLAG_ROUGHNESS_TEXTURE) != 0 ? checker : 1.0f);
+    it.albedo = albedo;
+    it.alpha = roughness * roughness;
+    it.ior = ld3(m.ior);
+    it.materialType = m.flags & DCRT_MATERIAL_FLAG_TYPE_MASK;
+    it.isTwoSided = (m.flags & DCRT_MATERIAL_FLAG_IS_TWOSIDED) != 0;
+    it.multiscattering = (m.flags & DCRT_MATERIAL_FLAG_MULTISCATTERING) != 0;
+    it.internalScatteringMode = (m.flags & DCRT_MATERIAL_FLAG_INTERNAL_SCATTERING_MASK) >> DCRT_MATERIAL_FLAG_INTERNAL_SCATTERING_SHIFT;
+    it.backface = (h.tri & 0x80000000u) != 0;
+    const float4* M = s.transforms + (size_t)inst * 3;
+    it.position = mul43(it.position, 1.0f, M);
+    it.normal = normalize(mul43(it.normal, 0.0f, M));
+    it.geometryNormal = normalize(mul43(it.geometryNormal, 0.0f, M));
+    it.tangent = normalize(mul43(it.tangent, 0.0f, M));
+}
+
+// ---- lights (Light.inc.hlsl, RayTracingCommon.inc.hlsl:124-225) -------------------
+struct LightSample {
+    V3 radiance, wi;
+    float pdf, distance;
+    bool isDelta;
+};
+DEV V3 tri_pos(const DeviceScene& s, uint32_t tri, int k) { return ld3(s.vertices[s.triangles[tri * 3 + k]].position); }
+
+DEV LightSample sample_light(const DeviceScene& s, V3 p, uint32_t lightCount, Rng& rng)
+{
+    LightSample r;
+    r.radiance = mk(0.0f, 0.0f, 0.0f); r.wi = mk(0.0f, 0.0f, 0.0f); r.pdf = 0.0f; r.distance = 0.0f; r.isDelta = false;
+    const float sel = next1(rng);
+    const uint32_t li = (uint32_t)floorf(sel * (float)lightCount);
+    const dcrt_light& L = s.lights[li];
+    if (L.flags & DCRT_LIGHT_FLAGS_POINT_LIGHT) {
+        r.wi = ld3(L.position_or_triangle_range) - p;
+        r.distance = length(r.wi);
+        r.wi = r.wi / r.distance;
+        r.radiance = ld3(L.radiance) / (r.distance * r.distance);
+        r.pdf = 1.0f;
+        r.isDelta = true;
+    } else if (L.flags & DCRT_LIGHT_FLAGS_DIRECTIONAL_LIGHT) {
+        r.wi = -ld3(L.position_or_triangle_range);
+        r.distance = inf();
+        r.radiance = ld3(L.radiance);
+        r.pdf = 1.0f;
+        r.isDelta = true;
+    } else if (L.flags & DCRT_LIGHT_FLAGS_MESH_LIGHT) {
+        const float triSel = next1(rng);
+        const float ts0 = next1(rng), ts1 = next1(rng);
+        const uint32_t triOffset = asu(L.position_or_triangle_range[0]);
+        const uint32_t triCount = asu(L.position_or_triangle_range[1]);
+        const uint32_t instance = asu(L.position_or_triangle_range[2]);
+        const uint32_t tri = (uint32_t)((float)triOffset + floorf(triSel * (float)triCount));
+        const V3 v0 = tri_pos(s, tri, 0), v1 = tri_pos(s, tri, 1), v2 = tri_pos(s, tri, 2);
+        const float4* M = s.transforms + (size_t)instance * 3;
+        const V3 w0 = mul43(v0, 1.0f, M), w1 = mul43(v1, 1.0f, M), w2 = mul43(v2, 1.0f, M);
+        const float area = length(cross(w2 - w0, w1 - w0)) * 0.5f;
+        const float sq = sqrtf(ts0);
+        const float bu = 1.0f - sq, bv = ts1 * sq;
+        V3 sp = bary3(v0, v1, v2, bu, bv);
+        V3 nrm = normalize(cross(v2 - v0, v1 - v0));
+        float pdf = area >= 1e-6f ? 1.0f / (area * 0.5f) : 0.0f;
+        sp = mul43(sp, 1.0f, M);
+        nrm = normalize(mul43(nrm, 0.0f, M));
+        r.wi = sp - p;
+        r.distance = length(r.wi);
+        r.wi = r.wi / r.distance;
+        const float WIdotN = -dot(r.wi, nrm);
+        pdf = pdf * (r.distance * r.distance / WIdotN);
+        r.radiance = (WIdotN > 0.0f && pdf > 0.0f) ? ld3(L.radiance) : mk(0.0f, 0.0f, 0.0f);
+        r.pdf = WIdotN > 0.0f ? pdf : 0.0f;
+        r.pdf = r.pdf / (float)triCount;
+    } else if (L.flags & DCRT_LIGHT_FLAGS_ENVIRONMENT_LIGHT) {
+        const float a = next1(rng), b = next1(rng);
+        r.wi = uniform_sphere(a, b);
+        r.pdf = uniform_sphere_pdf();
+        r.radiance = s.envCube ? sample_env(s, r.wi) * ld3(L.radiance) : ld3(L.radiance);
+        r.distance = inf();
+    }
+    r.pdf = r.pdf / (float)lightCount;
+    if (r.distance != inf()) r.distance = r.distance * (1.0f - kShadowEpsilon);
+    return r;
+}
+
+DEV void evaluate_light(const DeviceScene& s, uint32_t li, uint32_t tri, V3 normal, V3 wi, float distance, uint32_t lightCount,
+                        V3* radiance, float* pdf)
+{
+    *radiance = mk(0.0f, 0.0f, 0.0f);
+    *pdf = 0.0f;
+    const dcrt_light& L = s.lights[li];
+    if (L.flags & DCRT_LIGHT_FLAGS_MESH_LIGHT) {
+        const float4* M = s.transforms + (size_t)asu(L.position_or_triangle_range[2]) * 3;
+        const V3 v0 = mul43(tri_pos(s, tri, 0), 1.0f, M), v1 = mul43(tri_pos(s, tri, 1), 1.0f, M), v2 = mul43(tri_pos(s, tri, 2), 1.0f, M);
+        const float area = length(cross(v2 - v0, v1 - v0));
+        float p = area >= 1e-6f ? 1.0f / (area * 0.5f) : 0.0f;
+        const float WIdotN = -dot(wi, normal);
+        *radiance = WIdotN > 0.0f ? ld3(L.radiance) : mk(0.0f, 0.0f, 0.0f);
+        p = p * (WIdotN > 0.0f ? distance * distance / dot(-wi, normal) : 0.0f);
+        *pdf = p / (float)asu(L.position_or_triangle_range[1]);
+    } else if (L.flags & DCRT_LIGHT_FLAGS_ENVIRONMENT_LIGHT) {
+        *radiance = s.envCube ? sample_env(s, wi) * ld3(L.radiance) : ld3(L.radiance);
+        *pdf = uniform_sphere_pdf();
+    }
+    *pdf = *pdf / (float)lightCount;
+}
+
+}  // namespace dev
+}  // namespace dcrt

@@ -1,0 +1,111 @@
+// kernels.h -- the wavefront path tracing kernels for gfx950
+// (Shaders/WavefrontPathTracing.hlsl restated for 64-lane waves).
+//
+// Path pool is struct-of-arrays in HBM; queues are compacted with 64-bit wave
+// ballots + mbcnt prefix counts and ONE atomic per workgroup (the reference
+// issues one per 32-lane wave). CONTROL and NEW_PATH are fused: a fully idle
+// wave claims an 8x8 pixel block and generates its camera rays in place.
+#pragma once
+
+#include "dbsdf.h"
+
+namespace dcrt {
+namespace dev {
+
+constexpr uint32_t kFlagIdle = 0x80000000u;           // WavefrontPathTracing.hlsl:27-64
+constexpr uint32_t kFlagShadowRayHit = 0x40000000u;
+constexpr uint32_t kFlagTerminate = 0x20000000u;
+constexpr uint32_t kBlockW = 8, kBlockH = 8;           // one wave64 = one 8x8 pixel block
+
+struct Counters {        // one set per iteration parity
+    uint32_t ext, shadow, material, newPath;
+    uint32_t pad[4];
+};
+struct Globals {
+    uint32_t nextBlock;
+    uint32_t totalBlocks;
+    uint32_t stackOverflow;
+    uint32_t pad0;
+    unsigned long long extRays, shadowRays, newPaths, iterations;
+};
+
+// Per-image constants, read from HBM so a captured graph can be replayed for
+// every frame seed (SNewPathConstants / SMaterialConstants / SControlConstants).
+struct FrameConstants {
+    float camera[16];
+    uint32_t resolution[2];
+    float filmSize[2];
+    float apertureRadius, focalDistance, filmDistance;
+    uint32_t bladeCount;
+    float bladeVertexPos[2];
+    float apertureBaseAngle;
+    uint32_t frameSeed;
+    uint32_t maxBounce, lightCount, envLightIndex, features;
+    uint32_t blocksX, bandCount;     // blocks per row, number of 8-row bands
+};
+
+// SampleAperture + GenerateRay (RayTracingCommon.inc.hlsl:38-86).
+DEV void generate_ray(const FrameConstants& f, float fsx, float fsy, float a0, float a1, float a2, V3* origin, V3* direction)
+{
+    V3 filmPos = mk(-fsx + 0.5f, fsy - 0.5f, -f.filmDistance);
+    filmPos.x = filmPos.x * f.filmSize[0];
+    filmPos.y = filmPos.y * f.filmSize[1];
+    V3 o = mk(0.0f, 0.0f, 0.0f);
+    V3 d = normalize(-filmPos);
+    if (f.apertureRadius > 0.0f) {
+        float apx, apy;
+        if (f.bladeCount <= 2) {
+            concentric_disk(a0, a1, &apx, &apy);
+            apx = apx * f.apertureRadius;
+            apy = apy * f.apertureRadius;
+        } else {
+            const float s = sqrtf(a0);
+            const float u = 1.0f - s, v = a1 * s;
+            const float px = f.bladeVertexPos[0] * (u + v);
+            const float py = f.bladeVertexPos[1] * u - f.bladeVertexPos[1] * v;
+            const float n = floorf(a2 * (float)f.bladeCount);
+            const float theta = n * (kPiMul2 / (float)f.bladeCount) + f.apertureBaseAngle;
+            float st, ct;
+            det_sincos(theta, &st, &ct);
+            apx = px * ct - py * st;
+            apy = py * ct + px * st;
+        }
+        const V3 focus = d * (f.focalDistance / d.z);
+        o = mk(apx, apy, 0.0f);
+        d = normalize(focus - o);
+    }
+    *origin = mul44(o, 1.0f, f.camera);
+    *direction = mul44(d, 0.0f, f.camera);
+}
+
+struct PathPool {
+    float4* rayO;        // origin.xyz, tMax
+    float4* rayD;        // direction.xyz, tMin
+    float4* hit;         // t, u, v, asfloat(triangle | backface << 31)
+    uint32_t* hitInst;
+    float4* shadowO;
+    float4* shadowD;
+    uint32_t* pixel;     // x | y << 16
+    float2* pixelSample;
+    uint4* rng;
+    float4* lsr;         // light sampling result
+    float4* throughput;  // T.xyz, bsdfPdf
+    float4* li;          // Li.xyz, isDeltaBxdf (0/1)
+    uint32_t* flags;
+    uint32_t* extQueue;
+    uint32_t* shadowQueue;
+    uint32_t* materialQueue;
+    uint32_t size;
+};
+
+struct Film {
+    float2* samplePosition;   // W*H
+    float4* sampleValue;      // W*H
+    uint4* debugRng;          // W*H or nullptr
+    float4* accum;            // W*H RGBA32F (sum w*L, sum w)
+    const uint32_t* bandY;    // first row of each 8-row band this tracer renders
+    uint32_t width, height;
+};
+
+}  // namespace dev
+}  // namespace dcrt

@@ -1,0 +1,512 @@
+// kernels_impl.h -- MI355X (gfx950) kernels of the wavefront path tracer and the
+// BxDF LUT integrator. Host orchestration lives in tracer.hip.
+//
+// Reference map (Shaders/WavefrontPathTracing.hlsl):
+//   set_idle_kernel      SET_IDLE            :628-651
+//   control_kernel       CONTROL + NEW_PATH  :483-607 + :176-255 (fused)
+//   material_kernel      MATERIAL            :257-481
+//   extension_kernel     EXTENSION_RAY_CAST  :66-122
+//   shadow_kernel        SHADOW_RAY_CAST     :124-174
+//   film_kernel          SampleConvolution.hlsl:67-106
+//   lut_*_kernel         BxDFTexturesBuilding.hlsl:10-186
+#include "kernels.h"
+// (included once, by tracer.hip)
+
+namespace dcrt {
+namespace dev {
+
+// One atomic per workgroup: wave ballot + mbcnt prefix, LDS scan over waves.
+// Every thread of the block must call it (it contains barriers).
+__device__ __forceinline__ uint32_t block_append(bool pred, uint32_t* counter, uint32_t* sm)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const unsigned long long mask = __ballot(pred);
+    const uint32_t prefix = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+    if (lane == 0) sm[wave] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t total = 0;
+        const uint32_t waves = blockDim.x >> 6;
+        for (uint32_t w = 0; w < waves; ++w) { const uint32_t c = sm[w]; sm[w] = total; total += c; }
+        sm[32] = total ? atomicAdd(counter, total) : 0u;
+    }
+    __syncthreads();
+    const uint32_t r = sm[32] + sm[wave] + prefix;
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
+{
+    unsigned long long s = v;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    return s;
+}
+
+__global__ void set_frame_kernel(FrameConstants* dst, FrameConstants src) { *dst = src; }
+
+__global__ void set_idle_kernel(PathPool pool, Counters* counters, Globals* g, uint32_t totalBlocks)
+{
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid < pool.size) pool.flags[tid] = kFlagIdle;
+    if (tid < 2 * (uint32_t)(sizeof(Counters) / 4)) ((uint32_t*)counters)[tid] = 0u;
+    if (tid == 0) { g->nextBlock = 0u; g->totalBlocks = totalBlocks; }
+}
+
+__global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32_t* triangles, uint32_t count, float4* out)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    for (int k = 0; k < 3; ++k) {
+        const dcrt_vertex& v = vertices[triangles[t * 3 + k]];
+        out[(size_t)t * 3 + k] = make_float4(v.position[0], v.position[1], v.position[2], 0.0f);
+    }
+}
+
+// ---- CONTROL (+ NEW_PATH) -------------------------------------------------------
+__global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, const FrameConstants* fc, Counters* cnt,
+                                                       Globals* g, uint32_t debugRng)
+{
+    __shared__ uint32_t sm[64];
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < pool.size; base += gridDim.x * blockDim.x) {
+    const uint32_t tid = base + threadIdx.x;
+    const uint32_t flags = pool.flags[tid];
+    bool idle = (flags & kFlagIdle) != 0;
+    const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
+    const bool terminate = (flags & kFlagTerminate) != 0;
+    uint32_t bounce = flags & 0xFFu;
+    if (!idle) {
+        float4 li = pool.li[tid];
+        const float4 lsr = pool.lsr[tid];
+        li.x = li.x + (!shadowHit ? lsr.x : 0.0f);
+        li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
+        li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
+        if (terminate) {
+            const uint32_t pp = pool.pixel[tid];
+            const size_t p = (size_t)(pp >> 16) * film.width + (pp & 0xFFFFu);
+            film.samplePosition[p] = pool.pixelSample[tid];
+            film.sampleValue[p] = make_float4(li.x, li.y, li.z, 0.0f);
+            if (debugRng) film.debugRng[p] = pool.rng[tid];
+            idle = true;
+        } else {
+            pool.li[tid] = li;
+        }
+    }
+    const uint32_t mslot = block_append(!idle, &cnt->material, sm);
+    if (!idle) pool.materialQueue[mslot] = tid;
+
+    // A fully idle wave claims the next 8x8 block (one atomic per workgroup).
+    const bool waveIdle = __ballot(!idle) == 0ull;
+    bool want = false;
+    if (waveIdle && lane == 0) want = __hip_atomic_load(&g->nextBlock, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g->totalBlocks;
+    const uint32_t bslot = block_append(want, &g->nextBlock, sm);
+    const uint32_t block = (uint32_t)__shfl((int)bslot, 0, 64);
+    const bool got = __shfl((int)want, 0, 64) != 0 && block < g->totalBlocks;
+    bool newPath = false;
+    if (got) {
+        const uint32_t band = block / fc->blocksX, bx = block % fc->blocksX;
+        const uint32_t px = bx * kBlockW + (lane % kBlockW);
+        const uint32_t py = film.bandY[band] + lane / kBlockW;
+        const bool clipped = px >= fc->resolution[0] || py >= fc->resolution[1];
+        if (!clipped) {
+            // NEW_PATH :211-237
+            Rng rng = rng_init(px, py, fc->frameSeed);
+            const float psx = next1(rng), psy = next1(rng);
+            const float fsx = (psx + (float)px) / (float)fc->resolution[0];
+            const float fsy = (psy + (float)py) / (float)fc->resolution[1];
+            const float a0 = next1(rng), a1 = next1(rng), a2 = next1(rng);
+            V3 o, d;
+            generate_ray(*fc, fsx, fsy, a0, a1, a2, &o, &d);
+            pool.pixel[tid] = px | (py << 16);
+            pool.pixelSample[tid] = make_float2(psx, psy);
+            pool.lsr[tid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            pool.rng[tid] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+            pool.rayO[tid] = make_float4(o.x, o.y, o.z, inf());
+            pool.rayD[tid] = make_float4(d.x, d.y, d.z, 0.0f);
+            pool.li[tid] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+            pool.throughput[tid] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+            newPath = true;
+            idle = false;
+            bounce = 0;
+        }
+    }
+    const uint32_t eslot = block_append(newPath, &cnt->ext, sm);
+    if (newPath) pool.extQueue[eslot] = tid;
+    pool.flags[tid] = (idle ? kFlagIdle : 0u) | (bounce & 0xFFu);
+    }
+}
+
+// ---- MATERIAL -----------------------------------------------------------------------
+__global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt)
+{
+    __shared__ uint32_t sm[64];
+    const uint32_t count = cnt->material;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    const bool active = i < count;
+    bool terminate = false, hasShadow = false;
+    uint32_t path = 0;
+    if (active) {
+        path = pool.materialQueue[i];
+        const float4 h4 = pool.hit[path];
+        HitRecord hit;
+        hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = pool.hitInst[path];
+        const float4 ro = pool.rayO[path], rd = pool.rayD[path];
+        const V3 dir = mk(rd.x, rd.y, rd.z);
+        const uint4 r4 = pool.rng[path];
+        Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
+        float4 thr = pool.throughput[path];
+        float4 li = pool.li[path];
+        uint32_t flags = pool.flags[path];
+        const uint32_t bounce = flags & 0xFFu;
+        const uint32_t features = fc->features;
+        const bool vndf = (features & DCRT_FEATURE_GGX_SAMPLE_VNDF) != 0;
+        const bool hasHit = hit.t != inf();
+        Intersection it;
+        it.lightIndex = DCRT_LIGHT_INDEX_INVALID; it.triangleIndex = 0;
+        it.geometryNormal = mk(0.0f, 0.0f, 0.0f);
+        if (hasHit) hit_to_intersection(sc, hit, it);
+        V3 T = mk(thr.x, thr.y, thr.z);
+        V3 L = mk(li.x, li.y, li.z);
+        // Evaluate light :331-349
+        {
+            const uint32_t lightIndex = hasHit ? it.lightIndex : fc->envLightIndex;
+            const bool visible = (features & DCRT_FEATURE_LIGHT_VISIBLE) != 0;
+            if (visible ? lightIndex != DCRT_LIGHT_INDEX_INVALID : (bounce > 0 && lightIndex != DCRT_LIGHT_INDEX_INVALID)) {
+                V3 radiance; float lightPdf;
+                evaluate_light(sc, lightIndex, it.triangleIndex, it.geometryNormal, dir, hit.t, fc->lightCount, &radiance, &lightPdf);
+                if (lightPdf > 0.0f) {
+                    const float weight = !(li.w != 0.0f) ? power_heuristic(thr.w, lightPdf) : 1.0f;
+                    L = L + T * radiance * weight;
+                }
+            }
+        }
+        V3 lsr = mk(0.0f, 0.0f, 0.0f);
+        if (bounce > fc->maxBounce || !hasHit) {
+            flags |= kFlagTerminate;
+            terminate = true;
+        } else {
+            const V3 wo = -dir;
+            if (fc->lightCount != 0) {
+                const LightSample ls = sample_light(sc, it.position, fc->lightCount, rng);
+                if (any_pos(ls.radiance) && ls.pdf > 0.0f) {
+                    const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, wo, it);
+                    const float NdotWI = fabsf(dot(it.normal, ls.wi));
+                    const float bsdfPdf = evaluate_bsdf_pdf(sc, vndf, ls.wi, wo, it);
+                    const float weight = ls.isDelta ? 1.0f : power_heuristic(ls.pdf, bsdfPdf);
+                    lsr = T * ls.radiance * bsdf * NdotWI * weight / ls.pdf;
+                    const V3 so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
+                    pool.shadowO[path] = make_float4(so.x, so.y, so.z, ls.distance);
+                    pool.shadowD[path] = make_float4(ls.wi.x, ls.wi.y, ls.wi.z, 0.0f);
+                    hasShadow = true;
+                }
+            }
+            float bsdfPdf = 0.0f;
+            bool isDelta = false;
+            {
+                const float sel = next1(rng);
+                const float sx = next1(rng), sy = next1(rng);
+                V3 wi, bsdf;
+                sample_bsdf(sc, vndf, wo, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
+                if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
+                    const float NdotWI = fabsf(dot(it.normal, wi));
+                    T = T * bsdf * NdotWI / bsdfPdf;
+                    const V3 o = offset_ray_origin(it.position, it.geometryNormal, wi);
+                    pool.rayO[path] = make_float4(o.x, o.y, o.z, inf());
+                    pool.rayD[path] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+                    flags = (flags & 0xFFFFFF00u) | ((bounce + 1) & 0xFFu);
+                } else {
+                    flags |= kFlagTerminate;
+                    terminate = true;
+                }
+            }
+            thr.w = bsdfPdf;
+            li.w = isDelta ? 1.0f : 0.0f;
+        }
+        if (!hasShadow) flags = flags & ~kFlagShadowRayHit;
+        pool.flags[path] = flags;
+        pool.rng[path] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+        pool.throughput[path] = make_float4(T.x, T.y, T.z, thr.w);
+        pool.li[path] = make_float4(L.x, L.y, L.z, li.w);
+        pool.lsr[path] = make_float4(lsr.x, lsr.y, lsr.z, 0.0f);
+    }
+    const uint32_t es = block_append(active && !terminate, &cnt->ext, sm);
+    if (active && !terminate) pool.extQueue[es] = path;
+    const uint32_t ss = block_append(active && hasShadow, &cnt->shadow, sm);
+    if (active && hasShadow) pool.shadowQueue[ss] = path;
+    }
+}
+
+// ---- EXTENSION_RAY_CAST / SHADOW_RAY_CAST ----------------------------------------------
+template <bool INSTR>
+__global__ __launch_bounds__(256) void extension_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, const Counters* cnt,
+                                                         Globals* g, unsigned long long* instr)
+{
+    extern __shared__ uint32_t stackMem[];
+    const uint32_t n = cnt->ext;
+    uint32_t visits = 0, tris = 0, blas = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t path = pool.extQueue[i];
+        const float4 o = pool.rayO[path], d = pool.rayD[path];
+        HitRecord h;
+        h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.tri = 0u; h.inst = 0u;
+        TraversalStats st;
+        const bool hit = traverse_stats<false>(sc, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf(), fc->features,
+                                               stackMem + threadIdx.x, blockDim.x, &h, INSTR ? &st : nullptr);
+        pool.hit[path] = hit ? make_float4(h.t, h.u, h.v, asf(h.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
+        pool.hitInst[path] = hit ? h.inst : 0u;
+        if (INSTR) { visits += st.nodes; tris += st.tris; blas += st.blas; }
+    }
+    if (INSTR) {
+        const unsigned long long a = wave_sum(visits), b = wave_sum(tris), c = wave_sum(blas);
+        if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&instr[0], a); atomicAdd(&instr[1], b); atomicAdd(&instr[2], c); }
+    }
+    (void)g;
+}
+
+template <bool INSTR>
+__global__ __launch_bounds__(256) void shadow_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
+                                                      Counters* nextCnt, Globals* g, unsigned long long* instr)
+{
+    extern __shared__ uint32_t stackMem[];
+    const uint32_t n = cnt->shadow;
+    uint32_t visits = 0, tris = 0, blas = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t path = pool.shadowQueue[i];
+        const float4 o = pool.shadowO[path], d = pool.shadowD[path];
+        HitRecord h;
+        TraversalStats st;
+        const bool hit = traverse_stats<true>(sc, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, o.w, fc->features,
+                                              stackMem + threadIdx.x, blockDim.x, &h, INSTR ? &st : nullptr);
+        const uint32_t f = pool.flags[path];
+        pool.flags[path] = (hit ? kFlagShadowRayHit : 0u) | (f & 0xBFFFFFFFu);
+        if (INSTR) { visits += st.nodes; tris += st.tris; blas += st.blas; }
+    }
+    if (INSTR) {
+        const unsigned long long a = wave_sum(visits), b = wave_sum(tris), c = wave_sum(blas);
+        if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&instr[3], a); atomicAdd(&instr[4], b); atomicAdd(&instr[5], c); }
+    }
+    // End of the iteration: account and clear the other parity's counters.
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        g->extRays += cnt->ext;
+        g->shadowRays += cnt->shadow;
+        g->iterations += 1ull;
+        nextCnt->ext = 0u; nextCnt->shadow = 0u; nextCnt->material = 0u; nextCnt->newPath = 0u;
+    }
+}
+
+// ---- kernel-level batch entry points (tests / roofline) -----------------------------------
+template <bool ANY>
+__global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const dcrt_ray* rays, uint32_t n, uint32_t features,
+                                                           dcrt_ray_hit* hits, uint32_t* occluded, unsigned long long* instr)
+{
+    extern __shared__ uint32_t stackMem[];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t visits = 0, tris = 0, blas = 0;
+    if (i < n) {
+        const dcrt_ray r = rays[i];
+        HitRecord h;
+        h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.tri = 0u; h.inst = 0u;
+        TraversalStats st;
+        const bool hit = traverse_stats<ANY>(sc, ld3(r.origin), ld3(r.direction), 0.0f, ANY ? r.t_max : inf(), features,
+                                             stackMem + threadIdx.x, blockDim.x, &h, &st);
+        visits = st.nodes; tris = st.tris; blas = st.blas;
+        if (ANY) {
+            occluded[i] = hit ? 1u : 0u;
+        } else {
+            dcrt_ray_hit o;
+            o.t = hit ? h.t : inf(); o.u = hit ? h.u : 0.0f; o.v = hit ? h.v : 0.0f;
+            o.triangle_id = hit ? h.tri : 0u; o.instance_index = hit ? h.inst : 0u;
+            hits[i] = o;
+        }
+    }
+    if (instr) {
+        const unsigned long long a = wave_sum(visits), b = wave_sum(tris), c = wave_sum(blas);
+        if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&instr[0], a); atomicAdd(&instr[1], b); atomicAdd(&instr[2], c); }
+    }
+}
+
+__global__ void math_eval_kernel(int function, const float* x, uint32_t n, float* y)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    switch (function) {
+    case 0: y[i] = det_sin(x[i]); break;
+    case 1: y[i] = det_cos(x[i]); break;
+    case 2: y[i] = det_exp(x[i]); break;
+    default: y[i] = det_atan(x[i]); break;
+    }
+}
+
+// ---- SampleConvolution ----------------------------------------------------------------
+struct FilterConsts { float radius, gaussianAlpha, gaussianExp, mf[7]; uint32_t tau, kind; };
+
+__device__ __forceinline__ float filter_1d_sinc(float x) { x = fabsf(x); return x >= 1e-5f ? det_sin(3.1415926535f * x) / (3.1415926535f * x) : 1.0f; }
+__device__ __forceinline__ float evaluate_filter(const FilterConsts& c, float px, float py)
+{
+    const float r = c.radius;
+    switch (c.kind) {
+    case DCRT_FILTER_TRIANGLE: return fmaxf(0.0f, r - fabsf(px)) * fmaxf(0.0f, r - fabsf(py));
+    case DCRT_FILTER_GAUSSIAN: {
+        const float gx = fmaxf(0.0f, det_exp(-c.gaussianAlpha * px * px) - c.gaussianExp);
+        const float gy = fmaxf(0.0f, det_exp(-c.gaussianAlpha * py * py) - c.gaussianExp);
+        return gx * gy;
+    }
+    case DCRT_FILTER_MITCHELL: {
+        float v[2] = { px / c.radius, py / c.radius }, o[2];
+        for (int k = 0; k < 2; ++k) {
+            const float x = fabsf(2.0f * v[k]);
+            float m = x < 1.0f ? c.mf[4] * x * x * x + c.mf[5] * x * x + c.mf[6]
+                               : (x < 2.0f ? c.mf[0] * x * x * x + c.mf[1] * x * x + c.mf[2] * x + c.mf[3] : 0.0f);
+            o[k] = m * (1.0f / 6.0f);
+        }
+        return o[0] * o[1];
+    }
+    case DCRT_FILTER_LANCZOS: {
+        float o[2], v[2] = { px, py };
+        for (int k = 0; k < 2; ++k) {
+            const float x = fabsf(v[k]);
+            const float lanczos = filter_1d_sinc(x / (float)c.tau);
+            o[k] = x > r ? 0.0f : filter_1d_sinc(x) * lanczos;
+        }
+        return o[0] * o[1];
+    }
+    default: return (fabsf(px) <= r && fabsf(py) <= r) ? 1.0f : 0.0f;
+    }
+}
+
+__global__ void film_kernel(Film film, FilterConsts c, uint32_t worldSize, uint32_t rank, uint32_t stripeHeight)
+{
+    const uint32_t px = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t py = blockIdx.y * blockDim.y + threadIdx.y;
+    const uint32_t W = film.width, H = film.height;
+    if (px >= W || py >= H) return;
+    if (worldSize > 1 && (py / stripeHeight) % worldSize != rank) return;
+    const float r = c.radius;
+    const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
+    int xs = (int)floorf(cx - r); xs = xs < 0 ? 0 : xs;
+    int xe = (int)floorf(cx + r); xe = xe > (int)W - 1 ? (int)W - 1 : xe;
+    int ys = (int)floorf(cy - r); ys = ys < 0 ? 0 : ys;
+    int ye = (int)floorf(cy + r); ye = ye > (int)H - 1 ? (int)H - 1 : ye;
+    float wsum = 0.0f;
+    V3 sum = mk(0.0f, 0.0f, 0.0f);
+    for (int y = ys; y <= ye; ++y)
+        for (int x = xs; x <= xe; ++x) {
+            const size_t q = (size_t)y * W + x;
+            const float2 sp = film.samplePosition[q];
+            const float4 sv = film.sampleValue[q];
+            const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
+            sum = sum + mk(sv.x, sv.y, sv.z) * w;
+            wsum = wsum + w;
+        }
+    const size_t p = (size_t)py * W + px;
+    float4 v = film.accum[p];
+    v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
+    film.accum[p] = v;
+}
+
+// ---- BxDF LUT integration (BxDFTexturesBuilding.hlsl, "%f" defines) -------------------------
+__global__ void lut_integrate_kernel(int which, uint32_t texels, float* out)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= texels) return;
+    const float ix = 0.032258f;
+    const float iy = which == 0 ? 0.032258f : 0.066667f;
+    const float iz = which == 0 ? 1.0f : 0.133333f;
+    const float sz = which == 0 ? 0.0f : 1.0f;
+    const double weight = which == 2 ? 0.000010 : 0.000049;
+    const uint32_t batches = which == 2 ? 24u : 5u;
+    const uint32_t w = 32, h = which == 0 ? 32u : 16u;
+    const uint32_t slice = t / (w * h), rem = t % (w * h);
+    const uint32_t ty = rem / w, tx = rem % w;
+    const bool entering = slice >= 16;
+    const uint32_t tz = slice & 15u;
+    const float cosThetaO = fmaxf((float)tx * ix, 0.0001f);
+    const float alpha = (float)ty * iy;
+    const float ior = (float)tz * iz + sz;
+    const bool smooth = alpha < 0.00052441f;
+    float acc = 0.0f;
+    for (uint32_t batch = 0; batch < batches; ++batch) {
+        Rng rng = rng_init(0, 0, batch);
+        double result = batch == 0 ? 0.0 : (double)acc;
+        for (uint32_t i = 0; i < 4096; ++i) {
+            const V3 wo = mk(sqrtf(1.0f - cosThetaO * cosThetaO), 0.0f, cosThetaO);
+            V3 wi = mk(0.0f, 0.0f, 0.0f);
+            LCtx c; c.H = mk(0.0f, 0.0f, 0.0f); c.WOdotH = 0.0f;
+            float value = 0.0f, pdf = 0.0f;
+            if (which != 2) {
+                if (smooth) {
+                    wi = specular_brdf_sample(wo, &value, &pdf, c);
+                } else {
+                    const float sx = next1(rng), sy = next1(rng);
+                    const V3 m = sample_vndf(wo, sx, sy, alpha);
+                    wi = -reflect(wo, m);
+                    c.H = m; c.WOdotH = dot(m, wo);
+                    value = ct_brdf(wi, wo, alpha, c);
+                    pdf = ct_brdf_pdf(true, wi, wo, alpha, c);
+                }
+                if (pdf > 0.0f) {
+                    if (which == 1) {
+                        const float etaO = entering ? ior : 1.0f, etaI = entering ? 1.0f : ior;
+                        value = value * fresnel_dielectric(c.WOdotH, etaO, etaI);
+                    }
+                    result += weight * (double)value * (double)fabsf(wi.z) / (double)pdf;
+                }
+            } else {
+                const float etaO = entering ? ior : 1.0f, etaI = entering ? 1.0f : ior;
+                const float sel = next1(rng);
+                if (smooth) {
+                    wi = specular_bsdf_sample<true>(wo, sel, etaO, etaI, false, &value, &pdf, c);
+                } else {
+                    const float sx = next1(rng), sy = next1(rng);
+                    wi = ct_bsdf_sample(true, wo, sel, sx, sy, alpha, etaO, etaI, c);
+                    value = ct_bsdf<true>(wi, wo, alpha, etaO, etaI);
+                    pdf = ct_bsdf_pdf(true, wi, wo, alpha, etaO, etaI);
+                }
+                if (pdf > 0.0f) result += weight * (double)value * (double)fabsf(wi.z) / (double)pdf;
+            }
+        }
+        acc = (float)result;
+    }
+    out[t] = acc;
+}
+
+__device__ __forceinline__ uint16_t to_unorm16(float f) { return (uint16_t)rintf(saturate(f) * 65535.0f); }
+__device__ __forceinline__ float average_row(const float* row)
+{
+    const uint32_t n = 31;
+    const double fa = (double)(row[0] * 0.0001f);
+    double sum = 0.0;
+    for (uint32_t i = 1; i < n; ++i) {
+        const double cosTheta = (double)((float)i * 0.032258f);
+        sum += (double)saturate(row[i]) * cosTheta;
+    }
+    const double fb = (double)row[n];
+    const double result = (sum + (fa + fb) * 0.5) * (double)(1.0f / (float)n);
+    return (float)(result * 2.0);
+}
+__global__ void lut_finalize_kernel(const float* brdf, const float* brdfd, const float* bsdf, dcrt_bxdf_luts* L)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < DCRT_LUT_BRDF_COUNT) L->brdf[t] = to_unorm16(brdf[t]);
+    if (t < DCRT_LUT_BRDF_DIELECTRIC_COUNT) { L->brdf_dielectric[t] = to_unorm16(brdfd[t]); L->bsdf[t] = to_unorm16(bsdf[t]); }
+    if (t < 32) L->brdf_avg[t] = to_unorm16(average_row(brdf + t * 32));
+    if (t < 512) {
+        const uint32_t z = t / 16, y = t % 16;
+        const uint32_t dest = (z / 16) * 256 + (z % 16) * 16 + y;
+        L->brdf_dielectric_avg[dest] = to_unorm16(average_row(brdfd + (size_t)z * 512 + y * 32));
+        L->bsdf_avg[dest] = to_unorm16(average_row(bsdf + (size_t)z * 512 + y * 32));
+    }
+}
+
+// ---- explicit instantiations used by tracer.hip ---------------------------------------
+template __global__ void extension_kernel<false>(PathPool, DeviceScene, const FrameConstants*, const Counters*, Globals*, unsigned long long*);
+template __global__ void extension_kernel<true>(PathPool, DeviceScene, const FrameConstants*, const Counters*, Globals*, unsigned long long*);
+template __global__ void shadow_kernel<false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void shadow_kernel<true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void batch_trace_kernel<false>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
+template __global__ void batch_trace_kernel<true>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
+
+}  // namespace dev
+}  // namespace dcrt

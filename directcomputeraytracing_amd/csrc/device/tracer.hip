@@ -1,0 +1,918 @@
+// tracer.hip -- CWavefrontPathTracer on MI355X: pool allocation, scene upload,
+// the per-iteration launch sequence (captured into a hipGraph), image
+// completion, film accumulation, and the extern "C" tracer API of dcrt.h.
+// Reference: Source/WavefrontPathTracer.cpp:70-1162, Source/Scene.cpp:273-608,
+// Source/SampleConvolution.cpp:89-170, Source/BxDFTexturesBuilding.cpp:106-475.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../../include/dcrt.h"
+#include "kernels_impl.h"
+
+namespace dcrt {
+void SetLastError(const std::string& s);
+}
+using dcrt::SetLastError;
+using namespace dcrt::dev;
+
+#define HIPCHECK(expr)                                                                              \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess) {                                                                     \
+            SetLastError(std::string(#expr) + " failed: " + hipGetErrorString(e_));                 \
+            return DCRT_E_HIP;                                                                      \
+        }                                                                                           \
+    } while (0)
+#define CHECKED(expr)                      \
+    do {                                   \
+        const int r_ = (expr);             \
+        if (r_ != DCRT_OK) return r_;      \
+    } while (0)
+
+namespace {
+
+constexpr uint32_t kDefaultPoolSize = 1u << 20;      // 2^20 slots: 16 waves x 256 CUs x 256 (MI355X)
+constexpr uint32_t kDefaultIterations = 8;
+constexpr uint32_t kControlBlock = 256;
+constexpr uint32_t kMaterialBlock = 256;
+constexpr uint32_t kMaxPersistentBlocks = 256 * 8;   // CUs x resident workgroups
+
+template <typename T>
+int DeviceAlloc(T** p, size_t count, std::vector<void*>* owner)
+{
+    *p = nullptr;
+    if (count == 0) count = 1;
+    void* q = nullptr;
+    HIPCHECK(hipMalloc(&q, count * sizeof(T)));
+    *p = (T*)q;
+    if (owner) owner->push_back(q);
+    return DCRT_OK;
+}
+void FreeAll(std::vector<void*>* v)
+{
+    for (void* p : *v) (void)hipFree(p);
+    v->clear();
+}
+
+FilterConsts MakeFilter(const dcrt_filter_params& p)   // SampleConvolution.cpp:100-130
+{
+    FilterConsts c;
+    std::memset(&c, 0, sizeof(c));
+    c.kind = p.filter;
+    c.radius = p.radius;
+    if (p.filter == DCRT_FILTER_GAUSSIAN) {
+        c.gaussianAlpha = p.gaussian_alpha;
+        c.gaussianExp = std::exp(-p.gaussian_alpha * p.radius * p.radius);
+    } else if (p.filter == DCRT_FILTER_MITCHELL) {
+        const float B = p.mitchell_b, C = p.mitchell_c;
+        c.mf[0] = -B - 6 * C; c.mf[1] = 6 * B + 30 * C; c.mf[2] = -12 * B - 48 * C; c.mf[3] = 8 * B + 24 * C;
+        c.mf[4] = 12 - 9 * B - 6 * C; c.mf[5] = -18 + 12 * B + 6 * C; c.mf[6] = 6 - 2 * B;
+    } else if (p.filter == DCRT_FILTER_LANCZOS) {
+        c.tau = p.lanczos_tau ? p.lanczos_tau : 3;
+    }
+    return c;
+}
+
+}  // namespace
+
+struct dcrt_tracer {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool ownsStream = false;
+    uint32_t poolSize = 0;
+    uint32_t iterationsPerRender = kDefaultIterations;
+    bool debugRng = false;
+
+    std::vector<void*> poolAllocs, sceneAllocs, filmAllocs;
+    PathPool pool{};
+    DeviceScene scene{};
+    bool hasScene = false;
+    uint32_t castBlock = 256;
+    size_t castLds = 0;
+
+    dcrt_bxdf_luts* dLuts = nullptr;
+    Film film{};
+    uint32_t filmW = 0, filmH = 0;
+    uint32_t* dBands = nullptr;
+    uint32_t bandCount = 0;
+    dcrt_film_partition partition{ 1, 0, 64, 0 };
+
+    dcrt_frame_params frame{};
+    bool hasFrame = false;
+    FrameConstants* dFrame = nullptr;
+    Counters* dCounters = nullptr;     // [2]
+    Globals* dGlobals = nullptr;
+    unsigned long long* dInstr = nullptr;   // [8]
+    Counters* hCounters = nullptr;     // pinned [2]
+
+    bool newImage = true;
+    bool imageComplete = false;
+    bool filmClearTrigger = false;
+    uint32_t parity = 0;
+
+    // graph of `graphIters` iterations (even), rebuilt when launch parameters change
+    hipGraphExec_t graphExec = nullptr;
+    uint32_t graphIters = 0;
+    bool graphValid = false;
+    bool instrCounters = false;
+    bool extTiming = false;
+    std::vector<hipEvent_t> events;
+    size_t eventsUsed = 0;
+    double extMs = 0.0;
+    uint64_t extLaunches = 0;
+
+    ~dcrt_tracer();
+    int Create(const dcrt_tracer_config& cfg);
+    int BuildLuts();
+    int UploadScene(const dcrt_flat_scene& s);
+    int SetFrame(const dcrt_frame_params& p);
+    int SetPartition(const dcrt_film_partition& p);
+    int EnsureFilm(uint32_t w, uint32_t h);
+    int BuildBands();
+    int BeginImage();
+    int LaunchIteration(uint32_t par, bool timed);
+    int RunIterations(uint32_t n);
+    int ReadCompletion(bool* complete);
+    int Render(uint32_t maxIterations);
+    int RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_filter_params& filter);
+    int Accumulate(const dcrt_filter_params& filter);
+    void InvalidateGraph()
+    {
+        if (graphExec) (void)hipGraphExecDestroy(graphExec);
+        graphExec = nullptr;
+        graphValid = false;
+    }
+    uint32_t CastGrid(uint32_t block) const { return std::min<uint32_t>((poolSize + block - 1) / block, kMaxPersistentBlocks * (256 / block)); }
+};
+
+dcrt_tracer::~dcrt_tracer()
+{
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    InvalidateGraph();
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+    FreeAll(&poolAllocs);
+    FreeAll(&sceneAllocs);
+    FreeAll(&filmAllocs);
+    if (hCounters) (void)hipHostFree(hCounters);
+    if (ownsStream && stream) (void)hipStreamDestroy(stream);
+}
+
+int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
+{
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        SetLastError("no HIP device visible");
+        return DCRT_E_NO_DEVICE;
+    }
+    device = cfg.device;
+    if (device < 0 || device >= count) { SetLastError("invalid device ordinal"); return DCRT_E_INVALID_ARG; }
+    HIPCHECK(hipSetDevice(device));
+    if (cfg.stream) {
+        stream = (hipStream_t)cfg.stream;
+    } else {
+        HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        ownsStream = true;
+    }
+    poolSize = cfg.path_pool_size ? cfg.path_pool_size : kDefaultPoolSize;
+    poolSize = (poolSize + 255u) & ~255u;   // whole 256-thread workgroups of whole waves
+    iterationsPerRender = cfg.iterations_per_render ? cfg.iterations_per_render : kDefaultIterations;
+    debugRng = cfg.debug_rng != 0;
+    // WavefrontPathTracer.cpp:120-264 (SoA instead of AoS)
+    const size_t P = poolSize;
+    CHECKED(DeviceAlloc(&pool.rayO, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.rayD, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.hit, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.hitInst, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.shadowO, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.shadowD, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.pixel, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.pixelSample, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.rng, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.lsr, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.throughput, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.li, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.extQueue, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.shadowQueue, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.materialQueue, P, &poolAllocs));
+    pool.size = poolSize;
+    CHECKED(DeviceAlloc(&dFrame, 1, &poolAllocs));
+    CHECKED(DeviceAlloc(&dCounters, 2, &poolAllocs));
+    CHECKED(DeviceAlloc(&dGlobals, 1, &poolAllocs));
+    CHECKED(DeviceAlloc(&dInstr, 8, &poolAllocs));
+    CHECKED(DeviceAlloc(&dLuts, 1, &poolAllocs));
+    HIPCHECK(hipMemsetAsync(dCounters, 0, 2 * sizeof(Counters), stream));
+    HIPCHECK(hipMemsetAsync(dGlobals, 0, sizeof(Globals), stream));
+    HIPCHECK(hipMemsetAsync(dInstr, 0, 8 * sizeof(unsigned long long), stream));
+    HIPCHECK(hipHostMalloc((void**)&hCounters, 2 * sizeof(Counters), hipHostMallocDefault));
+    CHECKED(BuildLuts());
+    HIPCHECK(hipStreamSynchronize(stream));
+    return DCRT_OK;
+}
+
+// BxDFTexturesBuilding::Build (BxDFTexturesBuilding.cpp:106-475) as three
+// integration launches + one conversion/average launch.
+int dcrt_tracer::BuildLuts()
+{
+    std::vector<void*> tmp;
+    float *brdf = nullptr, *brdfd = nullptr, *bsdf = nullptr;
+    CHECKED(DeviceAlloc(&brdf, DCRT_LUT_BRDF_COUNT, &tmp));
+    CHECKED(DeviceAlloc(&brdfd, DCRT_LUT_BRDF_DIELECTRIC_COUNT, &tmp));
+    CHECKED(DeviceAlloc(&bsdf, DCRT_LUT_BSDF_COUNT, &tmp));
+    hipLaunchKernelGGL(lut_integrate_kernel, dim3((DCRT_LUT_BRDF_COUNT + 63) / 64), dim3(64), 0, stream, 0, (uint32_t)DCRT_LUT_BRDF_COUNT, brdf);
+    hipLaunchKernelGGL(lut_integrate_kernel, dim3((DCRT_LUT_BRDF_DIELECTRIC_COUNT + 63) / 64), dim3(64), 0, stream, 1,
+                       (uint32_t)DCRT_LUT_BRDF_DIELECTRIC_COUNT, brdfd);
+    hipLaunchKernelGGL(lut_integrate_kernel, dim3((DCRT_LUT_BSDF_COUNT + 63) / 64), dim3(64), 0, stream, 2, (uint32_t)DCRT_LUT_BSDF_COUNT, bsdf);
+    hipLaunchKernelGGL(lut_finalize_kernel, dim3((DCRT_LUT_BRDF_DIELECTRIC_COUNT + 255) / 256), dim3(256), 0, stream, brdf, brdfd, bsdf, dLuts);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(stream));
+    FreeAll(&tmp);
+    return DCRT_OK;
+}
+
+int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
+{
+    if (!s.vertices || !s.triangles || !s.bvh_nodes || !s.material_ids || !s.instance_transforms || !s.materials ||
+        !s.instance_light_indices || !s.instance_flags || !s.instance_material_overrides || s.triangle_count == 0 ||
+        s.bvh_node_count == 0 || s.instance_count == 0 || s.material_count == 0) {
+        SetLastError("incomplete flat scene");
+        return DCRT_E_INVALID_ARG;
+    }
+    if (s.light_count > DCRT_MAX_LIGHT_COUNT) { SetLastError("more than 5000 lights"); return DCRT_E_LIMIT; }
+    HIPCHECK(hipStreamSynchronize(stream));
+    InvalidateGraph();
+    FreeAll(&sceneAllocs);
+    hasScene = false;
+    DeviceScene d{};
+    auto upload = [&](auto** dst, const auto* src, size_t count) -> int {
+        using T = std::remove_const_t<std::remove_pointer_t<decltype(src)>>;
+        T* p = nullptr;
+        CHECKED(DeviceAlloc(&p, count, &sceneAllocs));
+        if (count && src) HIPCHECK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, stream));
+        *dst = p;
+        return DCRT_OK;
+    };
+    dcrt_vertex* vtx = nullptr;
+    uint32_t* tris = nullptr;
+    dcrt_bvh_node* nodes = nullptr;
+    dcrt_float4x3* xf = nullptr;
+    CHECKED(upload(&vtx, s.vertices, s.vertex_count));
+    CHECKED(upload(&tris, s.triangles, (size_t)s.triangle_count * 3));
+    CHECKED(upload(&nodes, s.bvh_nodes, s.bvh_node_count));
+    uint32_t* mids = nullptr; uint32_t* lidx = nullptr; uint32_t* iflags = nullptr; uint32_t* ovr = nullptr;
+    dcrt_material* mats = nullptr; dcrt_light* lights = nullptr;
+    CHECKED(upload(&mids, s.material_ids, s.triangle_count));
+    CHECKED(upload(&xf, s.instance_transforms, (size_t)s.instance_count * 2));
+    CHECKED(upload(&lidx, s.instance_light_indices, s.instance_count));
+    CHECKED(upload(&iflags, s.instance_flags, s.instance_count));
+    CHECKED(upload(&ovr, s.instance_material_overrides, s.instance_count));
+    CHECKED(upload(&mats, s.materials, s.material_count));
+    CHECKED(upload(&lights, s.lights, std::max<uint32_t>(s.light_count, 1)));
+    float4* triVerts = nullptr;
+    CHECKED(DeviceAlloc(&triVerts, (size_t)s.triangle_count * 3, &sceneAllocs));
+    hipLaunchKernelGGL(build_tri_verts_kernel, dim3((s.triangle_count + 255) / 256), dim3(256), 0, stream, vtx, tris, s.triangle_count, triVerts);
+    HIPCHECK(hipGetLastError());
+    // textures: one texel blob + descriptors (Scene.cpp:586-608)
+    std::vector<TextureDesc> descs(std::max<uint32_t>(s.texture_count, 1));
+    std::vector<uint8_t> blob;
+    for (uint32_t i = 0; i < s.texture_count; ++i) {
+        const dcrt_texture& t = s.textures[i];
+        TextureDesc& td = descs[i];
+        const size_t bpp = t.format == DCRT_TEXTURE_FORMAT_R8_UNORM ? 1 : 4;
+        td.width = t.pixels ? t.width : 0; td.height = t.pixels ? t.height : 0; td.format = t.format;
+        td.offset = (uint32_t)blob.size();
+        if (t.pixels) blob.insert(blob.end(), t.pixels, t.pixels + (size_t)t.width * t.height * bpp);
+        while (blob.size() % 4) blob.push_back(0);
+    }
+    if (blob.empty()) blob.resize(4, 0);
+    TextureDesc* dDescs = nullptr; uint8_t* dBlob = nullptr; float* dSrgb = nullptr;
+    CHECKED(upload(&dDescs, descs.data(), descs.size()));
+    CHECKED(upload(&dBlob, blob.data(), blob.size()));
+    float srgb[256];
+    for (int i = 0; i < 256; ++i) {
+        const double c = i / 255.0;
+        srgb[i] = (float)(c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4));
+    }
+    CHECKED(upload(&dSrgb, srgb, 256));
+    float* dEnv = nullptr;
+    if (s.env_cube_rgb && s.env_cube_size) CHECKED(upload(&dEnv, s.env_cube_rgb, (size_t)6 * s.env_cube_size * s.env_cube_size * 3));
+    d.nodes = (const float4*)nodes;
+    d.triVerts = triVerts;
+    d.vertices = vtx;
+    d.triangles = tris;
+    d.materialIds = mids;
+    d.transforms = (const float4*)xf;
+    d.instanceLightIndices = lidx;
+    d.instanceFlags = iflags;
+    d.overrides = ovr;
+    d.materials = mats;
+    d.lights = lights;
+    d.textures = dDescs;
+    d.texels = dBlob;
+    d.srgbTable = dSrgb;
+    d.envCube = dEnv;
+    d.envCubeSize = dEnv ? s.env_cube_size : 0;
+    d.lutBrdf = dLuts->brdf;
+    d.lutBrdfAvg = dLuts->brdf_avg;
+    d.lutBrdfDielectric = dLuts->brdf_dielectric;
+    d.lutBrdfDielectricAvg = dLuts->brdf_dielectric_avg;
+    d.lutBsdf = dLuts->bsdf;
+    d.lutBsdfAvg = dLuts->bsdf_avg;
+    d.instanceCount = s.instance_count;
+    d.nodeCount = s.bvh_node_count;
+    d.triangleCount = s.triangle_count;
+    d.stackSize = std::max<uint32_t>(s.bvh_traversal_stack_size, 1u);
+    scene = d;
+    // LDS stack: [stackSize][block] u32; keep a workgroup's stack <= 32 KiB
+    castBlock = 256;
+    while (castBlock > 64 && (size_t)d.stackSize * castBlock * 4 > 32768) castBlock >>= 1;
+    castLds = (size_t)d.stackSize * castBlock * 4;
+    if (castLds > 65536) { SetLastError("BVH traversal stack too deep for LDS"); return DCRT_E_LIMIT; }
+    HIPCHECK(hipStreamSynchronize(stream));
+    hasScene = true;
+    newImage = true;
+    return DCRT_OK;
+}
+
+int dcrt_tracer::EnsureFilm(uint32_t w, uint32_t h)
+{
+    if (w == filmW && h == filmH && film.accum) return DCRT_OK;
+    if (w == 0 || h == 0 || w > 65535 || h > 65535) { SetLastError("invalid film resolution"); return DCRT_E_INVALID_ARG; }
+    HIPCHECK(hipStreamSynchronize(stream));
+    InvalidateGraph();
+    FreeAll(&filmAllocs);
+    const size_t n = (size_t)w * h;
+    CHECKED(DeviceAlloc(&film.samplePosition, n, &filmAllocs));
+    CHECKED(DeviceAlloc(&film.sampleValue, n, &filmAllocs));
+    CHECKED(DeviceAlloc(&film.accum, n, &filmAllocs));
+    film.debugRng = nullptr;
+    if (debugRng) CHECKED(DeviceAlloc(&film.debugRng, n, &filmAllocs));
+    HIPCHECK(hipMemsetAsync(film.samplePosition, 0, n * sizeof(float2), stream));
+    HIPCHECK(hipMemsetAsync(film.sampleValue, 0, n * sizeof(float4), stream));
+    HIPCHECK(hipMemsetAsync(film.accum, 0, n * sizeof(float4), stream));
+    if (film.debugRng) HIPCHECK(hipMemsetAsync(film.debugRng, 0, n * sizeof(uint4), stream));
+    filmW = w; filmH = h;
+    film.width = w; film.height = h;
+    return BuildBands();
+}
+
+// 8-row bands this tracer renders: its stripes plus `halo` rows either side
+// (a band may be shorter than 8 rows at a halo edge; its missing rows are clipped).
+int dcrt_tracer::BuildBands()
+{
+    std::vector<uint32_t> bands;
+    const uint32_t H = filmH;
+    if (partition.world_size <= 1) {
+        for (uint32_t y = 0; y < H; y += kBlockH) bands.push_back(y);
+    } else {
+        const uint32_t S = partition.stripe_height, halo = partition.halo_rows ? partition.halo_rows : 2u;
+        std::vector<uint8_t> need(H, 0);
+        for (uint32_t y = 0; y < H; ++y) {
+            if ((y / S) % partition.world_size != partition.rank) continue;
+            const uint32_t lo = y >= halo ? y - halo : 0, hi = std::min(H - 1, y + halo);
+            for (uint32_t k = lo; k <= hi; ++k) need[k] = 1;
+        }
+        // one band per aligned 8-row group that contains a needed row
+        for (uint32_t y = 0; y < H; y += kBlockH) {
+            bool any = false;
+            for (uint32_t k = y; k < std::min(H, y + kBlockH); ++k) any = any || need[k];
+            if (any) bands.push_back(y);
+        }
+    }
+    if (bands.empty()) bands.push_back(0);
+    bandCount = (uint32_t)bands.size();
+    uint32_t* p = nullptr;
+    CHECKED(DeviceAlloc(&p, bands.size(), &filmAllocs));
+    HIPCHECK(hipMemcpyAsync(p, bands.data(), bands.size() * 4, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    dBands = p;
+    film.bandY = p;
+    return DCRT_OK;
+}
+
+int dcrt_tracer::SetFrame(const dcrt_frame_params& p)
+{
+    if (p.resolution[0] == 0 || p.resolution[1] == 0 || p.max_bounce_count > DCRT_MAX_RAY_BOUNCE) {
+        SetLastError("invalid frame parameters");
+        return DCRT_E_INVALID_ARG;
+    }
+    CHECKED(EnsureFilm(p.resolution[0], p.resolution[1]));
+    frame = p;
+    hasFrame = true;
+    return DCRT_OK;
+}
+
+int dcrt_tracer::SetPartition(const dcrt_film_partition& p)
+{
+    if (p.world_size == 0 || p.rank >= p.world_size || (p.world_size > 1 && (p.stripe_height == 0 || p.stripe_height % kBlockH))) {
+        SetLastError("invalid film partition");
+        return DCRT_E_INVALID_ARG;
+    }
+    partition = p;
+    if (filmW) {
+        HIPCHECK(hipStreamSynchronize(stream));
+        InvalidateGraph();
+        CHECKED(BuildBands());
+    }
+    newImage = true;
+    return DCRT_OK;
+}
+
+// ResetImage + SET_IDLE + constant upload for one image (WavefrontPathTracer.cpp:441-468)
+int dcrt_tracer::BeginImage()
+{
+    FrameConstants fc;
+    std::memset(&fc, 0, sizeof(fc));
+    std::memcpy(fc.camera, frame.camera_transform, sizeof(fc.camera));
+    fc.resolution[0] = frame.resolution[0]; fc.resolution[1] = frame.resolution[1];
+    fc.filmSize[0] = frame.film_size[0]; fc.filmSize[1] = frame.film_size[1];
+    fc.apertureRadius = frame.aperture_radius;
+    fc.focalDistance = frame.focal_distance;
+    fc.filmDistance = frame.film_distance;
+    fc.bladeCount = frame.blade_count;
+    fc.bladeVertexPos[0] = frame.blade_vertex_pos[0]; fc.bladeVertexPos[1] = frame.blade_vertex_pos[1];
+    fc.apertureBaseAngle = frame.aperture_base_angle;
+    fc.frameSeed = frame.frame_seed;
+    fc.maxBounce = frame.max_bounce_count;
+    fc.lightCount = frame.light_count;
+    fc.envLightIndex = frame.environment_light_index;
+    fc.features = frame.features;
+    fc.blocksX = (frame.resolution[0] + kBlockW - 1) / kBlockW;
+    fc.bandCount = bandCount;
+    hipLaunchKernelGGL(set_frame_kernel, dim3(1), dim3(1), 0, stream, dFrame, fc);
+    const uint32_t total = fc.blocksX * bandCount;
+    hipLaunchKernelGGL(set_idle_kernel, dim3((poolSize + 255) / 256), dim3(256), 0, stream, pool, dCounters, dGlobals, total);
+    HIPCHECK(hipGetLastError());
+    parity = 0;
+    newImage = false;
+    imageComplete = false;
+    return DCRT_OK;
+}
+
+// RenderOneIteration (WavefrontPathTracer.cpp:622-1162): CONTROL(+NEW_PATH) ->
+// MATERIAL -> EXTENSION_RAY_CAST -> SHADOW_RAY_CAST. Queue sizes are read on the
+// device, so no indirect-argument pass and no host round trip is needed.
+int dcrt_tracer::LaunchIteration(uint32_t par, bool timed)
+{
+    Counters* cnt = dCounters + par;
+    Counters* next = dCounters + (par ^ 1u);
+    const uint32_t controlGrid = std::min<uint32_t>(poolSize / kControlBlock, kMaxPersistentBlocks);
+    const uint32_t materialGrid = std::min<uint32_t>((poolSize + kMaterialBlock - 1) / kMaterialBlock, kMaxPersistentBlocks);
+    const uint32_t castGrid = CastGrid(castBlock);
+    hipLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, pool, film, (const FrameConstants*)dFrame, cnt,
+                       dGlobals, (uint32_t)(film.debugRng != nullptr));
+    hipLaunchKernelGGL(material_kernel, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timed) {
+        while (events.size() < eventsUsed + 2) {
+            hipEvent_t e;
+            HIPCHECK(hipEventCreate(&e));
+            events.push_back(e);
+        }
+        e0 = events[eventsUsed++];
+        e1 = events[eventsUsed++];
+        HIPCHECK(hipEventRecord(e0, stream));
+    }
+    if (instrCounters)
+        hipLaunchKernelGGL(extension_kernel<true>, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame,
+                           (const Counters*)cnt, dGlobals, dInstr);
+    else
+        hipLaunchKernelGGL(extension_kernel<false>, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame,
+                           (const Counters*)cnt, dGlobals, dInstr);
+    if (timed) HIPCHECK(hipEventRecord(e1, stream));
+    if (instrCounters)
+        hipLaunchKernelGGL(shadow_kernel<true>, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
+                           next, dGlobals, dInstr);
+    else
+        hipLaunchKernelGGL(shadow_kernel<false>, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
+                           next, dGlobals, dInstr);
+    HIPCHECK(hipGetLastError());
+    return DCRT_OK;
+}
+
+// n iterations; when n is even and event timing is off they replay a captured graph.
+int dcrt_tracer::RunIterations(uint32_t n)
+{
+    if (extTiming) {
+        for (uint32_t i = 0; i < n; ++i) {
+            CHECKED(LaunchIteration(parity, true));
+            parity ^= 1u;
+        }
+        return DCRT_OK;
+    }
+    while (n >= 2) {
+        const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
+        if (n >= chunk) {
+            if (!graphValid || graphIters != chunk) {
+                InvalidateGraph();
+                hipGraph_t g = nullptr;
+                HIPCHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+                int rc = DCRT_OK;
+                for (uint32_t i = 0; i < chunk && rc == DCRT_OK; ++i) rc = LaunchIteration(i & 1u, false);
+                hipError_t ec = hipStreamEndCapture(stream, &g);
+                if (rc != DCRT_OK) return rc;
+                HIPCHECK(ec);
+                HIPCHECK(hipGraphInstantiate(&graphExec, g, nullptr, nullptr, 0));
+                (void)hipGraphDestroy(g);
+                graphIters = chunk;
+                graphValid = true;
+            }
+            if (parity != 0) {   // keep the graph's parity pattern aligned
+                CHECKED(LaunchIteration(parity, false));
+                parity ^= 1u;
+                --n;
+                continue;
+            }
+            HIPCHECK(hipGraphLaunch(graphExec, stream));
+            n -= chunk;
+        } else {
+            CHECKED(LaunchIteration(parity, false));
+            parity ^= 1u;
+            --n;
+        }
+    }
+    while (n > 0) {
+        CHECKED(LaunchIteration(parity, false));
+        parity ^= 1u;
+        --n;
+    }
+    return DCRT_OK;
+}
+
+// IsImageComplete (WavefrontPathTracer.cpp:508-523): the material and new-path
+// queues of the last CONTROL pass were both empty. Here exact, not 2 frames late.
+int dcrt_tracer::ReadCompletion(bool* complete)
+{
+    const uint32_t last = parity ^ 1u;
+    HIPCHECK(hipMemcpyAsync(hCounters, dCounters + last, sizeof(Counters), hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    *complete = hCounters->material == 0 && hCounters->ext == 0;
+    return DCRT_OK;
+}
+
+int dcrt_tracer::Render(uint32_t maxIterations)
+{
+    if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
+    if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
+    if (newImage) CHECKED(BeginImage());
+    CHECKED(RunIterations(maxIterations ? maxIterations : iterationsPerRender));
+    bool complete = false;
+    CHECKED(ReadCompletion(&complete));
+    imageComplete = complete;
+    newImage = complete;   // WavefrontPathTracer.cpp:500
+    return DCRT_OK;
+}
+
+int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
+{
+    if (!film.accum) { SetLastError("no film"); return DCRT_E_INVALID_ARG; }
+    const FilterConsts c = MakeFilter(f);
+    const dim3 block(16, 16), grid((filmW + 15) / 16, (filmH + 15) / 16);
+    hipLaunchKernelGGL(film_kernel, grid, block, 0, stream, film, c, partition.world_size, partition.rank,
+                       std::max<uint32_t>(partition.stripe_height, 1));
+    HIPCHECK(hipGetLastError());
+    return DCRT_OK;
+}
+
+int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_filter_params& filter)
+{
+    if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
+    if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
+    const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
+    for (uint32_t img = 0; img < count; ++img) {
+        frame.frame_seed = firstSeed + img;
+        CHECKED(BeginImage());
+        for (uint32_t guard = 0;; ++guard) {
+            CHECKED(RunIterations(chunk));
+            bool complete = false;
+            CHECKED(ReadCompletion(&complete));
+            if (complete) break;
+            if (guard > 100000) { SetLastError("image did not complete"); return DCRT_E_LIMIT; }
+        }
+        CHECKED(Accumulate(filter));
+    }
+    imageComplete = true;
+    newImage = true;
+    HIPCHECK(hipStreamSynchronize(stream));
+    return DCRT_OK;
+}
+
+// ============================ C ABI ========================================
+#define TRACER_GUARD(t)                                         \
+    if (!(t)) return DCRT_E_INVALID_ARG;                        \
+    if (hipSetDevice((t)->device) != hipSuccess) {              \
+        SetLastError("hipSetDevice failed");                    \
+        return DCRT_E_HIP;                                      \
+    }
+
+extern "C" {
+
+DCRT_API int dcrt_device_count(int* out)
+{
+    if (!out) return DCRT_E_INVALID_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_create(const dcrt_tracer_config* config, dcrt_tracer** out)
+{
+    if (!out) return DCRT_E_INVALID_ARG;
+    *out = nullptr;
+    dcrt_tracer_config cfg{};
+    if (config) cfg = *config;
+    dcrt_tracer* t = new (std::nothrow) dcrt_tracer();
+    if (!t) return DCRT_E_LIMIT;
+    const int rc = t->Create(cfg);
+    if (rc != DCRT_OK) { delete t; return rc; }
+    *out = t;
+    return DCRT_OK;
+}
+
+DCRT_API void dcrt_tracer_destroy(dcrt_tracer* t) { delete t; }
+
+DCRT_API int dcrt_tracer_upload_scene(dcrt_tracer* t, const dcrt_flat_scene* s)
+{
+    TRACER_GUARD(t);
+    if (!s) return DCRT_E_INVALID_ARG;
+    return t->UploadScene(*s);
+}
+
+DCRT_API int dcrt_tracer_set_frame_params(dcrt_tracer* t, const dcrt_frame_params* p)
+{
+    TRACER_GUARD(t);
+    if (!p) return DCRT_E_INVALID_ARG;
+    return t->SetFrame(*p);
+}
+
+DCRT_API int dcrt_tracer_set_film_partition(dcrt_tracer* t, const dcrt_film_partition* p)
+{
+    TRACER_GUARD(t);
+    if (!p) return DCRT_E_INVALID_ARG;
+    return t->SetPartition(*p);
+}
+
+DCRT_API int dcrt_tracer_render(dcrt_tracer* t, uint32_t max_iterations)
+{
+    TRACER_GUARD(t);
+    return t->Render(max_iterations);
+}
+
+DCRT_API int dcrt_tracer_render_images(dcrt_tracer* t, uint32_t first_seed, uint32_t count, const dcrt_filter_params* f)
+{
+    TRACER_GUARD(t);
+    if (!f) return DCRT_E_INVALID_ARG;
+    return t->RenderImages(first_seed, count, *f);
+}
+
+DCRT_API int dcrt_tracer_reset_image(dcrt_tracer* t)
+{
+    TRACER_GUARD(t);
+    t->newImage = true;
+    t->imageComplete = false;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_is_image_complete(dcrt_tracer* t, int* out)
+{
+    TRACER_GUARD(t);
+    if (!out) return DCRT_E_INVALID_ARG;
+    *out = t->imageComplete ? 1 : 0;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_acquire_film_clear_trigger(dcrt_tracer* t, int* out)
+{
+    TRACER_GUARD(t);
+    if (!out) return DCRT_E_INVALID_ARG;
+    *out = t->filmClearTrigger ? 1 : 0;
+    t->filmClearTrigger = false;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_clear_film(dcrt_tracer* t)
+{
+    TRACER_GUARD(t);
+    if (!t->film.accum) return DCRT_E_INVALID_ARG;
+    HIPCHECK(hipMemsetAsync(t->film.accum, 0, (size_t)t->filmW * t->filmH * sizeof(float4), t->stream));
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_accumulate_film(dcrt_tracer* t, const dcrt_filter_params* f)
+{
+    TRACER_GUARD(t);
+    if (!f) return DCRT_E_INVALID_ARG;
+    return t->Accumulate(*f);
+}
+
+DCRT_API int dcrt_tracer_read_film(dcrt_tracer* t, float* out)
+{
+    TRACER_GUARD(t);
+    if (!out || !t->film.accum) return DCRT_E_INVALID_ARG;
+    HIPCHECK(hipMemcpyAsync(out, t->film.accum, (size_t)t->filmW * t->filmH * sizeof(float4), hipMemcpyDeviceToHost, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_read_samples(dcrt_tracer* t, float* pos, float* val)
+{
+    TRACER_GUARD(t);
+    if (!t->film.sampleValue) return DCRT_E_INVALID_ARG;
+    const size_t n = (size_t)t->filmW * t->filmH;
+    if (pos) HIPCHECK(hipMemcpyAsync(pos, t->film.samplePosition, n * sizeof(float2), hipMemcpyDeviceToHost, t->stream));
+    if (val) HIPCHECK(hipMemcpyAsync(val, t->film.sampleValue, n * sizeof(float4), hipMemcpyDeviceToHost, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_read_rng(dcrt_tracer* t, uint32_t* out)
+{
+    TRACER_GUARD(t);
+    if (!out || !t->film.debugRng) { SetLastError("tracer was created without debug_rng"); return DCRT_E_INVALID_ARG; }
+    HIPCHECK(hipMemcpyAsync(out, t->film.debugRng, (size_t)t->filmW * t->filmH * sizeof(uint4), hipMemcpyDeviceToHost, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_film_device_ptr(dcrt_tracer* t, void** out)
+{
+    TRACER_GUARD(t);
+    if (!out) return DCRT_E_INVALID_ARG;
+    *out = t->film.accum;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_counters(dcrt_tracer* t, dcrt_ray_stats* out)
+{
+    TRACER_GUARD(t);
+    if (!out) return DCRT_E_INVALID_ARG;
+    Globals g;
+    HIPCHECK(hipMemcpyAsync(&g, t->dGlobals, sizeof(Globals), hipMemcpyDeviceToHost, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    out->extension_rays = g.extRays;
+    out->shadow_rays = g.shadowRays;
+    out->new_paths = g.newPaths;
+    out->iterations = g.iterations;
+    out->images_completed = 0;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_set_instrumentation(dcrt_tracer* t, int counters, int ext_timing)
+{
+    TRACER_GUARD(t);
+    if ((counters != 0) != t->instrCounters) t->InvalidateGraph();
+    t->instrCounters = counters != 0;
+    t->extTiming = ext_timing != 0;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_traversal_stats(dcrt_tracer* t, dcrt_traversal_stats* out)
+{
+    TRACER_GUARD(t);
+    if (!out) return DCRT_E_INVALID_ARG;
+    unsigned long long v[8];
+    HIPCHECK(hipMemcpyAsync(v, t->dInstr, sizeof(v), hipMemcpyDeviceToHost, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    double ms = t->extMs;
+    uint64_t launches = t->extLaunches;
+    for (size_t i = 0; i + 1 < t->eventsUsed; i += 2) {
+        float e = 0.0f;
+        HIPCHECK(hipEventElapsedTime(&e, t->events[i], t->events[i + 1]));
+        ms += e;
+        ++launches;
+    }
+    t->extMs = ms;
+    t->extLaunches = launches;
+    t->eventsUsed = 0;
+    out->ext_node_visits = v[0]; out->ext_triangle_tests = v[1]; out->ext_blas_entries = v[2];
+    out->shadow_node_visits = v[3]; out->shadow_triangle_tests = v[4]; out->shadow_blas_entries = v[5];
+    out->ext_launches = launches;
+    out->ext_kernel_ms = ms;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_reset_stats(dcrt_tracer* t)
+{
+    TRACER_GUARD(t);
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    HIPCHECK(hipMemsetAsync(t->dInstr, 0, 8 * sizeof(unsigned long long), t->stream));
+    Globals g;
+    HIPCHECK(hipMemcpyAsync(&g, t->dGlobals, sizeof(Globals), hipMemcpyDeviceToHost, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    g.extRays = g.shadowRays = g.newPaths = g.iterations = 0;
+    HIPCHECK(hipMemcpyAsync(t->dGlobals, &g, sizeof(Globals), hipMemcpyHostToDevice, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    t->eventsUsed = 0;
+    t->extMs = 0.0;
+    t->extLaunches = 0;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_synchronize(dcrt_tracer* t)
+{
+    TRACER_GUARD(t);
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_get_luts(dcrt_tracer* t, dcrt_bxdf_luts* out)
+{
+    TRACER_GUARD(t);
+    if (!out) return DCRT_E_INVALID_ARG;
+    HIPCHECK(hipMemcpyAsync(out, t->dLuts, sizeof(dcrt_bxdf_luts), hipMemcpyDeviceToHost, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_set_luts(dcrt_tracer* t, const dcrt_bxdf_luts* luts)
+{
+    TRACER_GUARD(t);
+    if (!luts) return DCRT_E_INVALID_ARG;
+    HIPCHECK(hipMemcpyAsync(t->dLuts, luts, sizeof(dcrt_bxdf_luts), hipMemcpyHostToDevice, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    return DCRT_OK;
+}
+
+static int TraceBatch(dcrt_tracer* t, const dcrt_ray* d_rays, uint32_t n, dcrt_ray_hit* d_hits, uint32_t* d_occ, bool any, uint32_t features)
+{
+    if (!t->hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
+    const uint32_t grid = (n + t->castBlock - 1) / t->castBlock;
+    if (n == 0) return DCRT_OK;
+    unsigned long long* instr = t->instrCounters ? t->dInstr : nullptr;
+    if (any)
+        hipLaunchKernelGGL(batch_trace_kernel<true>, dim3(grid), dim3(t->castBlock), t->castLds, t->stream, t->scene, d_rays, n, features, d_hits, d_occ, instr);
+    else
+        hipLaunchKernelGGL(batch_trace_kernel<false>, dim3(grid), dim3(t->castBlock), t->castLds, t->stream, t->scene, d_rays, n, features, d_hits, d_occ, instr);
+    HIPCHECK(hipGetLastError());
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_trace_rays(dcrt_tracer* t, const dcrt_ray* rays, uint32_t n, dcrt_ray_hit* out, uint32_t features)
+{
+    TRACER_GUARD(t);
+    if ((!rays || !out) && n) return DCRT_E_INVALID_ARG;
+    std::vector<void*> tmp;
+    dcrt_ray* dr = nullptr; dcrt_ray_hit* dh = nullptr;
+    CHECKED(DeviceAlloc(&dr, n, &tmp));
+    CHECKED(DeviceAlloc(&dh, n, &tmp));
+    int rc = DCRT_OK;
+    if (hipMemcpyAsync(dr, rays, (size_t)n * sizeof(dcrt_ray), hipMemcpyHostToDevice, t->stream) != hipSuccess) rc = DCRT_E_HIP;
+    if (rc == DCRT_OK) rc = TraceBatch(t, dr, n, dh, nullptr, false, features);
+    if (rc == DCRT_OK && hipMemcpyAsync(out, dh, (size_t)n * sizeof(dcrt_ray_hit), hipMemcpyDeviceToHost, t->stream) != hipSuccess) rc = DCRT_E_HIP;
+    if (hipStreamSynchronize(t->stream) != hipSuccess) rc = DCRT_E_HIP;
+    FreeAll(&tmp);
+    return rc;
+}
+
+DCRT_API int dcrt_tracer_occluded(dcrt_tracer* t, const dcrt_ray* rays, uint32_t n, uint32_t* out, uint32_t features)
+{
+    TRACER_GUARD(t);
+    if ((!rays || !out) && n) return DCRT_E_INVALID_ARG;
+    std::vector<void*> tmp;
+    dcrt_ray* dr = nullptr; uint32_t* dOcc = nullptr;
+    CHECKED(DeviceAlloc(&dr, n, &tmp));
+    CHECKED(DeviceAlloc(&dOcc, n, &tmp));
+    int rc = DCRT_OK;
+    if (hipMemcpyAsync(dr, rays, (size_t)n * sizeof(dcrt_ray), hipMemcpyHostToDevice, t->stream) != hipSuccess) rc = DCRT_E_HIP;
+    if (rc == DCRT_OK) rc = TraceBatch(t, dr, n, nullptr, dOcc, true, features);
+    if (rc == DCRT_OK && hipMemcpyAsync(out, dOcc, (size_t)n * 4, hipMemcpyDeviceToHost, t->stream) != hipSuccess) rc = DCRT_E_HIP;
+    if (hipStreamSynchronize(t->stream) != hipSuccess) rc = DCRT_E_HIP;
+    FreeAll(&tmp);
+    return rc;
+}
+
+DCRT_API int dcrt_tracer_trace_rays_device(dcrt_tracer* t, const void* d_rays, uint32_t n, void* d_hits, uint32_t features)
+{
+    TRACER_GUARD(t);
+    return TraceBatch(t, (const dcrt_ray*)d_rays, n, (dcrt_ray_hit*)d_hits, nullptr, false, features);
+}
+
+DCRT_API int dcrt_device_math_eval(dcrt_tracer* t, int function, const float* x, uint32_t n, float* y)
+{
+    TRACER_GUARD(t);
+    if ((!x || !y) && n) return DCRT_E_INVALID_ARG;
+    std::vector<void*> tmp;
+    float *dx = nullptr, *dy = nullptr;
+    CHECKED(DeviceAlloc(&dx, n, &tmp));
+    CHECKED(DeviceAlloc(&dy, n, &tmp));
+    int rc = DCRT_OK;
+    if (hipMemcpyAsync(dx, x, (size_t)n * 4, hipMemcpyHostToDevice, t->stream) != hipSuccess) rc = DCRT_E_HIP;
+    if (rc == DCRT_OK && n) {
+        hipLaunchKernelGGL(math_eval_kernel, dim3((n + 255) / 256), dim3(256), 0, t->stream, function, dx, n, dy);
+        if (hipGetLastError() != hipSuccess) rc = DCRT_E_HIP;
+    }
+    if (rc == DCRT_OK && hipMemcpyAsync(y, dy, (size_t)n * 4, hipMemcpyDeviceToHost, t->stream) != hipSuccess) rc = DCRT_E_HIP;
+    if (hipStreamSynchronize(t->stream) != hipSuccess) rc = DCRT_E_HIP;
+    FreeAll(&tmp);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,230 @@
+// capi_scene.cpp -- extern "C" surface of the host scene (include/dcrt.h).
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "../../../include/dcrt.h"
+#include "scene.h"
+
+namespace dcrt {
+thread_local std::string g_lastError;
+void SetLastError(const std::string& s) { g_lastError = s; }
+}  // namespace dcrt
+
+struct dcrt_scene {
+    dcrt::CScene scene;
+};
+
+using dcrt::SetLastError;
+
+#define DCRT_GUARD_BEGIN try {
+#define DCRT_GUARD_END                                   \
+    }                                                    \
+    catch (const std::exception& e)                      \
+    {                                                    \
+        SetLastError(e.what());                          \
+        return DCRT_E_INVALID_ARG;                       \
+    }                                                    \
+    catch (...)                                          \
+    {                                                    \
+        SetLastError("unknown C++ exception");           \
+        return DCRT_E_INVALID_ARG;                       \
+    }
+
+extern "C" {
+
+DCRT_API const char* dcrt_version(void) { return "dcrt-mi355x 0.1.0 (gfx950)"; }
+DCRT_API const char* dcrt_last_error(void) { return dcrt::g_lastError.c_str(); }
+
+DCRT_API int dcrt_scene_create(dcrt_scene** out)
+{
+    if (!out) return DCRT_E_INVALID_ARG;
+    DCRT_GUARD_BEGIN
+    *out = new dcrt_scene();
+    (*out)->scene.Reset(1920, 1080);
+    return DCRT_OK;
+    DCRT_GUARD_END
+}
+
+DCRT_API void dcrt_scene_destroy(dcrt_scene* s) { delete s; }
+
+DCRT_API int dcrt_scene_reset(dcrt_scene* s, uint32_t w, uint32_t h)
+{
+    if (!s || !w || !h) return DCRT_E_INVALID_ARG;
+    s->scene.Reset(w, h);
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_load_from_file(dcrt_scene* s, const char* path)
+{
+    if (!s || !path) return DCRT_E_INVALID_ARG;
+    DCRT_GUARD_BEGIN
+    if (!s->scene.LoadFromFile(path)) {
+        SetLastError(std::string("failed to load scene ") + path);
+        return DCRT_E_IO;
+    }
+    return DCRT_OK;
+    DCRT_GUARD_END
+}
+
+DCRT_API int dcrt_scene_add_punctual_light(dcrt_scene* s, const float position[3], const float euler[3], const float color[3], int is_directional)
+{
+    if (!s || !position || !euler || !color) return DCRT_E_INVALID_ARG;
+    if (s->scene.GetLightCount() >= DCRT_MAX_LIGHT_COUNT) return DCRT_E_LIMIT;
+    dcrt::SPunctualLight l;
+    l.position = dcrt::Float3(position[0], position[1], position[2]);
+    l.eulerAngles = dcrt::Float3(euler[0], euler[1], euler[2]);
+    l.color = dcrt::Float3(color[0], color[1], color[2]);
+    l.isDirectional = is_directional != 0;
+    s->scene.punctualLights.push_back(l);
+    s->scene.Flatten();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_set_environment_light(dcrt_scene* s, const float color[3], const float* cube, uint32_t cube_size)
+{
+    if (!s || !color) return DCRT_E_INVALID_ARG;
+    s->scene.hasEnvironmentLight = true;
+    s->scene.environmentLight.color = dcrt::Float3(color[0], color[1], color[2]);
+    if (cube && cube_size) {
+        s->scene.environmentLight.cubeSize = cube_size;
+        s->scene.environmentLight.cubeRGB.assign(cube, cube + (size_t)6 * cube_size * cube_size * 3);
+    } else {
+        s->scene.environmentLight.cubeSize = 0;
+        s->scene.environmentLight.cubeRGB.clear();
+    }
+    s->scene.Flatten();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_set_camera(dcrt_scene* s, const float position[3], const float euler[3])
+{
+    if (!s || !position || !euler) return DCRT_E_INVALID_ARG;
+    s->scene.camera.position = dcrt::Float3(position[0], position[1], position[2]);
+    s->scene.camera.eulerAngles = dcrt::Float3(euler[0], euler[1], euler[2]);
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_set_lens(dcrt_scene* s, int camera_type, float fov_x, float focal_length, float focal_distance,
+                                 float relative_aperture, uint32_t blade_count, float aperture_rotation, const float film_size[2])
+{
+    if (!s || (camera_type != 0 && camera_type != 1)) return DCRT_E_INVALID_ARG;
+    s->scene.cameraType = (dcrt::ECameraType)camera_type;
+    s->scene.fovX = fov_x;
+    s->scene.focalLength = focal_length;
+    s->scene.focalDistance = focal_distance;
+    s->scene.relativeAperture = relative_aperture;
+    s->scene.apertureBladeCount = blade_count;
+    s->scene.apertureRotation = aperture_rotation;
+    if (film_size) s->scene.filmSize = { film_size[0], film_size[1] };
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_set_max_bounce(dcrt_scene* s, uint32_t max_bounce)
+{
+    if (!s || max_bounce > DCRT_MAX_RAY_BOUNCE) return DCRT_E_INVALID_ARG;
+    s->scene.maxBounceCount = max_bounce;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_set_filter(dcrt_scene* s, const dcrt_filter_params* f)
+{
+    if (!s || !f || f->filter > DCRT_FILTER_LANCZOS || !(f->radius >= 0.0f)) return DCRT_E_INVALID_ARG;
+    s->scene.filter = (dcrt::EFilter)f->filter;
+    s->scene.filterRadius = f->radius;
+    s->scene.gaussianFilterAlpha = f->gaussian_alpha;
+    s->scene.mitchellB = f->mitchell_b;
+    s->scene.mitchellC = f->mitchell_c;
+    s->scene.lanczosSincTau = f->lanczos_tau ? f->lanczos_tau : 3;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_filter(const dcrt_scene* s, dcrt_filter_params* out)
+{
+    if (!s || !out) return DCRT_E_INVALID_ARG;
+    *out = s->scene.GetFilterParams();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_resolution(const dcrt_scene* s, uint32_t* w, uint32_t* h)
+{
+    if (!s || !w || !h) return DCRT_E_INVALID_ARG;
+    *w = s->scene.resolutionWidth;
+    *h = s->scene.resolutionHeight;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_material_count(const dcrt_scene* s, uint32_t* out)
+{
+    if (!s || !out) return DCRT_E_INVALID_ARG;
+    *out = (uint32_t)s->scene.materials.size();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_set_material(dcrt_scene* s, uint32_t index, int type, const float albedo[3], float roughness,
+                                     const float ior[3], const float k[3], int multiscattering, int two_sided)
+{
+    if (!s || index >= s->scene.materials.size() || type < 0 || type > 4) return DCRT_E_INVALID_ARG;
+    dcrt::SMaterial& m = s->scene.materials[index];
+    m.type = (dcrt::EMaterialType)type;
+    if (albedo) m.albedo = dcrt::Float3(albedo[0], albedo[1], albedo[2]);
+    m.roughness = roughness;
+    if (ior) m.ior = dcrt::Float3(ior[0], ior[1], ior[2]);
+    if (k) m.k = dcrt::Float3(k[0], k[1], k[2]);
+    m.multiscattering = multiscattering != 0;
+    m.isTwoSided = two_sided != 0;
+    if (s->scene.hasValidScene) {
+        for (size_t i = 0; i < s->scene.meshes.size(); ++i) {
+            bool opaque = true;
+            for (uint32_t id : s->scene.meshes[i].materialIds) opaque = opaque && s->scene.materials[id].IsOpaque();
+            s->scene.meshOpaque[i] = opaque;
+        }
+        s->scene.Flatten();
+    }
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_flat(dcrt_scene* s, dcrt_flat_scene* out)
+{
+    if (!s || !out) return DCRT_E_INVALID_ARG;
+    if (!s->scene.hasValidScene) { SetLastError("scene has no content"); return DCRT_E_NO_SCENE; }
+    *out = s->scene.GetFlat();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_frame_params(const dcrt_scene* s, uint32_t seed, dcrt_frame_params* out)
+{
+    if (!s || !out) return DCRT_E_INVALID_ARG;
+    *out = s->scene.GetFrameParams(seed);
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_bvh_info(const dcrt_scene* s, uint32_t* tlas_nodes, uint32_t* total_nodes, uint32_t* max_stack)
+{
+    if (!s) return DCRT_E_INVALID_ARG;
+    uint32_t total = (uint32_t)s->scene.tlas.size();
+    for (const dcrt::Mesh& m : s->scene.meshes) total += (uint32_t)m.bvhNodes.size();
+    if (tlas_nodes) *tlas_nodes = (uint32_t)s->scene.tlas.size();
+    if (total_nodes) *total_nodes = total;
+    if (max_stack) *max_stack = s->scene.bvhTraversalStackSize;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_bvh_build_blas(const dcrt_vertex* vertices, const uint32_t* indices, uint32_t triangle_count, dcrt_bvh_node* out_nodes,
+                                 uint32_t* out_node_count, uint32_t* out_reordered_indices, uint32_t* out_reordered_triangles,
+                                 uint32_t* out_max_depth, uint32_t* out_max_stack_size)
+{
+    if (!vertices || !indices || !out_nodes || !out_node_count || !out_reordered_indices || !out_reordered_triangles || !triangle_count)
+        return DCRT_E_INVALID_ARG;
+    DCRT_GUARD_BEGIN
+    dcrt::bvh::BuildResult r;
+    dcrt::bvh::BuildBLAS(vertices, indices, triangle_count, out_reordered_indices, out_reordered_triangles, &r);
+    dcrt::bvh::PackBVH(r.nodes.data(), (uint32_t)r.nodes.size(), true, out_nodes);
+    *out_node_count = (uint32_t)r.nodes.size();
+    if (out_max_depth) *out_max_depth = r.maxDepth;
+    if (out_max_stack_size) *out_max_stack_size = r.maxStackSize;
+    return DCRT_OK;
+    DCRT_GUARD_END
+}
+
+}  // extern "C"

@@ -1,0 +1,145 @@
+"""Host scene (``CScene``, Source/Scene.h:67-224) over the C ABI.
+
+Loading (OBJ, Mitsuba XML), BVH build (BVHAccel) and flattening run in the
+native library; this class mirrors the reference's method names and exposes
+zero-copy numpy views of the flattened Appendix-B buffers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+from . import _abi
+from ._abi import check, f3
+
+
+class Scene:
+    """CScene: LoadFromFile / Reset / lights / camera / film settings."""
+
+    def __init__(self, resolution=(1920, 1080)):
+        self._lib = _abi.load_library()
+        h = C.c_void_p()
+        check(self._lib.dcrt_scene_create(C.byref(h)), "dcrt_scene_create")
+        self._h = h
+        self.reset(*resolution)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.dcrt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---- CScene API -----------------------------------------------------
+    def reset(self, width: int, height: int) -> None:            # Scene.cpp:626-660
+        check(self._lib.dcrt_scene_reset(self._h, int(width), int(height)), "Reset")
+
+    def load_from_file(self, path) -> None:                      # Scene.cpp:103-624
+        check(self._lib.dcrt_scene_load_from_file(self._h, str(Path(path)).encode()), "LoadFromFile")
+
+    def add_point_light(self, position, color) -> None:          # ImGui.cpp:322-331
+        check(self._lib.dcrt_scene_add_punctual_light(self._h, f3(position), f3((0, 0, 0)), f3(color), 0), "AddPointLight")
+
+    def add_directional_light(self, euler_angles, color) -> None:
+        check(self._lib.dcrt_scene_add_punctual_light(self._h, f3((0, 0, 0)), f3(euler_angles), f3(color), 1),
+              "AddDirectionalLight")
+
+    def set_environment_light(self, color, cube: np.ndarray | None = None) -> None:
+        if cube is None:
+            check(self._lib.dcrt_scene_set_environment_light(self._h, f3(color), None, 0), "SetEnvironmentLight")
+            return
+        cube = np.ascontiguousarray(cube, dtype=np.float32)
+        assert cube.ndim == 4 and cube.shape[0] == 6 and cube.shape[1] == cube.shape[2] and cube.shape[3] == 3
+        self._env_cube = cube
+        check(self._lib.dcrt_scene_set_environment_light(self._h, f3(color), cube.ctypes.data_as(_abi._FP),
+                                                         cube.shape[1]), "SetEnvironmentLight")
+
+    def set_camera(self, position, euler_angles=(0.0, 0.0, 0.0)) -> None:
+        check(self._lib.dcrt_scene_set_camera(self._h, f3(position), f3(euler_angles)), "SetCamera")
+
+    def set_lens(self, camera_type=1, fov_x=1.221730, focal_length=0.05, focal_distance=2.0, relative_aperture=8.0,
+                 blade_count=7, aperture_rotation=0.0, film_size=(0.05333, 0.03)) -> None:
+        fs = (C.c_float * 2)(*film_size)
+        check(self._lib.dcrt_scene_set_lens(self._h, int(camera_type), fov_x, focal_length, focal_distance,
+                                            relative_aperture, int(blade_count), aperture_rotation, fs), "SetLens")
+
+    def set_max_bounce(self, n: int) -> None:
+        check(self._lib.dcrt_scene_set_max_bounce(self._h, int(n)), "SetMaxBounce")
+
+    def set_filter(self, kind=_abi.FILTER_BOX, radius=1.0, gaussian_alpha=1.5, mitchell_b=1 / 3, mitchell_c=1 / 3,
+                   lanczos_tau=3) -> None:
+        f = _abi.FilterParams(kind, radius, gaussian_alpha, mitchell_b, mitchell_c, lanczos_tau)
+        check(self._lib.dcrt_scene_set_filter(self._h, C.byref(f)), "SetFilter")
+
+    def filter_params(self) -> _abi.FilterParams:
+        f = _abi.FilterParams()
+        check(self._lib.dcrt_scene_get_filter(self._h, C.byref(f)), "GetFilter")
+        return f
+
+    def set_material(self, index, material_type, albedo=None, roughness=1.0, ior=None, k=None,
+                     multiscattering=False, two_sided=False) -> None:
+        check(self._lib.dcrt_scene_set_material(self._h, int(index), int(material_type),
+                                                f3(albedo) if albedo is not None else None, float(roughness),
+                                                f3(ior) if ior is not None else None,
+                                                f3(k) if k is not None else None,
+                                                int(multiscattering), int(two_sided)), "SetMaterial")
+
+    @property
+    def material_count(self) -> int:
+        n = C.c_uint32()
+        check(self._lib.dcrt_scene_get_material_count(self._h, C.byref(n)))
+        return n.value
+
+    @property
+    def resolution(self):
+        w, h = C.c_uint32(), C.c_uint32()
+        check(self._lib.dcrt_scene_get_resolution(self._h, C.byref(w), C.byref(h)))
+        return w.value, h.value
+
+    def bvh_info(self):
+        t, n, s = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        check(self._lib.dcrt_scene_get_bvh_info(self._h, C.byref(t), C.byref(n), C.byref(s)))
+        return {"tlas_nodes": t.value, "total_nodes": n.value, "stack_size": s.value}
+
+    def flat(self) -> _abi.FlatScene:
+        f = _abi.FlatScene()
+        check(self._lib.dcrt_scene_get_flat(self._h, C.byref(f)), "GetFlat")
+        return f
+
+    def frame_params(self, frame_seed: int = 0) -> _abi.FrameParams:
+        p = _abi.FrameParams()
+        check(self._lib.dcrt_scene_get_frame_params(self._h, int(frame_seed), C.byref(p)), "GetFrameParams")
+        return p
+
+    # ---- numpy views of the flattened buffers (valid until the scene changes)
+    def arrays(self) -> dict:
+        f = self.flat()
+
+        def view(ptr, count, dtype, cols=None):
+            if count == 0 or not ptr:
+                return np.zeros((0,) if cols is None else (0, cols), dtype=dtype)
+            n = count * (cols or 1)
+            a = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dtype))), shape=(n,))
+            return a.reshape(-1, cols) if cols else a
+
+        return {
+            "vertices": view(f.vertices, f.vertex_count, np.float32, 11),
+            "triangles": view(f.triangles, f.triangle_count, np.uint32, 3),
+            "bvh_nodes": view(f.bvh_nodes, f.bvh_node_count, np.uint32, 8),
+            "material_ids": view(f.material_ids, f.triangle_count, np.uint32),
+            "instance_transforms": view(f.instance_transforms, f.instance_count * 2, np.float32, 12),
+            "materials": view(f.materials, f.material_count, np.uint32, 13),
+            "lights": view(f.lights, f.light_count, np.uint32, 7),
+            "tlas_node_count": f.tlas_node_count,
+            "stack_size": f.bvh_traversal_stack_size,
+        }

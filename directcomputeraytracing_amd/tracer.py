@@ -1,0 +1,188 @@
+"""``CWavefrontPathTracer`` (Source/WavefrontPathTracer.h:7-101) on MI355X.
+
+A thin host mirror over the C ABI: every call goes to ``libdcrt.so`` (gfx950
+kernels). Method names follow the reference's ``CPathTracer`` interface
+(Source/PathTracer.h:3-31): ``create``/``destroy``/``on_scene_loaded``/
+``render``/``reset_image``/``is_image_complete``/``acquire_film_clear_trigger``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._abi import check
+from .scene import Scene
+
+RAY_DTYPE = np.dtype([("origin", "<f4", 3), ("t_max", "<f4"), ("direction", "<f4", 3), ("t_min", "<f4")])
+HIT_DTYPE = np.dtype([("t", "<f4"), ("u", "<f4"), ("v", "<f4"), ("triangle_id", "<u4"), ("instance_index", "<u4")])
+assert RAY_DTYPE.itemsize == 32 and HIT_DTYPE.itemsize == 20
+
+MATH_SIN, MATH_COS, MATH_EXP, MATH_ATAN = range(4)
+
+
+def make_rays(origins, directions, t_min=0.0, t_max=np.inf) -> np.ndarray:
+    o = np.asarray(origins, np.float32).reshape(-1, 3)
+    d = np.asarray(directions, np.float32).reshape(-1, 3)
+    r = np.zeros(len(o), RAY_DTYPE)
+    r["origin"], r["direction"] = o, d
+    r["t_min"], r["t_max"] = t_min, t_max
+    return r
+
+
+class WavefrontPathTracer:
+    """CWavefrontPathTracer: path pool, queues and kernels resident in HBM."""
+
+    def __init__(self, path_pool_size: int = 0, iterations_per_render: int = 0, device: int = 0,
+                 stream: int | None = None, debug_rng: bool = False):
+        self._lib = _abi.load_library()
+        self._h = None
+        self.create(path_pool_size, iterations_per_render, device, stream, debug_rng)
+
+    # ---- CPathTracer --------------------------------------------------------
+    def create(self, path_pool_size=0, iterations_per_render=0, device=0, stream=None, debug_rng=False):
+        cfg = _abi.TracerConfig(int(path_pool_size), int(iterations_per_render), int(device),
+                                C.c_void_p(stream or 0), 1 if debug_rng else 0)
+        h = C.c_void_p()
+        check(self._lib.dcrt_tracer_create(C.byref(cfg), C.byref(h)), "Create")
+        self._h = h
+        self.width = self.height = 0
+        self.filter = _abi.FilterParams(_abi.FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3)
+
+    def destroy(self):
+        if self._h:
+            self._lib.dcrt_tracer_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+    def on_scene_loaded(self, scene: Scene, frame_seed: int = 0) -> None:
+        """Upload the flattened scene and the camera/film constants (OnSceneLoaded)."""
+        flat = scene.flat()
+        check(self._lib.dcrt_tracer_upload_scene(self._h, C.byref(flat)), "OnSceneLoaded")
+        self.set_frame_params(scene.frame_params(frame_seed))
+        self.filter = scene.filter_params()
+
+    def set_frame_params(self, params: _abi.FrameParams) -> None:
+        check(self._lib.dcrt_tracer_set_frame_params(self._h, C.byref(params)), "SetFrameParams")
+        self.width, self.height = params.resolution[0], params.resolution[1]
+
+    def set_film_partition(self, world_size: int, rank: int, stripe_height: int = 64, halo_rows: int = 0) -> None:
+        p = _abi.FilmPartition(world_size, rank, stripe_height, halo_rows)
+        check(self._lib.dcrt_tracer_set_film_partition(self._h, C.byref(p)), "SetFilmPartition")
+
+    def render(self, max_iterations: int = 0) -> None:
+        check(self._lib.dcrt_tracer_render(self._h, int(max_iterations)), "Render")
+
+    def render_images(self, first_seed: int, count: int, filter_params: _abi.FilterParams | None = None) -> None:
+        f = filter_params or self.filter
+        check(self._lib.dcrt_tracer_render_images(self._h, int(first_seed), int(count), C.byref(f)), "RenderImages")
+
+    def reset_image(self) -> None:
+        check(self._lib.dcrt_tracer_reset_image(self._h), "ResetImage")
+
+    def is_image_complete(self) -> bool:
+        v = C.c_int()
+        check(self._lib.dcrt_tracer_is_image_complete(self._h, C.byref(v)), "IsImageComplete")
+        return bool(v.value)
+
+    def acquire_film_clear_trigger(self) -> bool:
+        v = C.c_int()
+        check(self._lib.dcrt_tracer_acquire_film_clear_trigger(self._h, C.byref(v)), "AcquireFilmClearTrigger")
+        return bool(v.value)
+
+    # ---- film --------------------------------------------------------------
+    def clear_film(self) -> None:
+        check(self._lib.dcrt_tracer_clear_film(self._h), "ClearFilm")
+
+    def accumulate_film(self, filter_params: _abi.FilterParams | None = None) -> None:
+        f = filter_params or self.filter
+        check(self._lib.dcrt_tracer_accumulate_film(self._h, C.byref(f)), "SampleConvolution")
+
+    def read_film(self) -> np.ndarray:
+        out = np.empty((self.height, self.width, 4), np.float32)
+        check(self._lib.dcrt_tracer_read_film(self._h, out.ctypes.data_as(_abi._FP)), "ReadFilm")
+        return out
+
+    def read_samples(self):
+        pos = np.empty((self.height, self.width, 2), np.float32)
+        val = np.empty((self.height, self.width, 4), np.float32)
+        check(self._lib.dcrt_tracer_read_samples(self._h, pos.ctypes.data_as(_abi._FP), val.ctypes.data_as(_abi._FP)),
+              "ReadSamples")
+        return pos, val
+
+    def read_rng(self) -> np.ndarray:
+        out = np.empty((self.height, self.width, 4), np.uint32)
+        check(self._lib.dcrt_tracer_read_rng(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32))), "ReadRng")
+        return out
+
+    def film_device_ptr(self) -> int:
+        p = C.c_void_p()
+        check(self._lib.dcrt_tracer_film_device_ptr(self._h, C.byref(p)), "FilmDevicePtr")
+        return p.value or 0
+
+    # ---- statistics ----------------------------------------------------------
+    def counters(self) -> dict:
+        s = _abi.RayStats()
+        check(self._lib.dcrt_tracer_counters(self._h, C.byref(s)), "Counters")
+        return {k: getattr(s, k) for k, _ in _abi.RayStats._fields_}
+
+    def set_instrumentation(self, counters: bool, ext_timing: bool) -> None:
+        check(self._lib.dcrt_tracer_set_instrumentation(self._h, int(counters), int(ext_timing)), "SetInstrumentation")
+
+    def traversal_stats(self) -> dict:
+        s = _abi.TraversalStats()
+        check(self._lib.dcrt_tracer_traversal_stats(self._h, C.byref(s)), "TraversalStats")
+        return {k: getattr(s, k) for k, _ in _abi.TraversalStats._fields_}
+
+    def reset_stats(self) -> None:
+        check(self._lib.dcrt_tracer_reset_stats(self._h), "ResetStats")
+
+    def synchronize(self) -> None:
+        check(self._lib.dcrt_tracer_synchronize(self._h), "Synchronize")
+
+    def luts(self) -> _abi.BxDFLuts:
+        l = _abi.BxDFLuts()
+        check(self._lib.dcrt_tracer_get_luts(self._h, C.byref(l)), "GetLuts")
+        return l
+
+    def set_luts(self, luts: _abi.BxDFLuts) -> None:
+        check(self._lib.dcrt_tracer_set_luts(self._h, C.byref(luts)), "SetLuts")
+
+    # ---- kernel-level entry points -------------------------------------------
+    def trace_rays(self, rays: np.ndarray, features: int = _abi.FEATURE_DEFAULT) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, RAY_DTYPE)
+        hits = np.zeros(len(rays), HIT_DTYPE)
+        check(self._lib.dcrt_tracer_trace_rays(self._h, rays.ctypes.data_as(C.POINTER(_abi.Ray)), len(rays),
+                                               hits.ctypes.data_as(C.POINTER(_abi.RayHit)), int(features)), "TraceRays")
+        return hits
+
+    def occluded(self, rays: np.ndarray, features: int = _abi.FEATURE_DEFAULT) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, RAY_DTYPE)
+        out = np.zeros(len(rays), np.uint32)
+        check(self._lib.dcrt_tracer_occluded(self._h, rays.ctypes.data_as(C.POINTER(_abi.Ray)), len(rays),
+                                             out.ctypes.data_as(C.POINTER(C.c_uint32)), int(features)), "Occluded")
+        return out
+
+    def trace_rays_device(self, d_rays: int, count: int, d_hits: int, features: int = _abi.FEATURE_DEFAULT) -> None:
+        check(self._lib.dcrt_tracer_trace_rays_device(self._h, C.c_void_p(d_rays), int(count), C.c_void_p(d_hits),
+                                                      int(features)), "TraceRaysDevice")
+
+    def math_eval(self, function: int, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.float32)
+        y = np.empty_like(x)
+        check(self._lib.dcrt_device_math_eval(self._h, int(function), x.ctypes.data_as(_abi._FP), x.size,
+                                              y.ctypes.data_as(_abi._FP)), "MathEval")
+        return y
+
+
+def device_count() -> int:
+    lib = _abi.load_library()
+    n = C.c_int()
+    check(lib.dcrt_device_count(C.byref(n)))
+    return n.value

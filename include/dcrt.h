@@ -1,0 +1,363 @@
+/*
+ * dcrt.h -- C ABI of the MI355X-native wavefront path tracer.
+ *
+ * This is the drop-in boundary for the hot path of
+ * YaoTiancheng/DirectComputeRayTracing: the `CWavefrontPathTracer` plug-in
+ * (Source/PathTracer.h:6-26, Source/WavefrontPathTracer.cpp:70-1162) and the
+ * scene buffers `CScene` flattens for it (Source/Scene.cpp:273-608).
+ *
+ * Conventions (every entry point):
+ *   - plain C types, pointers and sizes; no C++ or torch types cross the ABI;
+ *   - return int status: 0 = ok, negative = error (see DCRT_E_*); nothing throws;
+ *   - one tracer handle per HIP device; calls on a handle are serialised by the caller;
+ *   - all GPU work of a tracer is ordered on the stream passed to dcrt_tracer_create
+ *     (NULL = the tracer's own non-blocking stream).
+ *
+ * Wire format: the structs below reproduce the reference's GPU layouts byte for
+ * byte (Appendix B of SURVEY.md): Vertex 44 B, BVHNode 32 B, Material 52 B,
+ * SLight 28 B, float4x3 48 B (HLSL column-major), so a maintainer can hand the
+ * reference's CScene arrays straight through.
+ */
+#ifndef DCRT_H_
+#define DCRT_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCRT_API __attribute__((visibility("default")))
+
+/* ---- status codes ---------------------------------------------------- */
+#define DCRT_OK              0
+#define DCRT_E_INVALID_ARG  -1
+#define DCRT_E_HIP          -2   /* a HIP runtime call failed               */
+#define DCRT_E_NO_SCENE     -3   /* render before dcrt_tracer_upload_scene   */
+#define DCRT_E_IO           -4   /* file could not be read / parsed         */
+#define DCRT_E_LIMIT        -5   /* a reference limit was exceeded          */
+#define DCRT_E_NO_DEVICE    -6   /* no HIP device visible                   */
+
+/* ---- constants shared with the reference shaders ----------------------- */
+/* Shaders/LightSharedDef.inc.hlsl:6-12 */
+#define DCRT_LIGHT_INDEX_INVALID        0xFFFFFFFFu
+#define DCRT_LIGHT_FLAGS_POINT_LIGHT        0x1u
+#define DCRT_LIGHT_FLAGS_MESH_LIGHT         0x2u
+#define DCRT_LIGHT_FLAGS_DIRECTIONAL_LIGHT  0x4u
+#define DCRT_LIGHT_FLAGS_ENVIRONMENT_LIGHT  0x8u
+/* Shaders/Material.inc.hlsl:6-19 */
+#define DCRT_MATERIAL_FLAG_ROUGHNESS_TEXTURE 0x20u
+#define DCRT_MATERIAL_FLAG_IS_TWOSIDED       0x40u
+#define DCRT_MATERIAL_FLAG_MULTISCATTERING   0x80u
+#define DCRT_MATERIAL_FLAG_INTERNAL_SCATTERING_SHIFT 8
+#define DCRT_MATERIAL_FLAG_INTERNAL_SCATTERING_MASK  0x300u
+#define DCRT_MATERIAL_FLAG_TYPE_MASK         0xFu
+#define DCRT_MATERIAL_TYPE_DIFFUSE          0
+#define DCRT_MATERIAL_TYPE_PLASTIC          1
+#define DCRT_MATERIAL_TYPE_CONDUCTOR        2
+#define DCRT_MATERIAL_TYPE_DIELECTRIC       3
+#define DCRT_MATERIAL_TYPE_THIN_DIELECTRIC  4
+/* Shaders/InternalScatteringMode.inc.hlsl:4-6 */
+#define DCRT_INTERNAL_SCATTERING_IGNORE   0
+#define DCRT_INTERNAL_SCATTERING_SINGLE   1
+#define DCRT_INTERNAL_SCATTERING_MULTIPLE 2
+/* Shaders/InstanceSharedDef.inc.hlsl:4-5 */
+#define DCRT_INSTANCE_FLAG_OPAQUE             0x1u
+#define DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE  0xFFFFFFFFu
+/* Shaders/BVHSharedDef.inc.hlsl:4 */
+#define DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT 0x1FFFFFFFu
+/* Scene.h:108-109 */
+#define DCRT_MAX_RAY_BOUNCE   20
+#define DCRT_MAX_LIGHT_COUNT  5000
+/* Shaders/BxDFTextureDef.inc.hlsl:4-9 */
+#define DCRT_BXDFTEX_BRDF_SIZE_X 32
+#define DCRT_BXDFTEX_BRDF_SIZE_Y 32
+#define DCRT_BXDFTEX_BRDF_DIELECTRIC_SIZE_X 32
+#define DCRT_BXDFTEX_BRDF_DIELECTRIC_SIZE_Y 16
+#define DCRT_BXDFTEX_BRDF_DIELECTRIC_SIZE_Z 16
+
+/* ---- feature variants (WavefrontPathTracer.cpp:554-590 shader defines) -- */
+#define DCRT_FEATURE_GGX_SAMPLE_VNDF          0x01u  /* GGX_SAMPLE_VNDF (default on)            */
+#define DCRT_FEATURE_NO_FRONT_TO_BACK         0x02u  /* BVH_NO_FRONT_TO_BACK_TRAVERSAL (off)    */
+#define DCRT_FEATURE_LIGHT_VISIBLE            0x04u  /* LIGHT_VISIBLE (default on)              */
+#define DCRT_FEATURE_WATERTIGHT               0x08u  /* WATERTIGHT_RAY_TRIANGLE_INTERSECTION(on)*/
+#define DCRT_FEATURE_DEFAULT (DCRT_FEATURE_GGX_SAMPLE_VNDF | DCRT_FEATURE_LIGHT_VISIBLE | DCRT_FEATURE_WATERTIGHT)
+
+/* ---- Appendix-B layouts ------------------------------------------------ */
+/* Shaders/Vertex.inc.hlsl:8-14 -- 44 bytes */
+typedef struct dcrt_vertex {
+    float position[3];
+    float normal[3];
+    float tangent[3];
+    float texcoord[2];
+} dcrt_vertex;
+
+/* Shaders/BVHNode.inc.hlsl:8-14 -- 32 bytes.
+ * misc = primCount(or TLAS-leaf instance index) << 3 | (TLAS leaf ? 4 : 0) | split axis */
+typedef struct dcrt_bvh_node {
+    float bbox_min[3];
+    float bbox_max[3];
+    uint32_t right_child_or_prim_index;
+    uint32_t misc;
+} dcrt_bvh_node;
+
+/* Shaders/Material.inc.hlsl:23-33 -- 52 bytes */
+typedef struct dcrt_material {
+    float albedo[3];
+    int32_t albedo_texture_index;
+    float ior[3];
+    float roughness;
+    float tex_tiling[2];
+    float opacity;
+    uint32_t flags;
+    int32_t opacity_texture_index;
+} dcrt_material;
+
+/* Shaders/LightSharedDef.inc.hlsl:15-20 -- 28 bytes. For mesh lights the
+ * second float3 holds (triangle offset, triangle count, instance) as uint bits. */
+typedef struct dcrt_light {
+    float radiance[3];
+    float position_or_triangle_range[3];
+    uint32_t flags;
+} dcrt_light;
+
+/* HLSL `float4x3` in a StructuredBuffer, column-major: m[c*4 + r] = M[r][c],
+ * row-vector convention p' = mul(float4(p,1), M) (Scene.cpp:431-444). 48 bytes. */
+typedef struct dcrt_float4x3 {
+    float m[12];
+} dcrt_float4x3;
+
+/* Bindless scene texture (Texture2D<float4> g_Textures[], Scene.cpp:586-608). */
+#define DCRT_TEXTURE_FORMAT_RGBA8_SRGB 0   /* DXGI_FORMAT_R8G8B8A8_UNORM_SRGB */
+#define DCRT_TEXTURE_FORMAT_R8_UNORM   1   /* DXGI_FORMAT_R8_UNORM            */
+typedef struct dcrt_texture {
+    uint32_t width;
+    uint32_t height;
+    uint32_t format;            /* DCRT_TEXTURE_FORMAT_*            */
+    const uint8_t* pixels;      /* tightly packed rows              */
+} dcrt_texture;
+
+/* The flattened scene: exactly what Scene.cpp:273-608 uploads. Host pointers. */
+typedef struct dcrt_flat_scene {
+    const dcrt_vertex* vertices;            uint32_t vertex_count;
+    const uint32_t* triangles;              uint32_t triangle_count;   /* 3 indices / triangle */
+    const dcrt_bvh_node* bvh_nodes;         uint32_t bvh_node_count;   /* TLAS first, then BLASes */
+    uint32_t tlas_node_count;
+    const uint32_t* material_ids;                                       /* one per triangle */
+    const dcrt_float4x3* instance_transforms; uint32_t instance_count;  /* 2N: forward, inverse */
+    const uint32_t* instance_light_indices;                             /* N */
+    const uint32_t* instance_flags;                                     /* N */
+    const uint32_t* instance_material_overrides;                        /* N */
+    const dcrt_material* materials;         uint32_t material_count;
+    const dcrt_light* lights;               uint32_t light_count;       /* mesh, env, punctual */
+    uint32_t environment_light_index;       /* #mesh lights, or DCRT_LIGHT_INDEX_INVALID */
+    const dcrt_texture* textures;           uint32_t texture_count;
+    /* Environment cube (TextureCube<float3>): 6 faces (+X,-X,+Y,-Y,+Z,-Z) of
+     * size x size texels, RGB float, NULL when the scene has none. */
+    const float* env_cube_rgb;              uint32_t env_cube_size;
+    uint32_t bvh_traversal_stack_size;      /* CScene::m_BVHTraversalStackSize */
+} dcrt_flat_scene;
+
+/* The six R16_UNORM BxDF lookup tables (BxDFTexturesBuilding.cpp:171-175,265-270,379-384). */
+#define DCRT_LUT_BRDF_COUNT            (32 * 32)
+#define DCRT_LUT_BRDF_AVG_COUNT        (32)
+#define DCRT_LUT_BRDF_DIELECTRIC_COUNT (32 * 16 * 32)
+#define DCRT_LUT_BRDF_DIELECTRIC_AVG_COUNT (16 * 16 * 2)
+#define DCRT_LUT_BSDF_COUNT            (32 * 16 * 32)
+#define DCRT_LUT_BSDF_AVG_COUNT        (16 * 16 * 2)
+typedef struct dcrt_bxdf_luts {
+    uint16_t brdf[DCRT_LUT_BRDF_COUNT];                         /* [alpha 32][cos 32]            */
+    uint16_t brdf_avg[DCRT_LUT_BRDF_AVG_COUNT];                 /* [alpha 32]                    */
+    uint16_t brdf_dielectric[DCRT_LUT_BRDF_DIELECTRIC_COUNT];   /* [slice 32][alpha 16][cos 32]  */
+    uint16_t brdf_dielectric_avg[DCRT_LUT_BRDF_DIELECTRIC_AVG_COUNT]; /* [slice 2][ior 16][alpha 16] */
+    uint16_t bsdf[DCRT_LUT_BSDF_COUNT];                         /* [slice 32][alpha 16][cos 32]  */
+    uint16_t bsdf_avg[DCRT_LUT_BSDF_AVG_COUNT];                 /* [slice 2][ior 16][alpha 16]   */
+} dcrt_bxdf_luts;
+
+/* Union of SControlConstants / SNewPathConstants / SMaterialConstants
+ * (WavefrontPathTracer.cpp:34-63,372-428). */
+typedef struct dcrt_frame_params {
+    float camera_transform[16];   /* row-major float4x4, translation in row 3 (Camera.cpp:87-96) */
+    uint32_t resolution[2];       /* current film width, height                   */
+    float film_size[2];
+    float aperture_radius;        /* CalculateApertureDiameter() * 0.5            */
+    float focal_distance;
+    float film_distance;          /* CalculateFilmDistance()                      */
+    uint32_t blade_count;
+    float blade_vertex_pos[2];    /* cos/sin(pi / blades) * aperture radius       */
+    float aperture_base_angle;
+    uint32_t frame_seed;
+    uint32_t max_bounce_count;
+    uint32_t light_count;
+    uint32_t environment_light_index;
+    uint32_t features;            /* DCRT_FEATURE_* */
+} dcrt_frame_params;
+
+/* Film reconstruction (Scene.h:131-136, SampleConvolution.cpp:100-130). */
+#define DCRT_FILTER_BOX      0
+#define DCRT_FILTER_TRIANGLE 1
+#define DCRT_FILTER_GAUSSIAN 2
+#define DCRT_FILTER_MITCHELL 3
+#define DCRT_FILTER_LANCZOS  4
+typedef struct dcrt_filter_params {
+    uint32_t filter;              /* DCRT_FILTER_* */
+    float radius;
+    float gaussian_alpha;
+    float mitchell_b;
+    float mitchell_c;
+    uint32_t lanczos_tau;
+} dcrt_filter_params;
+
+/* Ray / hit records of the kernel-level boundary (WavefrontPathTracing.hlsl:3-17). */
+typedef struct dcrt_ray {
+    float origin[3];
+    float t_max;
+    float direction[3];
+    float t_min;
+} dcrt_ray;                       /* 32 bytes, SRay */
+typedef struct dcrt_ray_hit {
+    float t;                      /* +inf on a miss                                   */
+    float u, v;
+    uint32_t triangle_id;         /* bit 31 = backface                                */
+    uint32_t instance_index;
+} dcrt_ray_hit;                   /* 20 bytes, SRayHit */
+
+/* Tracer configuration (CWavefrontPathTracer::Create, WavefrontPathTracer.cpp:25-28). */
+typedef struct dcrt_tracer_config {
+    uint32_t path_pool_size;      /* slots; 0 = default (2^20 on MI355X)             */
+    uint32_t iterations_per_render; /* m_IterationPerFrame; 0 = default              */
+    int32_t device;               /* HIP device ordinal                               */
+    void* stream;                 /* hipStream_t or NULL                              */
+    uint32_t debug_rng;           /* nonzero: keep each pixel's terminal RNG state    */
+} dcrt_tracer_config;
+
+/* Counters of the last rendered image(s). */
+typedef struct dcrt_ray_stats {
+    uint64_t extension_rays;
+    uint64_t shadow_rays;
+    uint64_t new_paths;
+    uint64_t iterations;
+    uint64_t images_completed;
+} dcrt_ray_stats;
+
+/* Rows of the film a tracer renders and convolves (multi-GPU film tiling).
+ * Stripes of `stripe_height` rows; stripe k belongs to rank k % world_size. */
+typedef struct dcrt_film_partition {
+    uint32_t world_size;          /* 1 = whole film                                   */
+    uint32_t rank;
+    uint32_t stripe_height;       /* multiple of 8                                    */
+    uint32_t halo_rows;           /* rows rendered beyond each stripe edge (filter support); 0 = 2 */
+} dcrt_film_partition;
+
+/* Traversal work counters of the extension / shadow casts
+ * (SRayTraversalCounters semantics, SceneRayTrace.h:13-19): node visits =
+ * iterationCounter (BVHAccel.inc.hlsl:121), triangle tests, BLAS entries. */
+typedef struct dcrt_traversal_stats {
+    uint64_t ext_node_visits, ext_triangle_tests, ext_blas_entries;
+    uint64_t shadow_node_visits, shadow_triangle_tests, shadow_blas_entries;
+    uint64_t ext_launches;
+    double ext_kernel_ms;         /* summed HIP-event time of the timed EXTENSION_RAY_CAST launches */
+} dcrt_traversal_stats;
+
+typedef struct dcrt_tracer dcrt_tracer;
+typedef struct dcrt_scene dcrt_scene;
+
+/* ===== version / device ================================================== */
+DCRT_API const char* dcrt_version(void);
+DCRT_API const char* dcrt_last_error(void);
+DCRT_API int dcrt_device_count(int* out_count);
+
+/* ===== host scene: CScene + loaders + BVHAccel (Scene.cpp, BVHAccel.cpp) ==== */
+DCRT_API int dcrt_scene_create(dcrt_scene** out_scene);
+DCRT_API void dcrt_scene_destroy(dcrt_scene* scene);
+/* CScene::Reset (Scene.cpp:626-660): resolution, camera defaults, clears content. */
+DCRT_API int dcrt_scene_reset(dcrt_scene* scene, uint32_t resolution_width, uint32_t resolution_height);
+/* CScene::LoadFromFile (Scene.cpp:103-624): .obj (WavefrontOBJLoading.cpp) or .xml (SceneXMLLoading.cpp). */
+DCRT_API int dcrt_scene_load_from_file(dcrt_scene* scene, const char* path);
+/* Equivalent of UI "Create -> Point/Directional Light" (ImGui.cpp:322-331). */
+DCRT_API int dcrt_scene_add_punctual_light(dcrt_scene* scene, const float position[3], const float euler_angles[3],
+                                           const float color[3], int is_directional);
+/* Constant environment light (SceneXMLLoading.cpp:1454-1467); cube may be NULL. */
+DCRT_API int dcrt_scene_set_environment_light(dcrt_scene* scene, const float color[3],
+                                              const float* cube_rgb, uint32_t cube_size);
+DCRT_API int dcrt_scene_set_camera(dcrt_scene* scene, const float position[3], const float euler_angles[3]);
+/* Camera / film parameters (Scene.h:118-137): camera_type 0 = pinhole, 1 = thin lens. */
+DCRT_API int dcrt_scene_set_lens(dcrt_scene* scene, int camera_type, float fov_x, float focal_length,
+                                 float focal_distance, float relative_aperture, uint32_t blade_count,
+                                 float aperture_rotation, const float film_size[2]);
+DCRT_API int dcrt_scene_set_max_bounce(dcrt_scene* scene, uint32_t max_bounce);
+DCRT_API int dcrt_scene_set_filter(dcrt_scene* scene, const dcrt_filter_params* filter);
+DCRT_API int dcrt_scene_get_filter(const dcrt_scene* scene, dcrt_filter_params* out_filter);
+DCRT_API int dcrt_scene_get_resolution(const dcrt_scene* scene, uint32_t* width, uint32_t* height);
+/* Edit material i (UI material editing, ImGui.cpp:560-660). */
+DCRT_API int dcrt_scene_get_material_count(const dcrt_scene* scene, uint32_t* out_count);
+DCRT_API int dcrt_scene_set_material(dcrt_scene* scene, uint32_t index, int material_type, const float albedo[3],
+                                     float roughness, const float ior[3], const float k[3],
+                                     int multiscattering, int two_sided);
+/* Flattened buffers; pointers stay valid until the scene is modified or destroyed. */
+DCRT_API int dcrt_scene_get_flat(dcrt_scene* scene, dcrt_flat_scene* out_flat);
+/* The frame constants Render() would upload (WavefrontPathTracer.cpp:372-428). */
+DCRT_API int dcrt_scene_get_frame_params(const dcrt_scene* scene, uint32_t frame_seed, dcrt_frame_params* out_params);
+/* BVH statistics: node counts and depth (Scene.cpp:169-207). */
+DCRT_API int dcrt_scene_get_bvh_info(const dcrt_scene* scene, uint32_t* tlas_nodes, uint32_t* total_nodes,
+                                     uint32_t* max_stack_size);
+
+/* Standalone BVHAccel::BuildBLAS + PackBVH over one triangle soup
+ * (BVHAccel.cpp:376-447). out_nodes holds 2*triangle_count-1 entries at most;
+ * out_reordered_indices 3*triangle_count; out_reordered_triangles triangle_count. */
+DCRT_API int dcrt_bvh_build_blas(const dcrt_vertex* vertices, const uint32_t* indices, uint32_t triangle_count,
+                                 dcrt_bvh_node* out_nodes, uint32_t* out_node_count,
+                                 uint32_t* out_reordered_indices, uint32_t* out_reordered_triangles,
+                                 uint32_t* out_max_depth, uint32_t* out_max_stack_size);
+
+/* ===== tracer: CWavefrontPathTracer on MI355X ============================== */
+DCRT_API int dcrt_tracer_create(const dcrt_tracer_config* config, dcrt_tracer** out_tracer);  /* Create()  */
+DCRT_API void dcrt_tracer_destroy(dcrt_tracer* tracer);                                        /* Destroy() */
+/* OnSceneLoaded + the uploads of Scene.cpp:273-608. Copies everything to HBM. */
+DCRT_API int dcrt_tracer_upload_scene(dcrt_tracer* tracer, const dcrt_flat_scene* scene);
+DCRT_API int dcrt_tracer_set_frame_params(dcrt_tracer* tracer, const dcrt_frame_params* params);
+DCRT_API int dcrt_tracer_set_film_partition(dcrt_tracer* tracer, const dcrt_film_partition* partition);
+/* Render(): run up to max_iterations wavefront iterations (0 = config value). */
+DCRT_API int dcrt_tracer_render(dcrt_tracer* tracer, uint32_t max_iterations);
+/* Render whole images: image s uses frame seed first_seed + s; each completed image is
+ * convolved into the film (SampleConvolution) before the next starts. */
+DCRT_API int dcrt_tracer_render_images(dcrt_tracer* tracer, uint32_t first_seed, uint32_t image_count,
+                                       const dcrt_filter_params* filter);
+DCRT_API int dcrt_tracer_reset_image(dcrt_tracer* tracer);                                     /* ResetImage() */
+DCRT_API int dcrt_tracer_is_image_complete(dcrt_tracer* tracer, int* out_complete);           /* IsImageComplete() */
+DCRT_API int dcrt_tracer_acquire_film_clear_trigger(dcrt_tracer* tracer, int* out_trigger);    /* AcquireFilmClearTrigger() */
+DCRT_API int dcrt_tracer_clear_film(dcrt_tracer* tracer);
+DCRT_API int dcrt_tracer_accumulate_film(dcrt_tracer* tracer, const dcrt_filter_params* filter);
+DCRT_API int dcrt_tracer_read_film(dcrt_tracer* tracer, float* out_rgba);                      /* W*H*4 floats */
+DCRT_API int dcrt_tracer_read_samples(dcrt_tracer* tracer, float* out_position, float* out_value); /* W*H*2, W*H*4 */
+DCRT_API int dcrt_tracer_read_rng(dcrt_tracer* tracer, uint32_t* out_state);                   /* W*H*4 (debug_rng) */
+DCRT_API int dcrt_tracer_film_device_ptr(dcrt_tracer* tracer, void** out_ptr);
+DCRT_API int dcrt_tracer_counters(dcrt_tracer* tracer, dcrt_ray_stats* out_stats);
+/* counters != 0: traversal work counters in the cast kernels; ext_timing != 0: plain
+ * (non-graph) launches with HIP events around every EXTENSION_RAY_CAST launch. */
+DCRT_API int dcrt_tracer_set_instrumentation(dcrt_tracer* tracer, int counters, int ext_timing);
+DCRT_API int dcrt_tracer_traversal_stats(dcrt_tracer* tracer, dcrt_traversal_stats* out_stats);
+DCRT_API int dcrt_tracer_reset_stats(dcrt_tracer* tracer);
+DCRT_API int dcrt_tracer_synchronize(dcrt_tracer* tracer);
+DCRT_API int dcrt_tracer_get_luts(dcrt_tracer* tracer, dcrt_bxdf_luts* out_luts);
+DCRT_API int dcrt_tracer_set_luts(dcrt_tracer* tracer, const dcrt_bxdf_luts* luts);
+
+/* Kernel-level entry points used by the parity tests and the roofline bench:
+ * one EXTENSION_RAY_CAST / SHADOW_RAY_CAST launch over a host ray batch. */
+DCRT_API int dcrt_tracer_trace_rays(dcrt_tracer* tracer, const dcrt_ray* rays, uint32_t count, dcrt_ray_hit* out_hits,
+                                    uint32_t features);
+DCRT_API int dcrt_tracer_occluded(dcrt_tracer* tracer, const dcrt_ray* rays, uint32_t count, uint32_t* out_occluded,
+                                  uint32_t features);
+/* Device-resident variant for timing: rays/hits already in HBM, launched on the tracer stream. */
+DCRT_API int dcrt_tracer_trace_rays_device(dcrt_tracer* tracer, const void* d_rays, uint32_t count, void* d_hits,
+                                           uint32_t features);
+
+/* Deterministic transcendental helpers shared by kernels (parity tests). */
+DCRT_API int dcrt_device_math_eval(dcrt_tracer* tracer, int function, const float* x, uint32_t count, float* out_y);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DCRT_H_ */

@@ -1,0 +1,81 @@
+/*
+ * dcrt_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of YaoTiancheng/DirectComputeRayTracing's wavefront path
+ * (Shaders/ *.hlsl) used as the parity checker for the MI355X HIP kernels and as
+ * the scalar CPU baseline (MegakernelPathTracing.hlsl:65-208 transcription).
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it. The product (directcomputeraytracing_amd/) never links or calls it.
+ *
+ * Parity status: pinned against the reference's own public constants (SplitMix64,
+ * xoshiro128** 1.0) and against independent native-uint64 / textbook restatements;
+ * the reference has no tests or golden vectors, so image-level
+ * parity vs. the D3D12 renderer itself is "parity unpinned" (no D3D12/DXC exists here).
+ */
+#ifndef DCRT_ORACLE_H_
+#define DCRT_ORACLE_H_
+
+#include "../include/dcrt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORACLE_MODE_WAVEFRONT  0   /* WavefrontPathTracing.hlsl state machine (per path)  */
+#define ORACLE_MODE_MEGAKERNEL 1   /* MegakernelPathTracing.hlsl:110-208                  */
+
+typedef struct oracle_counters {
+    uint64_t extension_rays;
+    uint64_t shadow_rays;
+    uint64_t node_visits;       /* iterationCounter semantics, BVHAccel.inc.hlsl:121 */
+    uint64_t triangle_tests;
+    uint64_t blas_entries;
+    uint64_t shadow_node_visits;
+    uint64_t shadow_triangle_tests;
+    uint64_t shadow_blas_entries;
+} oracle_counters;
+
+/* Render pixels [x0,x0+w) x [y0,y0+h) of image `frame->frame_seed`; writes the
+ * sample textures (position W*H*2, value W*H*4, alpha lane = 0) at full-film
+ * addressing, and optionally the terminal RNG state (W*H*4). */
+int oracle_render(const dcrt_flat_scene* scene, const dcrt_bxdf_luts* luts, const dcrt_frame_params* frame,
+                  int mode, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                  float* sample_position, float* sample_value, uint32_t* rng_state,
+                  oracle_counters* counters, int num_threads);
+
+/* SampleConvolution.hlsl:67-106 over the whole film. */
+void oracle_sample_convolution(const dcrt_filter_params* filter, uint32_t width, uint32_t height,
+                               const float* sample_position, const float* sample_value, float* film_rgba,
+                               uint32_t row_begin, uint32_t row_end);
+
+/* BVHIntersectNoInterp / BVHIntersect over a ray batch (BVHAccel.inc.hlsl:85-369). */
+void oracle_trace_rays(const dcrt_flat_scene* scene, const dcrt_ray* rays, uint32_t count, dcrt_ray_hit* hits,
+                       uint32_t features, oracle_counters* counters);
+void oracle_occluded(const dcrt_flat_scene* scene, const dcrt_ray* rays, uint32_t count, uint32_t* occluded,
+                     uint32_t features, oracle_counters* counters);
+
+/* BxDFTexturesBuilding.hlsl restated. which: 0 = BRDF, 1 = BRDF dielectric, 2 = BSDF.
+ * Integrates texels [texel_begin, texel_end) of that table's R32 accumulation
+ * image (full MC, all batches) into out_float; `finalize` converts whole tables. */
+void oracle_lut_integrate(int which, uint32_t texel_begin, uint32_t texel_end, float* out_float);
+void oracle_lut_finalize(const float* brdf_f32, const float* brdf_dielectric_f32, const float* bsdf_f32,
+                         dcrt_bxdf_luts* out_luts);
+int oracle_build_luts(dcrt_bxdf_luts* out_luts, int num_threads);
+
+/* RNG / sampling primitives for known-answer tests (Samples.inc.hlsl, Xoshiro.inc.hlsl). */
+void oracle_rng_init(uint32_t px, uint32_t py, uint32_t frame_seed, uint32_t state[4]);
+uint32_t oracle_rng_next(uint32_t state[4]);
+void oracle_splitmix64_pair(uint32_t lo, uint32_t hi, uint32_t out[6]);
+uint32_t oracle_morton(uint32_t x, uint32_t y);
+void oracle_xoshiro_jump(uint32_t state[4]);
+void oracle_offset_ray_origin(const float p[3], const float n[3], const float d[3], float out[3]);
+void oracle_generate_camera_ray(const dcrt_frame_params* frame, uint32_t px, uint32_t py, float origin[3],
+                                float direction[3], uint32_t rng_out[4]);
+/* function: 0 sin, 1 cos, 2 exp, 3 atan */
+void oracle_math_eval(int function, const float* x, uint32_t count, float* y);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

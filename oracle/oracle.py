@@ -1,0 +1,197 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes binding of the CPU oracle (``libdcrt_oracle.so``).
+
+The oracle is a plain-C restatement of the reference's WavefrontPathTracing.hlsl
+path (see dcrt_oracle.c for per-function reference file:line citations). Only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+may import this module; the product (``directcomputeraytracing_amd``) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+ORACLE_LIB = ORACLE_DIR / "build" / "libdcrt_oracle.so"
+
+WAVEFRONT, MEGAKERNEL = 0, 1
+
+
+class OracleCounters(C.Structure):
+    _fields_ = [("extension_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("node_visits", C.c_uint64),
+                ("triangle_tests", C.c_uint64), ("blas_entries", C.c_uint64), ("shadow_node_visits", C.c_uint64),
+                ("shadow_triangle_tests", C.c_uint64), ("shadow_blas_entries", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not ORACLE_LIB.exists():
+        import sys
+        sys.path.insert(0, str(ORACLE_DIR.parent))
+        from directcomputeraytracing_amd.build import build_oracle
+        build_oracle()
+    from directcomputeraytracing_amd import _abi as A
+    lib = C.CDLL(str(ORACLE_LIB))
+    P = C.POINTER
+    U = C.c_uint32
+    lib.oracle_render.restype = C.c_int
+    lib.oracle_render.argtypes = [P(A.FlatScene), P(A.BxDFLuts), P(A.FrameParams), C.c_int, U, U, U, U,
+                                  P(C.c_float), P(C.c_float), P(U), P(OracleCounters), C.c_int]
+    lib.oracle_sample_convolution.restype = None
+    lib.oracle_sample_convolution.argtypes = [P(A.FilterParams), U, U, P(C.c_float), P(C.c_float), P(C.c_float), U, U]
+    lib.oracle_trace_rays.restype = None
+    lib.oracle_trace_rays.argtypes = [P(A.FlatScene), P(A.Ray), U, P(A.RayHit), U, P(OracleCounters)]
+    lib.oracle_occluded.restype = None
+    lib.oracle_occluded.argtypes = [P(A.FlatScene), P(A.Ray), U, P(U), U, P(OracleCounters)]
+    lib.oracle_lut_integrate.restype = None
+    lib.oracle_lut_integrate.argtypes = [C.c_int, U, U, P(C.c_float)]
+    lib.oracle_lut_finalize.restype = None
+    lib.oracle_lut_finalize.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), P(A.BxDFLuts)]
+    lib.oracle_build_luts.restype = C.c_int
+    lib.oracle_build_luts.argtypes = [P(A.BxDFLuts), C.c_int]
+    lib.oracle_rng_init.restype = None
+    lib.oracle_rng_init.argtypes = [U, U, U, P(U)]
+    lib.oracle_rng_next.restype = U
+    lib.oracle_rng_next.argtypes = [P(U)]
+    lib.oracle_splitmix64_pair.restype = None
+    lib.oracle_splitmix64_pair.argtypes = [U, U, P(U)]
+    lib.oracle_morton.restype = U
+    lib.oracle_morton.argtypes = [U, U]
+    lib.oracle_xoshiro_jump.restype = None
+    lib.oracle_xoshiro_jump.argtypes = [P(U)]
+    lib.oracle_offset_ray_origin.restype = None
+    lib.oracle_offset_ray_origin.argtypes = [P(C.c_float)] * 4
+    lib.oracle_generate_camera_ray.restype = None
+    lib.oracle_generate_camera_ray.argtypes = [P(A.FrameParams), U, U, P(C.c_float), P(C.c_float), P(U)]
+    lib.oracle_math_eval.restype = None
+    lib.oracle_math_eval.argtypes = [C.c_int, P(C.c_float), U, P(C.c_float)]
+    _lib = lib
+    return lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _up(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+def default_threads() -> int:
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1), 16))
+
+
+def render(flat, luts, frame, mode=WAVEFRONT, rect=None, rng=False, threads=None):
+    """Render one image (frame.frame_seed) over `rect` (x0, y0, w, h); returns
+    (sample_position HxWx2, sample_value HxWx4, rng HxWx4 or None, counters)."""
+    lib = load()
+    W, H = frame.resolution[0], frame.resolution[1]
+    x0, y0, w, h = rect or (0, 0, W, H)
+    pos = np.zeros((H, W, 2), np.float32)
+    val = np.zeros((H, W, 4), np.float32)
+    st = np.zeros((H, W, 4), np.uint32) if rng else None
+    cnt = OracleCounters()
+    rc = lib.oracle_render(C.byref(flat), C.byref(luts), C.byref(frame), mode, x0, y0, w, h, _fp(pos), _fp(val),
+                           _up(st) if st is not None else None, C.byref(cnt), threads or default_threads())
+    if rc != 0:
+        raise RuntimeError(f"oracle_render failed: {rc}")
+    return pos, val, st, cnt.as_dict()
+
+
+def sample_convolution(filter_params, pos, val, film=None, rows=None):
+    lib = load()
+    H, W = pos.shape[:2]
+    film = np.zeros((H, W, 4), np.float32) if film is None else film
+    r0, r1 = rows or (0, H)
+    lib.oracle_sample_convolution(C.byref(filter_params), W, H, _fp(np.ascontiguousarray(pos)),
+                                  _fp(np.ascontiguousarray(val)), _fp(film), r0, r1)
+    return film
+
+
+def trace_rays(flat, rays, features):
+    from directcomputeraytracing_amd import _abi as A
+    from directcomputeraytracing_amd.tracer import HIT_DTYPE
+    lib = load()
+    hits = np.zeros(len(rays), HIT_DTYPE)
+    cnt = OracleCounters()
+    lib.oracle_trace_rays(C.byref(flat), rays.ctypes.data_as(C.POINTER(A.Ray)), len(rays),
+                          hits.ctypes.data_as(C.POINTER(A.RayHit)), features, C.byref(cnt))
+    return hits, cnt.as_dict()
+
+
+def occluded(flat, rays, features):
+    from directcomputeraytracing_amd import _abi as A
+    lib = load()
+    out = np.zeros(len(rays), np.uint32)
+    cnt = OracleCounters()
+    lib.oracle_occluded(C.byref(flat), rays.ctypes.data_as(C.POINTER(A.Ray)), len(rays), _up(out), features,
+                        C.byref(cnt))
+    return out, cnt.as_dict()
+
+
+def build_luts(threads=None):
+    from directcomputeraytracing_amd import _abi as A
+    lib = load()
+    luts = A.BxDFLuts()
+    if lib.oracle_build_luts(C.byref(luts), threads or default_threads()) != 0:
+        raise RuntimeError("oracle_build_luts failed")
+    return luts
+
+
+def luts_to_arrays(luts) -> dict:
+    return {name: np.ctypeslib.as_array(getattr(luts, name)).copy() for name, _ in luts._fields_}
+
+
+def luts_from_arrays(arrays: dict):
+    from directcomputeraytracing_amd import _abi as A
+    luts = A.BxDFLuts()
+    for name, _ in luts._fields_:
+        dst = np.ctypeslib.as_array(getattr(luts, name))
+        dst[:] = np.asarray(arrays[name], np.uint16).reshape(dst.shape)
+    return luts
+
+
+def rng_init(px, py, seed):
+    lib = load()
+    s = np.zeros(4, np.uint32)
+    lib.oracle_rng_init(px, py, seed, _up(s))
+    return s
+
+
+def rng_next(state):
+    return load().oracle_rng_next(_up(state))
+
+
+def splitmix64_pair(lo, hi):
+    out = np.zeros(6, np.uint32)
+    load().oracle_splitmix64_pair(lo, hi, _up(out))
+    return out
+
+
+def morton(x, y):
+    return load().oracle_morton(x, y)
+
+
+def math_eval(function, x):
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.empty_like(x)
+    load().oracle_math_eval(function, _fp(x), x.size, _fp(y))
+    return y
+
+
+def camera_ray(frame, px, py):
+    o = np.zeros(3, np.float32)
+    d = np.zeros(3, np.float32)
+    r = np.zeros(4, np.uint32)
+    load().oracle_generate_camera_ray(C.byref(frame), px, py, _fp(o), _fp(d), _up(r))
+    return o, d, r
