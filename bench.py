@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s and ms/spp, Cornell box 1920x1080, 8-bounce wavefront.
+
+A *step* is one sample-per-pixel image (frame seed = step index) rendered by the
+wavefront pipeline over the whole film (all ranks together) and convolved into
+the fp32 film. ``--gpus N`` > 1 is launched by torch.distributed.run: each rank
+renders its round-robin stripes (+halo) of the same film and one RCCL reduce
+of the RGBA32F film closes the timed region.
+
+Prints ONE JSON line (rank 0). Besides the contract fields it carries
+``roofline`` (EXTENSION_RAY_CAST: algorithmic bytes / HIP-event kernel time
+against the MI355X HBM peak) and ``cpu_baseline`` (the oracle's scalar
+MegakernelPathTracing restatement on this host's cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+EXT_RAY_BYTES = 4 + 32 + 20    # queue index + SRay + SRayHit
+NODE_BYTES, TRI_BYTES, BLAS_BYTES = 32, 48, 56
+SHADOW_RAY_BYTES = 4 + 32 + 4 + 4
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64, help="timed images (1 spp each); configs[1] is 64 spp")
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--pool", type=int, default=1 << 21, help="path pool slots")
+    ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
+    ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
+    ap.add_argument("--roofline-images", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per EXTENSION_RAY_CAST launch (from tools/pmc_traffic.py), if present")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, luts_arrays, seconds: float) -> dict:
+    """Oracle megakernel (MegakernelPathTracing.hlsl restated in C) on host cores, bounded."""
+    import oracle  # cpu_baseline leg only
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 16))
+    luts = oracle.luts_from_arrays(luts_arrays)
+    flat = scene.flat()
+    fr = scene.frame_params(0)
+    W, H = fr.resolution[0], fr.resolution[1]
+    # calibrate on 16 centre rows, then time one centred band sized to ~`seconds`
+    t0 = time.perf_counter()
+    oracle.render(flat, luts, fr, oracle.MEGAKERNEL, rect=(0, (H - 16) // 2, W, 16), threads=threads)
+    rate = 16 / max(time.perf_counter() - t0, 1e-6)
+    done_rows = int(min(H, max(16, rate * seconds)))
+    t0 = time.perf_counter()
+    _, _, _, c = oracle.render(flat, luts, fr, oracle.MEGAKERNEL, rect=(0, (H - done_rows) // 2, W, done_rows),
+                               threads=threads)
+    elapsed = time.perf_counter() - t0
+    rays = c["extension_rays"] + c["shadow_rays"]
+    mrays = rays / elapsed / 1e6
+    return {"value": round(mrays, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"oracle megakernel (scalar C restatement of MegakernelPathTracing.hlsl), {W}x{done_rows} "
+                      f"rows of the 1920x1080 8-bounce Cornell image (seed 0, 1 spp), {elapsed:.1f} s",
+            "ms_per_spp_extrapolated": round(elapsed * 1e3 * H / done_rows, 1)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import numpy as np
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
+    luts_arrays = dict(np.load(ROOT / "tests" / "golden" / "bxdf_luts.npz"))
+
+    scene = Scene((args.width, args.height))
+    scenes.setup_cornell(scene, args.width, args.height, args.bounces)
+    tracer = WavefrontPathTracer(path_pool_size=args.pool, iterations_per_render=args.iterations, device=local_rank)
+    tracer.on_scene_loaded(scene)
+    if world > 1:
+        tracer.set_film_partition(world, rank, args.stripe)
+    filt = scene.filter_params()
+
+    def barrier_sync():
+        tracer.synchronize()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    film_buf = None
+    if dist is not None:
+        import torch
+        film_buf = torch.empty(args.width * args.height * 4, dtype=torch.float32, device="cuda")
+
+    # warmup (also builds the graphs)
+    tracer.clear_film()
+    if args.warmup:
+        tracer.render_images(10_000, args.warmup, filt)
+    tracer.clear_film()
+    tracer.reset_stats()
+    barrier_sync()
+    t0 = time.perf_counter()
+    tracer.render_images(0, args.steps, filt)
+    if dist is not None:
+        tracer.copy_film_device(film_buf.data_ptr())
+        dist.reduce(film_buf, dst=0, op=dist.ReduceOp.SUM)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    c = tracer.counters()
+    rays = c["extension_rays"] + c["shadow_rays"]
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda")
+        tmax = t[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed, rays = float(tmax.item()), float(tsum.item())
+
+    # ---- roofline leg: same workload (seeds 0..R-1), counters then HIP-event timing
+    R = max(1, args.roofline_images)
+    tracer.set_instrumentation(True, False)
+    tracer.reset_stats()
+    tracer.render_images(0, R, filt)
+    st = tracer.traversal_stats()
+    cr = tracer.counters()
+    tracer.set_instrumentation(False, True)
+    tracer.reset_stats()
+    tracer.render_images(0, R, filt)
+    tm = tracer.traversal_stats()
+    tracer.set_instrumentation(False, False)
+    ext_bytes = (EXT_RAY_BYTES * cr["extension_rays"] + NODE_BYTES * st["ext_node_visits"]
+                 + TRI_BYTES * st["ext_triangle_tests"] + BLAS_BYTES * st["ext_blas_entries"])
+    launches = max(1, tm["ext_launches"])
+    avg_ms = tm["ext_kernel_ms"] / launches
+    bytes_per_launch = ext_bytes / launches
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    tj = Path(args.traffic_json)
+    if tj.exists():
+        try:
+            traffic = json.loads(tj.read_text()).get("ext_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": "Mrays/s and ms/spp at 1920x1080, 8-bounce wavefront",
+        "value": round(rays / elapsed / 1e6, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+        "ms_per_spp": round(elapsed * 1e3 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak" if world > 1 else "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"cornell_box_obj {args.width}x{args.height}, {args.steps} spp (1 spp/step), "
+                               f"{args.bounces} bounces, wavefront, point light",
+                   "resolution": [args.width, args.height], "spp": args.steps, "max_bounce": args.bounces,
+                   "path_pool": args.pool, "parallelism": f"film stripes x{world}" if world > 1 else "single GPU",
+                   "rays": int(rays)},
+        "roofline": {"bound": "hbm", "kernel": "extension_kernel (EXTENSION_RAY_CAST)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 2),
+                     "launches": int(launches),
+                     "per_ray": {"nodes": st["ext_node_visits"] / max(1, cr["extension_rays"]),
+                                 "tris": st["ext_triangle_tests"] / max(1, cr["extension_rays"]),
+                                 "blas": st["ext_blas_entries"] / max(1, cr["extension_rays"])}},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(scene, luts_arrays, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    tracer.destroy()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

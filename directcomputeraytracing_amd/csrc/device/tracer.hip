@@ -750,6 +750,16 @@ DCRT_API int dcrt_tracer_film_device_ptr(dcrt_tracer* t, void** out)
     return DCRT_OK;
 }
 
+DCRT_API int dcrt_tracer_copy_film_device(dcrt_tracer* t, void* d_dst)
+{
+    TRACER_GUARD(t);
+    if (!d_dst || !t->film.accum) return DCRT_E_INVALID_ARG;
+    HIPCHECK(hipMemcpyAsync(d_dst, t->film.accum, (size_t)t->filmW * t->filmH * sizeof(float4), hipMemcpyDeviceToDevice,
+                            t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    return DCRT_OK;
+}
+
 DCRT_API int dcrt_tracer_counters(dcrt_tracer* t, dcrt_ray_stats* out)
 {
     TRACER_GUARD(t);

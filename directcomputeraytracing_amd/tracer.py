@@ -126,6 +126,9 @@ class WavefrontPathTracer:
         check(self._lib.dcrt_tracer_film_device_ptr(self._h, C.byref(p)), "FilmDevicePtr")
         return p.value or 0
 
+    def copy_film_device(self, d_dst: int) -> None:
+        check(self._lib.dcrt_tracer_copy_film_device(self._h, C.c_void_p(d_dst)), "CopyFilmDevice")
+
     # ---- statistics ----------------------------------------------------------
     def counters(self) -> dict:
         s = _abi.RayStats()

@@ -333,6 +333,9 @@ DCRT_API int dcrt_tracer_read_film(dcrt_tracer* tracer, float* out_rgba);       
 DCRT_API int dcrt_tracer_read_samples(dcrt_tracer* tracer, float* out_position, float* out_value); /* W*H*2, W*H*4 */
 DCRT_API int dcrt_tracer_read_rng(dcrt_tracer* tracer, uint32_t* out_state);                   /* W*H*4 (debug_rng) */
 DCRT_API int dcrt_tracer_film_device_ptr(dcrt_tracer* tracer, void** out_ptr);
+/* Device-to-device copy of the RGBA32F film (W*H*4 floats) into d_dst, e.g. an
+ * RCCL buffer for the multi-GPU reduce; synchronous with the tracer stream. */
+DCRT_API int dcrt_tracer_copy_film_device(dcrt_tracer* tracer, void* d_dst);
 DCRT_API int dcrt_tracer_counters(dcrt_tracer* tracer, dcrt_ray_stats* out_stats);
 /* counters != 0: traversal work counters in the cast kernels; ext_timing != 0: plain
  * (non-graph) launches with HIP events around every EXTENSION_RAY_CAST launch. */

@@ -1028,7 +1028,7 @@ static void ct_brdf_sample(v3 wo, f2 sample, float alpha, v3* wi, lctx* c) /* :1
     *wi = vneg(reflect3(wo, m));
     lctx_assign_h(wo, m, c);
 }
-static int g_refraction_no_scale;   /* REFRACTION_NO_SCALE_FACTOR (LUT builder only) */
+static _Thread_local int g_refraction_no_scale;   /* REFRACTION_NO_SCALE_FACTOR (LUT builder only; per thread) */
 static float ct_bsdf(v3 wi, v3 wo, float alpha, float etaO, float etaI)   /* :152-189 */
 {
     int active = wo.z != 0.0f && wi.z != 0.0f;
@@ -1620,6 +1620,7 @@ int oracle_render(const dcrt_flat_scene* sc, const dcrt_bxdf_luts* luts, const d
                   oracle_counters* counters, int num_threads)
 {
     if (!sc || !luts || !f || !pos || !val) return DCRT_E_INVALID_ARG;
+    if ((uint64_t)x0 + w > f->resolution[0] || (uint64_t)y0 + h > f->resolution[1]) return DCRT_E_INVALID_ARG;
     init_srgb();
     g_luts = luts;
     g_vndf = (f->features & DCRT_FEATURE_GGX_SAMPLE_VNDF) != 0;

@@ -1,0 +1,72 @@
+"""C-ABI surface: the library loads and exports every symbol include/*.h declares."""
+import ctypes as C
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    names = []
+    for h in (ROOT / "include").glob("*.h"):
+        names += re.findall(r"DCRT_API\s+[\w\s\*]+?\b(dcrt_\w+)\s*\(", h.read_text())
+    return sorted(set(names))
+
+
+def test_header_declares_api():
+    names = _declared()
+    assert "dcrt_tracer_create" in names and "dcrt_scene_load_from_file" in names
+    assert len(names) >= 45
+
+
+def test_library_exports_every_declared_symbol(native_lib):
+    missing = [n for n in _declared() if not hasattr(native_lib, n)]
+    assert not missing, missing
+
+
+def test_python_mirror_binds_every_symbol():
+    from directcomputeraytracing_amd import _abi
+    bound = {n for n, _, _ in _abi.SIGNATURES}
+    assert bound == set(_declared())
+
+
+def test_struct_sizes_match_header(native_lib):
+    from directcomputeraytracing_amd import _abi
+    assert C.sizeof(_abi.Vertex) == 44
+    assert C.sizeof(_abi.BVHNode) == 32
+    assert C.sizeof(_abi.Material) == 52
+    assert C.sizeof(_abi.Light) == 28
+    assert C.sizeof(_abi.Float4x3) == 48
+    assert C.sizeof(_abi.Ray) == 32
+    assert C.sizeof(_abi.RayHit) == 20
+
+
+def test_version_and_errors(native_lib):
+    from directcomputeraytracing_amd import DCRTError, Scene, version
+    assert "gfx950" in version()
+    s = Scene((64, 64))
+    with pytest.raises(DCRTError):
+        s.load_from_file(ROOT / "tests" / "golden" / "does_not_exist.obj")
+    with pytest.raises(DCRTError):
+        s.reset(0, 0)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    from directcomputeraytracing_amd import _abi
+    saved = _abi._lib
+    _abi._lib = None
+    try:
+        with pytest.raises(_abi.DCRTError):
+            _abi.load_library(tmp_path / "libdcrt.so")
+    finally:
+        _abi._lib = saved
+
+
+def test_tracer_without_device_reports_no_device(native_lib):
+    """No GPU here: Create must fail with an error, never fall back to the CPU."""
+    from directcomputeraytracing_amd import DCRTError, WavefrontPathTracer, device_count
+    if device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(DCRTError, match="NO_DEVICE"):
+        WavefrontPathTracer(path_pool_size=1024)

@@ -1,0 +1,196 @@
+"""GPU parity: the gfx950 path (through the C ABI) against the CPU oracle.
+
+Bar: integer state (RNG, hit indices, counters) is
+bit-exact; the float outputs are also required bit-exact here because both
+sides compile without contraction and with IEEE div/sqrt and share the same
+deterministic transcendentals (DESIGN.md "Numerics"). Where a float
+comparison is not bit-exact the tolerance is stated in the assertion.
+"""
+import numpy as np
+import pytest
+
+from conftest import cornell
+
+pytestmark = pytest.mark.gpu
+
+
+def _rays(n, seed, room=True):
+    from directcomputeraytracing_amd import make_rays
+    rng = np.random.default_rng(seed)
+    if room:
+        o = rng.uniform([-1.4, 0.05, 1.05], [1.4, 1.95, 4.4], size=(n, 3))
+    else:
+        o = rng.uniform([-3, -1, -3], [3, 3, 0], size=(n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    # axis-aligned directions exercise the infinite-inverse slab path
+    k = n // 16
+    d[:k] = 0.0
+    d[np.arange(k), rng.integers(0, 3, k)] = rng.choice([-1.0, 1.0], k)
+    r = make_rays(o, d, 0.0, np.inf)
+    r["t_max"][n // 2: n // 2 + n // 8] = rng.uniform(0.1, 2.0, n // 8)
+    return r
+
+
+def test_device_math_matches_oracle(gpu_tracer, oracle_mod):
+    rng = np.random.default_rng(7)
+    xs = [rng.uniform(-7, 7, 100000), rng.uniform(-100, 100, 20000), rng.uniform(-20, 20, 20000),
+          rng.standard_normal(20000) * 1e-3, np.array([0.0, -0.0, 1.0, -1.0, 3.14159265, 1e-30, 88.0, -88.0])]
+    x = np.concatenate(xs).astype(np.float32)
+    for fn in range(4):
+        y_gpu = gpu_tracer.math_eval(fn, x)
+        y_cpu = oracle_mod.math_eval(fn, x)
+        assert np.array_equal(y_gpu.view(np.uint32), y_cpu.view(np.uint32)), f"function {fn}"
+
+
+def test_bxdf_luts_match_golden(gpu_tracer, golden_luts, oracle_mod):
+    gpu = oracle_mod.luts_to_arrays(gpu_tracer.luts())
+    ref = oracle_mod.luts_to_arrays(golden_luts)
+    for k in ref:
+        diff = np.abs(gpu[k].astype(np.int64) - ref[k].astype(np.int64))
+        assert diff.max() == 0, f"{k}: {np.count_nonzero(diff)} texels differ, max {diff.max()} LSB"
+
+
+@pytest.mark.parametrize("features", [0x0D, 0x05, 0x0F, 0x07])
+def test_trace_rays_bit_exact(gpu_tracer, golden_luts, oracle_mod, features):
+    s = cornell(64, 64, 2)
+    gpu_tracer.on_scene_loaded(s)
+    flat = s.flat()
+    for room in (True, False):
+        rays = _rays(50000, 11 + features + room, room)
+        h_gpu = gpu_tracer.trace_rays(rays, features)
+        h_cpu, _ = oracle_mod.trace_rays(flat, rays, features)
+        assert np.array_equal(h_gpu.view(np.uint8), h_cpu.view(np.uint8))
+        o_gpu = gpu_tracer.occluded(rays, features)
+        o_cpu, _ = oracle_mod.occluded(flat, rays, features)
+        assert np.array_equal(o_gpu, o_cpu)
+
+
+def _render_and_compare(tracer, oracle_mod, luts, scene, seeds):
+    tracer.set_luts(luts)
+    tracer.on_scene_loaded(scene)
+    flat = scene.flat()
+    for seed in seeds:
+        fr = scene.frame_params(seed)
+        tracer.set_frame_params(fr)
+        tracer.reset_image()
+        for _ in range(10000):
+            tracer.render()
+            if tracer.is_image_complete():
+                break
+        assert tracer.is_image_complete()
+        pos, val = tracer.read_samples()
+        rng = tracer.read_rng()
+        p_ref, v_ref, r_ref, c_ref = oracle_mod.render(flat, luts, fr, oracle_mod.WAVEFRONT, rng=True)
+        assert np.array_equal(rng, r_ref), f"seed {seed}: RNG state differs at {np.count_nonzero((rng != r_ref).any(-1))} px"
+        assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32)), f"seed {seed}: sample positions"
+        bad = np.count_nonzero((val.view(np.uint32) != v_ref.view(np.uint32)).any(-1))
+        assert bad == 0, f"seed {seed}: {bad} pixels differ; max |d| {np.abs(val - v_ref).max()}"
+        c = tracer.counters()
+        yield c, c_ref
+
+
+def test_render_config1_bit_exact(gpu_tracer, golden_luts, oracle_mod):
+    """configs[0]: Cornell box 128x128, 1 spp, maxBounce 2."""
+    s = cornell(128, 128, 2)
+    for c, c_ref in _render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0]):
+        pass
+
+
+def test_render_8_bounces_odd_size_bit_exact(gpu_tracer, golden_luts, oracle_mod):
+    """Ragged film (not a multiple of the 8x8 block), 8 bounces, several seeds."""
+    s = cornell(133, 77, 8)
+    list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 1, 5]))
+
+
+def test_render_full_1080p_one_spp_bit_exact(native_lib, golden_luts, oracle_mod):
+    """configs[1] resolution and depth: 1920x1080, 8 bounces, one image, whole film."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    t = WavefrontPathTracer(path_pool_size=1 << 21, iterations_per_render=16, debug_rng=True)
+    try:
+        s = cornell(1920, 1080, 8)
+        list(_render_and_compare(t, oracle_mod, golden_luts, s, [3]))
+    finally:
+        t.destroy()
+
+
+def test_film_accumulation_matches_oracle(native_lib, golden_luts, oracle_mod):
+    from directcomputeraytracing_amd import FILTER_BOX, FILTER_GAUSSIAN, FILTER_MITCHELL, FilterParams, \
+        WavefrontPathTracer
+    t = WavefrontPathTracer(path_pool_size=1 << 16)
+    try:
+        s = cornell(96, 64, 3)
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        flat = s.flat()
+        for filt in (FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3),
+                     FilterParams(FILTER_GAUSSIAN, 1.5, 2.0, 1 / 3, 1 / 3, 3),
+                     FilterParams(FILTER_MITCHELL, 2.0, 1.5, 1 / 3, 1 / 3, 3)):
+            t.clear_film()
+            t.render_images(0, 3, filt)
+            film = t.read_film()
+            ref = np.zeros_like(film)
+            for seed in range(3):
+                p, v, _, _ = oracle_mod.render(flat, golden_luts, s.frame_params(seed), oracle_mod.WAVEFRONT)
+                oracle_mod.sample_convolution(filt, p, v, ref)
+            assert np.array_equal(film.view(np.uint32), ref.view(np.uint32)), \
+                f"filter {filt.filter}: max |d| {np.abs(film - ref).max()}"
+    finally:
+        t.destroy()
+
+
+def test_film_partition_sums_to_single_gpu(native_lib, golden_luts):
+    """Stripes + halo per rank: the rank films sum to the 1-GPU film exactly."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    s = cornell(160, 120, 3)
+    films = []
+    for world, rank in [(1, 0), (3, 0), (3, 1), (3, 2)]:
+        t = WavefrontPathTracer(path_pool_size=1 << 15)
+        try:
+            t.set_luts(golden_luts)
+            t.on_scene_loaded(s)
+            t.set_film_partition(world, rank, 16)
+            t.clear_film()
+            t.render_images(0, 2)
+            films.append(t.read_film())
+        finally:
+            t.destroy()
+    total = films[1] + films[2] + films[3]
+    assert np.array_equal(total.view(np.uint32), films[0].view(np.uint32))
+
+
+def test_traversal_counters_match_oracle(native_lib, golden_luts, oracle_mod):
+    """Instrumented casts count the same AABB/triangle/BLAS work as the oracle (bytes/ray basis)."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    t = WavefrontPathTracer(path_pool_size=1 << 16)
+    try:
+        s = cornell(128, 96, 4)
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        t.set_instrumentation(True, True)
+        t.reset_stats()
+        t.render_images(2, 1)
+        st = t.traversal_stats()
+        c = t.counters()
+        _, _, _, ref = oracle_mod.render(s.flat(), golden_luts, s.frame_params(2), oracle_mod.WAVEFRONT)
+        assert c["extension_rays"] == ref["extension_rays"]
+        assert c["shadow_rays"] == ref["shadow_rays"]
+        assert st["ext_node_visits"] == ref["node_visits"]
+        assert st["ext_triangle_tests"] == ref["triangle_tests"]
+        assert st["ext_blas_entries"] == ref["blas_entries"]
+        assert st["shadow_node_visits"] == ref["shadow_node_visits"]
+        assert st["shadow_triangle_tests"] == ref["shadow_triangle_tests"]
+        assert st["shadow_blas_entries"] == ref["shadow_blas_entries"]
+        assert st["ext_launches"] > 0 and st["ext_kernel_ms"] > 0
+    finally:
+        t.destroy()
+
+
+def test_missing_scene_fails_loudly(native_lib):
+    from directcomputeraytracing_amd import DCRTError, WavefrontPathTracer
+    t = WavefrontPathTracer(path_pool_size=1 << 12)
+    try:
+        with pytest.raises(DCRTError):
+            t.render()
+    finally:
+        t.destroy()

@@ -1,0 +1,20 @@
+#!/bin/bash
+# GPU-box check: smoke, GPU parity tests, short bench, kernel-trace profile.
+# Every GPU step has its own time limit; a fault/abort/timeout ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; ok $rc || exit $rc
+timeout -k 10 600 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; ok $rc || exit $rc
+timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
+if [ -n "${PROFILE:-}" ]; then
+  ROOTDIR=$(pwd)
+  export TMPDIR=/tmp
+  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOTDIR/gpurun_out/prof" -o run -- \
+      python3 "$ROOTDIR/bench.py" --steps 16 --warmup 1 --no-cpu-baseline > "$ROOTDIR/gpurun_out/prof.log" 2>&1)
+  rc=$?; echo "rocprof rc=$rc"; exit $rc
+fi
