@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mrays/s and ms/spp, Cornell box 1920x1080, 8-bounce wavefront.
 
-A *step* is one sample-per-pixel image (frame seed = step index) rendered by the
-wavefront pipeline over the whole film (all ranks together) and convolved into
-the fp32 film. ``--gpus N`` > 1 is launched by torch.distributed.run: each rank
-renders its round-robin stripes (+halo) of the same film and one RCCL reduce
-of the RGBA32F film closes the timed region.
+A *step* is N one-sample-per-pixel images of the full film (N = number of GPUs;
+frame seed = image index), rendered by the wavefront pipeline and convolved
+into the fp32 film. Each rank renders its round-robin stripes (+halo) of every
+image, so per-GPU work per step is one full image: weak scaling. ``--gpus N``
+> 1 is launched by torch.distributed.run; one RCCL reduce of the RGBA32F film
+closes the timed region.
 
 Prints ONE JSON line (rank 0). Besides the contract fields it carries
 ``roofline`` (EXTENSION_RAY_CAST: algorithmic bytes / HIP-event kernel time
@@ -44,8 +45,8 @@ def parse():
     ap.add_argument("--roofline-images", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
-                    help="PMC-derived HBM bytes per EXTENSION_RAY_CAST launch (from tools/pmc_traffic.py), if present")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary from tools/pmc_traffic.py (default: newest profiles/r*_pmc_traffic.json)")
     return ap.parse_args()
 
 
@@ -57,20 +58,29 @@ def cpu_baseline(scene, luts_arrays, seconds: float) -> dict:
     flat = scene.flat()
     fr = scene.frame_params(0)
     W, H = fr.resolution[0], fr.resolution[1]
-    # calibrate on 16 centre rows, then time one centred band sized to ~`seconds`
+    # whole 1-spp images (seeds 0, 1, ...) until about `seconds` of CPU time; if one
+    # image would take far longer, a centred band of rows sized from a 16-row probe
     t0 = time.perf_counter()
     oracle.render(flat, luts, fr, oracle.MEGAKERNEL, rect=(0, (H - 16) // 2, W, 16), threads=threads)
     rate = 16 / max(time.perf_counter() - t0, 1e-6)
-    done_rows = int(min(H, max(16, rate * seconds)))
-    t0 = time.perf_counter()
-    _, _, _, c = oracle.render(flat, luts, fr, oracle.MEGAKERNEL, rect=(0, (H - done_rows) // 2, W, done_rows),
-                               threads=threads)
-    elapsed = time.perf_counter() - t0
-    rays = c["extension_rays"] + c["shadow_rays"]
+    band = int(min(H, max(16, rate * seconds)))
+    rays, elapsed, images = 0, 0.0, 0
+    while elapsed < seconds:
+        fr_s = scene.frame_params(images)
+        t0 = time.perf_counter()
+        _, _, _, c = oracle.render(flat, luts, fr_s, oracle.MEGAKERNEL, rect=(0, (H - band) // 2, W, band),
+                                   threads=threads)
+        elapsed += time.perf_counter() - t0
+        rays += c["extension_rays"] + c["shadow_rays"]
+        images += 1
+        if band < H:
+            break
+    done_rows = band * images
     mrays = rays / elapsed / 1e6
     return {"value": round(mrays, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"oracle megakernel (scalar C restatement of MegakernelPathTracing.hlsl), {W}x{done_rows} "
-                      f"rows of the 1920x1080 8-bounce Cornell image (seed 0, 1 spp), {elapsed:.1f} s",
+                      f"rows ({images} image(s) of {band} rows, seeds 0..{images - 1}) of the 1920x1080 8-bounce Cornell "
+                      f"image at 1 spp, {elapsed:.1f} s",
             "ms_per_spp_extrapolated": round(elapsed * 1e3 * H / done_rows, 1)}
 
 
@@ -118,7 +128,8 @@ def main():
     tracer.reset_stats()
     barrier_sync()
     t0 = time.perf_counter()
-    tracer.render_images(0, args.steps, filt)
+    images = args.steps * world            # weak scaling: each step is one image per GPU-equivalent
+    tracer.render_images(0, images, filt)
     if dist is not None:
         tracer.copy_film_device(film_buf.data_ptr())
         dist.reduce(film_buf, dst=0, op=dist.ReduceOp.SUM)
@@ -155,7 +166,8 @@ def main():
     bytes_per_launch = ext_bytes / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     traffic = None
-    tj = Path(args.traffic_json)
+    cands = sorted((ROOT / "profiles").glob("r*_pmc_traffic.json"))
+    tj = Path(args.traffic_json) if args.traffic_json else (cands[-1] if cands else Path("/nonexistent"))
     if tj.exists():
         try:
             traffic = json.loads(tj.read_text()).get("ext_hbm_bytes_per_launch")
@@ -170,15 +182,15 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
-        "ms_per_spp": round(elapsed * 1e3 / args.steps, 3),
+        "ms_per_spp": round(elapsed * 1e3 / images, 3),
         "higher_is_better": True,
-        "scaling": "weak" if world > 1 else "weak",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": f"cornell_box_obj {args.width}x{args.height}, {args.steps} spp (1 spp/step), "
-                               f"{args.bounces} bounces, wavefront, point light",
-                   "resolution": [args.width, args.height], "spp": args.steps, "max_bounce": args.bounces,
+        "config": {"workload": f"cornell_box_obj {args.width}x{args.height}, {images} spp ({world} spp/step, film "
+                               f"stripes across {world} GPU(s)), {args.bounces} bounces, wavefront, point light",
+                   "resolution": [args.width, args.height], "spp": images, "max_bounce": args.bounces,
                    "path_pool": args.pool, "parallelism": f"film stripes x{world}" if world > 1 else "single GPU",
                    "rays": int(rays)},
         "roofline": {"bound": "hbm", "kernel": "extension_kernel (EXTENSION_RAY_CAST)",

@@ -1,0 +1,92 @@
+"""Film partitioning across ranks on CPU with gloo, world size 2.
+
+Each rank path-traces only the 8-row bands of its round-robin stripes plus
+halo (directcomputeraytracing_amd.partition, mirroring dcrt_tracer::BuildBands),
+convolves only the rows it owns, and one reduce(SUM) of the RGBA32F film
+yields the single-rank film bit for bit. The per-rank rendering here is the
+oracle (no GPU in this container); the GPU path is covered by
+test_gpu_parity.py::test_film_partition_sums_to_single_gpu.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+
+def test_partition_rows_cover_film():
+    from directcomputeraytracing_amd.partition import owned_rows, render_bands
+    H, S = 1080, 64
+    for world in (1, 2, 3, 4, 8):
+        owners = np.stack([owned_rows(H, world, r, S) for r in range(world)])
+        assert np.all(owners.sum(0) == 1)                      # every row owned exactly once
+        for r in range(world):
+            bands = render_bands(H, world, r, S)
+            covered = np.zeros(H, bool)
+            for y in bands:
+                covered[y:y + 8] = True
+            own = np.nonzero(owners[r])[0]
+            for y in own:                                      # owned rows +- 2-row halo rendered
+                assert covered[max(0, y - 2):min(H, y + 3)].all()
+        if world > 1:
+            extra = sum(len(render_bands(H, world, r, S)) for r in range(world)) * 8 / H - 1
+            assert extra < 0.3                                 # halo overhead at S = 64
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, str(ROOT))
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle
+    from directcomputeraytracing_amd import FILTER_BOX, FilterParams, Scene, scenes
+    from directcomputeraytracing_amd.partition import owned_row_ranges, render_bands
+    W, H, S = 96, 80, 16
+    s = Scene((W, H))
+    scenes.setup_cornell(s, W, H, 3)
+    luts = oracle.luts_from_arrays(dict(np.load(GOLDEN / "bxdf_luts.npz")))
+    filt = FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3)
+    film = np.zeros((H, W, 4), np.float32)
+    for seed in range(2):
+        fr = s.frame_params(seed)
+        pos = np.zeros((H, W, 2), np.float32)
+        val = np.zeros((H, W, 4), np.float32)
+        for y in render_bands(H, world, rank, S):
+            h = min(8, H - y)
+            p, v, _, _ = oracle.render(s.flat(), luts, fr, oracle.WAVEFRONT, rect=(0, y, W, h), threads=1)
+            pos[y:y + h], val[y:y + h] = p[y:y + h], v[y:y + h]
+        for (r0, r1) in owned_row_ranges(H, world, rank, S):
+            oracle.sample_convolution(filt, pos, val, film, rows=(r0, r1))
+    t = torch.from_numpy(film)
+    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "film_reduced.npy"), t.numpy())
+    dist.destroy_process_group()
+
+
+def test_gloo_two_rank_film_reduce_is_bit_exact(tmp_path, oracle_mod, golden_luts):
+    import torch.multiprocessing as mp
+    from directcomputeraytracing_amd import FILTER_BOX, FilterParams, Scene, scenes
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    reduced = np.load(tmp_path / "film_reduced.npy")
+    W, H = 96, 80
+    s = Scene((W, H))
+    scenes.setup_cornell(s, W, H, 3)
+    filt = FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3)
+    ref = np.zeros((H, W, 4), np.float32)
+    for seed in range(2):
+        p, v, _, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(seed), oracle_mod.WAVEFRONT)
+        oracle_mod.sample_convolution(filt, p, v, ref)
+    assert np.array_equal(reduced.view(np.uint32), ref.view(np.uint32))

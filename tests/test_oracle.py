@@ -1,0 +1,217 @@
+"""CPU oracle pinned against independent restatements and the committed golden fixtures.
+
+The reference's D3D12 shaders cannot run here (no Windows/DXC), so the oracle
+is pinned by: (1) independent Python/numpy restatements of the integer
+primitives (SplitMix64, xoshiro128**, Morton) from their published algorithms
+as used by Samples.inc.hlsl / Xoshiro.inc.hlsl / UInt64.inc.hlsl; (2) the
+golden BxDF LUT fixture (tests/golden/make_golden.py) recomputed texel by texel;
+(3) brute-force geometry checks of the BVH traversal; (4) internal
+consistency of the two oracle modes (wavefront vs megakernel).
+"""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, cornell
+
+M64 = (1 << 64) - 1
+M32 = (1 << 32) - 1
+
+
+def splitmix64(state):
+    state = (state + 0x9E3779B97F4A7C15) & M64
+    z = state
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return state, z ^ (z >> 31)
+
+
+def rotl(x, k):
+    return ((x << k) | (x >> (32 - k))) & M32
+
+
+def xoshiro_next(s):
+    """xoshiro128** 1.0 (the scrambler multiplies state[0], Xoshiro.inc.hlsl:18; 1.1 uses state[1])."""
+    result = (rotl((s[0] * 5) & M32, 7) * 9) & M32
+    t = (s[1] << 9) & M32
+    s[2] ^= s[0]
+    s[3] ^= s[1]
+    s[1] ^= s[2]
+    s[0] ^= s[3]
+    s[2] ^= t
+    s[3] = rotl(s[3], 11)
+    return result
+
+
+def morton(x, y):
+    out = 0
+    for b in range(16):
+        out |= ((x >> b) & 1) << (2 * b)
+        out |= ((y >> b) & 1) << (2 * b + 1)
+    return out
+
+
+def test_morton_kat(oracle_mod):
+    rng = np.random.default_rng(1)
+    for x, y in [(0, 0), (1, 0), (0, 1), (65535, 65535), (1919, 1079)] + [tuple(v) for v in rng.integers(0, 65536, (200, 2))]:
+        assert oracle_mod.morton(int(x), int(y)) == morton(int(x), int(y))
+
+
+def test_splitmix64_kat(oracle_mod):
+    rng = np.random.default_rng(2)
+    for _ in range(200):
+        lo, hi = (int(v) for v in rng.integers(0, 1 << 32, 2, dtype=np.uint64))
+        st, a = splitmix64((hi << 32) | lo)
+        st, b = splitmix64(st)
+        out = oracle_mod.splitmix64_pair(lo, hi)
+        assert [int(v) for v in out] == [a & M32, a >> 32, b & M32, b >> 32, st & M32, st >> 32]
+
+
+def test_rng_init_and_stream_kat(oracle_mod):
+    """Pixel seeding (Samples.inc.hlsl:59-70): SplitMix64 of frameSeed<<32 | morton(x,y)."""
+    for px, py, seed in [(0, 0, 0), (17, 3, 1), (1919, 1079, 63), (640, 360, 12345)]:
+        st, a = splitmix64((seed << 32) | morton(px, py))
+        st, b = splitmix64(st)
+        ref = [a & M32, a >> 32, b & M32, b >> 32]
+        s = oracle_mod.rng_init(px, py, seed)
+        assert [int(v) for v in s] == ref
+        for _ in range(64):
+            assert oracle_mod.rng_next(s) == xoshiro_next(ref)
+        assert [int(v) for v in s] == ref
+
+
+def test_golden_luts_recomputed(oracle_mod, golden_luts):
+    """A spread of texels of each table (incl. chunk edges) recomputed single-threaded."""
+    import ctypes as C
+    lib = oracle_mod.load()
+    golden = oracle_mod.luts_to_arrays(golden_luts)
+    tables = {0: ("brdf", 1024), 1: ("brdf_dielectric", 16384), 2: ("bsdf", 16384)}
+    rng = np.random.default_rng(3)
+    for which, (name, n) in tables.items():
+        picks = sorted(set([0, 1, n // 2 - 1, n // 2, n - 2, n - 1] + list(rng.integers(0, n, 10))))
+        for t in picks:
+            out = np.zeros(1, np.float32)
+            lib.oracle_lut_integrate(which, int(t), int(t) + 1, out.ctypes.data_as(C.POINTER(C.c_float)))
+            u16 = int(np.rint(np.clip(out[0], 0.0, 1.0) * np.float32(65535.0)))
+            assert u16 == int(golden[name][t]), f"{name}[{t}]"
+
+
+def test_golden_lut_sanity(golden_luts, oracle_mod):
+    a = oracle_mod.luts_to_arrays(golden_luts)
+    brdf = a["brdf"].reshape(32, 32) / 65535.0          # rows: alpha, cols: cos(theta_o)
+    assert np.all(brdf[0, 1:] > 0.999)                   # perfectly smooth mirror conserves energy
+    assert brdf[-1, 1:].mean() < brdf[0, 1:].mean()      # single scattering loses energy with roughness
+    assert np.all(a["brdf_avg"] <= 65535)
+
+
+def _brute_force_closest(flat_arrays, origins, dirs):
+    """Double-precision Moller-Trumbore over every triangle of every instance."""
+    v = flat_arrays["vertices"][:, :3].astype(np.float64)
+    tri = flat_arrays["triangles"].astype(np.int64)
+    p0, p1, p2 = v[tri[:, 0]], v[tri[:, 1]], v[tri[:, 2]]
+    e1, e2 = p1 - p0, p2 - p0
+    best_t = np.full(len(origins), np.inf)
+    best_id = np.full(len(origins), -1)
+    for i, (o, d) in enumerate(zip(origins.astype(np.float64), dirs.astype(np.float64))):
+        pv = np.cross(d, e2)
+        det = np.einsum("ij,ij->i", e1, pv)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            inv = 1.0 / det
+            tv = o - p0
+            u = np.einsum("ij,ij->i", tv, pv) * inv
+            qv = np.cross(tv, e1)
+            w = (qv @ d) * inv
+            t = np.einsum("ij,ij->i", e2, qv) * inv
+        ok = (np.abs(det) > 1e-12) & (u >= 0) & (w >= 0) & (u + w <= 1) & (t > 0)
+        if ok.any():
+            j = np.where(ok)[0][np.argmin(t[ok])]
+            best_t[i], best_id[i] = t[j], j
+    return best_t, best_id
+
+
+def test_traversal_matches_brute_force(oracle_mod):
+    """BVH build + two-level traversal find the same closest triangle as brute force.
+
+    The Cornell instances carry identity transforms, so world = object space.
+    """
+    from directcomputeraytracing_amd import make_rays
+    s = cornell(32, 32, 2)
+    arr = s.arrays()
+    rng = np.random.default_rng(5)
+    o = rng.uniform([-1.4, 0.05, 1.05], [1.4, 1.95, 4.4], size=(400, 3)).astype(np.float32)
+    d = rng.normal(size=(400, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = make_rays(o, d)
+    hits, cnt = oracle_mod.trace_rays(s.flat(), rays, 0x0D)
+    bt, bid = _brute_force_closest(arr, o, d)
+    hit = np.isfinite(bt)                   # the room is open towards the camera
+    assert hit.mean() > 0.6
+    assert np.array_equal(np.isfinite(hits["t"]), hit)
+    np.testing.assert_allclose(hits["t"][hit], bt[hit], rtol=1e-4, atol=1e-5)
+    # triangle ids agree wherever the closest hit is not a shared edge/tie
+    tid = (hits["triangle_id"] & 0x7FFFFFFF).astype(np.int64)
+    assert np.mean(tid[hit] == bid[hit]) > 0.97
+    assert cnt["node_visits"] > 0 and cnt["triangle_tests"] >= 400
+
+
+def test_wavefront_equals_megakernel_without_emitters(oracle_mod, golden_luts):
+    """No emissive geometry -> the two oracle schedules must produce identical bits."""
+    s = cornell(64, 48, 4)
+    fr = s.frame_params(9)
+    a = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rng=True)
+    b = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.MEGAKERNEL, rng=True)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+    assert a[3] == b[3]
+
+
+def test_render_thread_count_independent(oracle_mod, golden_luts):
+    s = cornell(48, 40, 3)
+    fr = s.frame_params(4)
+    a = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rng=True, threads=1)
+    b = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rng=True, threads=5)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+
+
+def test_render_rect_and_bounds(oracle_mod, golden_luts):
+    s = cornell(40, 32, 2)
+    fr = s.frame_params(1)
+    full = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rng=True)
+    part = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rect=(8, 8, 16, 8), rng=True)
+    assert np.array_equal(part[1][8:16, 8:24], full[1][8:16, 8:24])
+    assert np.all(part[1][:8] == 0)
+    with pytest.raises(RuntimeError):
+        oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rect=(0, 30, 40, 8))
+
+
+def test_sample_invariants(oracle_mod, golden_luts):
+    s = cornell(64, 64, 8)
+    pos, val, rng, cnt = oracle_mod.render(s.flat(), golden_luts, s.frame_params(0), oracle_mod.WAVEFRONT, rng=True)
+    assert np.all((pos >= 0) & (pos < 1))            # pixel sample inside the pixel
+    assert np.all(np.isfinite(val)) and np.all(val[..., :3] >= 0) and np.all(val[..., 3] == 0)
+    assert cnt["extension_rays"] >= 64 * 64          # every pixel casts its camera ray
+    assert cnt["shadow_rays"] > 0
+
+
+def _numpy_box_convolution(pos, val, r):
+    H, W = pos.shape[:2]
+    film = np.zeros((H, W, 4), np.float64)
+    for py in range(H):
+        for px in range(W):
+            cx, cy = px + 0.5, py + 0.5
+            for y in range(max(0, int(np.floor(cy - r))), min(H - 1, int(np.floor(cy + r))) + 1):
+                for x in range(max(0, int(np.floor(cx - r))), min(W - 1, int(np.floor(cx + r))) + 1):
+                    sx, sy = pos[y, x, 0] + x, pos[y, x, 1] + y
+                    if abs(cx - sx) <= r and abs(cy - sy) <= r:
+                        film[py, px, :3] += val[y, x, :3]
+                        film[py, px, 3] += 1.0
+    return film
+
+
+def test_sample_convolution_box_matches_numpy(oracle_mod, golden_luts):
+    from directcomputeraytracing_amd import FILTER_BOX, FilterParams
+    s = cornell(24, 16, 2)
+    pos, val, _, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(2), oracle_mod.WAVEFRONT)
+    film = oracle_mod.sample_convolution(FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3), pos, val)
+    ref = _numpy_box_convolution(pos, val, 1.0)
+    np.testing.assert_allclose(film, ref, rtol=1e-5, atol=1e-6)

@@ -1,0 +1,60 @@
+"""Summarise rocprofv3 outputs of tools/profile.sh into profiles/.
+
+* kernel stats (kernel-trace --stats) -> per-kernel call count / average duration
+* PMC passes: FETCH_SIZE and WRITE_SIZE are in KiB (1 KiB = 16 x 64-B
+  TCC_EA0_RDREQ, checked against the TCC_EA0_RDREQ_sum pass). Per the MI355X
+  guide, gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so read bytes are
+  doubled; WRITE_SIZE is taken as is. Traffic is averaged per launch over the
+  same whole-image launch mix the bench's roofline leg uses.
+
+Usage: python tools/pmc_traffic.py gpurun_out/prof profiles/r01
+"""
+import collections
+import csv
+import json
+import sys
+from pathlib import Path
+
+
+def per_kernel(path: Path):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        agg[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main(src, dst_prefix):
+    src, dst_prefix = Path(src), str(dst_prefix)
+    out = {"kernels": {}}
+    stats = src / "trace_kernel_stats.csv"
+    if stats.exists():
+        for r in csv.DictReader(open(stats)):
+            name = r["Name"].split("(")[0].replace("void ", "")
+            out["kernels"].setdefault(name, {})
+            out["kernels"][name].update(calls=int(r["Calls"]), avg_us=float(r["AverageNs"]) / 1e3,
+                                        total_ms=float(r["TotalDurationNs"]) / 1e6)
+    counters = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE", "TCC_EA0_RDREQ_sum"):
+        p = src / f"pmc_{ctr}_counter_collection.csv"
+        if p.exists():
+            counters[ctr] = per_kernel(p)
+    for name in set().union(*[set(v) for v in counters.values()]) if counters else []:
+        d = out["kernels"].setdefault(name, {})
+        for ctr, agg in counters.items():
+            if name in agg:
+                vals = agg[name]
+                d[f"{ctr}_avg"] = sum(vals) / len(vals)
+        if "FETCH_SIZE_avg" in d and "WRITE_SIZE_avg" in d:
+            d["hbm_read_bytes_per_launch"] = d["FETCH_SIZE_avg"] * 1024 * 2
+            d["hbm_write_bytes_per_launch"] = d["WRITE_SIZE_avg"] * 1024
+            d["hbm_bytes_per_launch"] = d["hbm_read_bytes_per_launch"] + d["hbm_write_bytes_per_launch"]
+        if "FETCH_SIZE_avg" in d and "TCC_EA0_RDREQ_sum_avg" in d and d["TCC_EA0_RDREQ_sum_avg"]:
+            d["fetch_kib_per_rdreq"] = d["FETCH_SIZE_avg"] / d["TCC_EA0_RDREQ_sum_avg"]
+    ext = out["kernels"].get("dcrt::dev::extension_kernel<false>", {})
+    out["ext_hbm_bytes_per_launch"] = ext.get("hbm_bytes_per_launch")
+    Path(dst_prefix + "_pmc_traffic.json").write_text(json.dumps(out, indent=1, sort_keys=True))
+    print(json.dumps({"ext_hbm_bytes_per_launch": out["ext_hbm_bytes_per_launch"]}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
