@@ -17,17 +17,50 @@ constexpr uint32_t kFlagShadowRayHit = 0x40000000u;
 constexpr uint32_t kFlagTerminate = 0x20000000u;
 constexpr uint32_t kBlockW = 8, kBlockH = 8;           // one wave64 = one 8x8 pixel block
 
+// Queue counters are sharded: producer workgroup b appends to shard b % kShards,
+// each shard counter on its own 256-B line. One returning device-scope atomic on
+// a single word saturates at ~88 per microsecond on MI355X (MI355X_MICROARCH.md,
+// "dequeue"), which would cap a 2M-path wavefront at ~100 us per queue per
+// iteration; eight words spread that over eight memory-side atomic units.
+constexpr uint32_t kShards = 8;
+constexpr uint32_t kShardStride = 64;                  // uint32 words (256 B)
+constexpr uint32_t kQExt = 0, kQShadow = 1, kQMaterial = 2, kQueues = 3;
+
 struct Counters {        // one set per iteration parity
-    uint32_t ext, shadow, material, newPath;
-    uint32_t pad[4];
+    uint32_t w[kQueues * kShards * kShardStride];
 };
 struct Globals {
-    uint32_t nextBlock;
+    uint32_t nextBlock[kShards * kShardStride];        // per-shard pixel-block cursors
     uint32_t totalBlocks;
     uint32_t stackOverflow;
-    uint32_t pad0;
+    uint32_t pad0[2];
     unsigned long long extRays, shadowRays, newPaths, iterations;
 };
+
+DEV uint32_t* qctr(Counters* c, uint32_t q, uint32_t s) { return c->w + (q * kShards + s) * kShardStride; }
+DEV uint32_t qctr_load(const Counters* c, uint32_t q, uint32_t s) { return c->w[(q * kShards + s) * kShardStride]; }
+DEV uint32_t qtotal(const Counters* c, uint32_t q)
+{
+    uint32_t t = 0;
+    for (uint32_t s = 0; s < kShards; ++s) t += qctr_load(c, q, s);
+    return t;
+}
+// Concatenated view of the shards of one queue: item i -> (shard, offset).
+struct QueueMap {
+    uint32_t prefix[kShards + 1];
+};
+DEV void qmap(const Counters* c, uint32_t q, QueueMap* m)
+{
+    m->prefix[0] = 0;
+    for (uint32_t s = 0; s < kShards; ++s) m->prefix[s + 1] = m->prefix[s] + qctr_load(c, q, s);
+}
+DEV uint32_t qentry(const uint32_t* queue, uint32_t cap, const QueueMap& m, uint32_t i)
+{
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < kShards; ++k) s += i >= m.prefix[k] ? 1u : 0u;
+    return queue[(size_t)s * cap + (i - m.prefix[s])];
+}
 
 // Per-image constants, read from HBM so a captured graph can be replayed for
 // every frame seed (SNewPathConstants / SMaterialConstants / SControlConstants).
@@ -92,7 +125,7 @@ struct PathPool {
     float4* throughput;  // T.xyz, bsdfPdf
     float4* li;          // Li.xyz, isDeltaBxdf (0/1)
     uint32_t* flags;
-    uint32_t* extQueue;
+    uint32_t* extQueue;        // kShards x size entries each
     uint32_t* shadowQueue;
     uint32_t* materialQueue;
     uint32_t size;

@@ -50,7 +50,8 @@ __global__ void set_idle_kernel(PathPool pool, Counters* counters, Globals* g, u
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid < pool.size) pool.flags[tid] = kFlagIdle;
     if (tid < 2 * (uint32_t)(sizeof(Counters) / 4)) ((uint32_t*)counters)[tid] = 0u;
-    if (tid == 0) { g->nextBlock = 0u; g->totalBlocks = totalBlocks; }
+    if (tid < kShards) g->nextBlock[tid * kShardStride] = 0u;
+    if (tid == 0) g->totalBlocks = totalBlocks;
 }
 
 __global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32_t* triangles, uint32_t count, float4* out)
@@ -69,6 +70,10 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
 {
     __shared__ uint32_t sm[64];
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t shard = blockIdx.x % kShards;
+    uint32_t* cursor = &g->nextBlock[shard * kShardStride];
+    // pixel blocks of this shard: shard, shard + kShards, ...
+    const uint32_t shardBlocks = g->totalBlocks > shard ? (g->totalBlocks - shard + kShards - 1) / kShards : 0u;
     for (uint32_t base = blockIdx.x * blockDim.x; base < pool.size; base += gridDim.x * blockDim.x) {
     const uint32_t tid = base + threadIdx.x;
     const uint32_t flags = pool.flags[tid];
@@ -93,16 +98,17 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
             pool.li[tid] = li;
         }
     }
-    const uint32_t mslot = block_append(!idle, &cnt->material, sm);
-    if (!idle) pool.materialQueue[mslot] = tid;
+    const uint32_t mslot = block_append(!idle, qctr(cnt, kQMaterial, shard), sm);
+    if (!idle) pool.materialQueue[(size_t)shard * pool.size + mslot] = tid;
 
     // A fully idle wave claims the next 8x8 block (one atomic per workgroup).
     const bool waveIdle = __ballot(!idle) == 0ull;
     bool want = false;
-    if (waveIdle && lane == 0) want = __hip_atomic_load(&g->nextBlock, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g->totalBlocks;
-    const uint32_t bslot = block_append(want, &g->nextBlock, sm);
-    const uint32_t block = (uint32_t)__shfl((int)bslot, 0, 64);
-    const bool got = __shfl((int)want, 0, 64) != 0 && block < g->totalBlocks;
+    if (waveIdle && lane == 0) want = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shardBlocks;
+    const uint32_t bslot = block_append(want, cursor, sm);
+    const uint32_t claimed = (uint32_t)__shfl((int)bslot, 0, 64);
+    const bool got = __shfl((int)want, 0, 64) != 0 && claimed < shardBlocks;
+    const uint32_t block = shard + claimed * kShards;
     bool newPath = false;
     if (got) {
         const uint32_t band = block / fc->blocksX, bx = block % fc->blocksX;
@@ -131,8 +137,8 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
             bounce = 0;
         }
     }
-    const uint32_t eslot = block_append(newPath, &cnt->ext, sm);
-    if (newPath) pool.extQueue[eslot] = tid;
+    const uint32_t eslot = block_append(newPath, qctr(cnt, kQExt, shard), sm);
+    if (newPath) pool.extQueue[(size_t)shard * pool.size + eslot] = tid;
     pool.flags[tid] = (idle ? kFlagIdle : 0u) | (bounce & 0xFFu);
     }
 }
@@ -141,14 +147,17 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
 __global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt)
 {
     __shared__ uint32_t sm[64];
-    const uint32_t count = cnt->material;
+    QueueMap qm;
+    qmap(cnt, kQMaterial, &qm);
+    const uint32_t count = qm.prefix[kShards];
+    const uint32_t shard = blockIdx.x % kShards;
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
     const bool active = i < count;
     bool terminate = false, hasShadow = false;
     uint32_t path = 0;
     if (active) {
-        path = pool.materialQueue[i];
+        path = qentry(pool.materialQueue, pool.size, qm, i);
         const float4 h4 = pool.hit[path];
         HitRecord hit;
         hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = pool.hitInst[path];
@@ -231,10 +240,10 @@ __global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScen
         pool.li[path] = make_float4(L.x, L.y, L.z, li.w);
         pool.lsr[path] = make_float4(lsr.x, lsr.y, lsr.z, 0.0f);
     }
-    const uint32_t es = block_append(active && !terminate, &cnt->ext, sm);
-    if (active && !terminate) pool.extQueue[es] = path;
-    const uint32_t ss = block_append(active && hasShadow, &cnt->shadow, sm);
-    if (active && hasShadow) pool.shadowQueue[ss] = path;
+    const uint32_t es = block_append(active && !terminate, qctr(cnt, kQExt, shard), sm);
+    if (active && !terminate) pool.extQueue[(size_t)shard * pool.size + es] = path;
+    const uint32_t ss = block_append(active && hasShadow, qctr(cnt, kQShadow, shard), sm);
+    if (active && hasShadow) pool.shadowQueue[(size_t)shard * pool.size + ss] = path;
     }
 }
 
@@ -244,10 +253,12 @@ __global__ __launch_bounds__(256) void extension_kernel(PathPool pool, DeviceSce
                                                          Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
-    const uint32_t n = cnt->ext;
+    QueueMap qm;
+    qmap(cnt, kQExt, &qm);
+    const uint32_t n = qm.prefix[kShards];
     uint32_t visits = 0, tris = 0, blas = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t path = pool.extQueue[i];
+        const uint32_t path = qentry(pool.extQueue, pool.size, qm, i);
         const float4 o = pool.rayO[path], d = pool.rayD[path];
         HitRecord h;
         h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.tri = 0u; h.inst = 0u;
@@ -270,10 +281,12 @@ __global__ __launch_bounds__(256) void shadow_kernel(PathPool pool, DeviceScene 
                                                       Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
-    const uint32_t n = cnt->shadow;
+    QueueMap qm;
+    qmap(cnt, kQShadow, &qm);
+    const uint32_t n = qm.prefix[kShards];
     uint32_t visits = 0, tris = 0, blas = 0;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t path = pool.shadowQueue[i];
+        const uint32_t path = qentry(pool.shadowQueue, pool.size, qm, i);
         const float4 o = pool.shadowO[path], d = pool.shadowD[path];
         HitRecord h;
         TraversalStats st;
@@ -288,11 +301,13 @@ __global__ __launch_bounds__(256) void shadow_kernel(PathPool pool, DeviceScene 
         if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&instr[3], a); atomicAdd(&instr[4], b); atomicAdd(&instr[5], c); }
     }
     // End of the iteration: account and clear the other parity's counters.
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        g->extRays += cnt->ext;
-        g->shadowRays += cnt->shadow;
-        g->iterations += 1ull;
-        nextCnt->ext = 0u; nextCnt->shadow = 0u; nextCnt->material = 0u; nextCnt->newPath = 0u;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            g->extRays += qtotal(cnt, kQExt);
+            g->shadowRays += n;
+            g->iterations += 1ull;
+        }
+        if (threadIdx.x < kQueues * kShards) nextCnt->w[threadIdx.x * kShardStride] = 0u;
     }
 }
 

@@ -199,9 +199,9 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.throughput, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.li, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.extQueue, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.shadowQueue, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.materialQueue, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.extQueue, (size_t)P * kShards, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.shadowQueue, (size_t)P * kShards, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.materialQueue, (size_t)P * kShards, &poolAllocs));
     pool.size = poolSize;
     CHECKED(DeviceAlloc(&dFrame, 1, &poolAllocs));
     CHECKED(DeviceAlloc(&dCounters, 2, &poolAllocs));
@@ -448,7 +448,8 @@ int dcrt_tracer::BeginImage()
     fc.bandCount = bandCount;
     hipLaunchKernelGGL(set_frame_kernel, dim3(1), dim3(1), 0, stream, dFrame, fc);
     const uint32_t total = fc.blocksX * bandCount;
-    hipLaunchKernelGGL(set_idle_kernel, dim3((poolSize + 255) / 256), dim3(256), 0, stream, pool, dCounters, dGlobals, total);
+    const uint32_t idleThreads = std::max<uint32_t>(poolSize, 2u * (uint32_t)(sizeof(Counters) / 4));
+    hipLaunchKernelGGL(set_idle_kernel, dim3((idleThreads + 255) / 256), dim3(256), 0, stream, pool, dCounters, dGlobals, total);
     HIPCHECK(hipGetLastError());
     parity = 0;
     newImage = false;
@@ -553,7 +554,12 @@ int dcrt_tracer::ReadCompletion(bool* complete)
     const uint32_t last = parity ^ 1u;
     HIPCHECK(hipMemcpyAsync(hCounters, dCounters + last, sizeof(Counters), hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipStreamSynchronize(stream));
-    *complete = hCounters->material == 0 && hCounters->ext == 0;
+    uint32_t material = 0, ext = 0;
+    for (uint32_t sh = 0; sh < kShards; ++sh) {
+        material += hCounters->w[(kQMaterial * kShards + sh) * kShardStride];
+        ext += hCounters->w[(kQExt * kShards + sh) * kShardStride];
+    }
+    *complete = material == 0 && ext == 0;
     return DCRT_OK;
 }
 
