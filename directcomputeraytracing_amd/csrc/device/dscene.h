@@ -85,12 +85,13 @@ DEV Shear make_shear(V3 d)   // BVHAccel.inc.hlsl:72-83
 }
 
 // Watertight test (RayPrimitiveIntersect.inc.hlsl:8-70).
-DEV bool tri_watertight(V3 o, const Shear& sh, float tMin, float tMax, V3 v0, V3 v1, V3 v2,
+// `degenerate` = (|cross(v1-v0, v2-v0)|^2 == 0), precomputed per triangle at upload
+// with the same arithmetic (build_tri_verts_kernel) and stored in triVerts[3t].w.
+DEV bool tri_watertight(V3 o, const Shear& sh, float tMin, float tMax, V3 v0, V3 v1, V3 v2, bool degenerate,
                         float* t, float* u, float* v, bool* backface)
 {
     *t = 0.0f; *u = 0.0f; *v = 0.0f; *backface = false;
-    const V3 cp = cross(v1 - v0, v2 - v0);
-    if (dot(cp, cp) == 0.0f) return false;
+    if (degenerate) return false;
     const V3 a = v0 - o, b = v1 - o, c = v2 - o;
     float p0x = comp(a, sh.kx), p0y = comp(a, sh.ky), p0z = comp(a, sh.kz);
     float p1x = comp(b, sh.kx), p1y = comp(b, sh.ky), p1z = comp(b, sh.kz);
@@ -137,101 +138,108 @@ struct HitRecord {
     uint32_t inst;
 };
 
-// Two-level traversal with a per-lane stack in LDS (column `lane` of a
-// [stackSize][blockDim] array: consecutive lanes hit consecutive banks).
-// ANY_HIT = BVHIntersect (shadow), else BVHIntersectNoInterp (closest hit).
-// Traversal counters (SRayTraversalCounters semantics) go to *stats when non-null.
+// Two-level traversal (BVHIntersectNoInterp / BVHIntersect, BVHAccel.inc.hlsl:85-369)
+// as a resumable per-lane state machine: one call = one node visit in the
+// reference's order (test-on-visit, near child first by the split axis' direction
+// sign, far child pushed), so hits, tie-breaking and the SRayTraversalCounters
+// counts are the reference's. Kernels interleave steps with refills of finished
+// lanes (persistent "while-while" with per-lane dynamic ray fetch), so a wave64
+// does not idle until its slowest ray is done.
+// The per-lane stack lives in LDS: column `lane` of a [stackSize][blockDim] array
+// (consecutive lanes on consecutive banks).
 struct TraversalStats {
     uint32_t nodes;   // iterationCounter (BVHAccel.inc.hlsl:121)
     uint32_t tris;    // triangle tests
     uint32_t blas;    // TLAS -> BLAS entries
 };
 
-template <bool ANY_HIT>
-DEV bool traverse_stats(const DeviceScene& sc, V3 origin, V3 dir, float tMin, float tMaxIn, uint32_t features,
-                        uint32_t* lds, uint32_t stride, HitRecord* hit, TraversalStats* stats)
-{
-    uint32_t tris = 0, blas = 0;
-    const bool watertight = (features & DCRT_FEATURE_WATERTIGHT) != 0;
-    const bool f2b = (features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
-    float tMax = tMaxIn;
-    uint32_t count = 0;
-    uint32_t node = 0, inst = 0;
-    bool inBlas = false;
-    V3 lo = origin, ld = dir;
-    V3 inv = inv_dir(ld);
+struct TravState {
+    V3 o, d, invW;        // world ray and 1/d (restored on BLAS -> TLAS without dividing again)
+    V3 lo, ld, inv;       // ray in the current space (world or instance)
+    float tMin, tMax;
+    uint32_t node, count, inst;
+    bool inBlas, shearValid, found;
     Shear sh;
-    bool shearValid = false;
-    uint32_t n = 0;
-    for (;;) {
-        ++n;
-        const float4 a = sc.nodes[node * 2];
-        const float4 b = sc.nodes[node * 2 + 1];
-        bool pop = false;
-        if (ray_aabb(lo, inv, tMin, tMax, a, b)) {
-            const uint32_t misc = asu(b.w);
-            const uint32_t primOrInst = (misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
-            if (misc & 0x4u) {
-                const float4* M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
-                lo = mul43(origin, 1.0f, M);
-                ld = mul43(dir, 0.0f, M);
-                inv = inv_dir(ld);
-                shearValid = false;
-                inBlas = true;
-                inst = primOrInst;
-                node = asu(b.z);
-                ++blas;
-            } else if (primOrInst == 0) {
-                const uint32_t axis = misc & 0x3u;
-                bool neg = false;
-                if (f2b) neg = axis == 0 ? ld.x < 0.0f : (axis == 1 ? ld.y < 0.0f : ld.z < 0.0f);
-                const uint32_t right = asu(b.z);
-                const uint32_t push = neg ? node + 1 : right;
-                node = neg ? right : node + 1;
-                if (count < sc.stackSize) lds[count * stride] = (push & 0x7FFFFFFFu) | (inBlas ? 0x80000000u : 0u);
-                ++count;
-            } else {
-                if (watertight && !shearValid) { sh = make_shear(ld); shearValid = true; }
-                const uint32_t begin = asu(b.z);
-                const uint32_t end = begin + primOrInst;
-                for (uint32_t p = begin; p < end; ++p) {
-                    ++tris;
-                    const float4 q0 = sc.triVerts[(size_t)p * 3];
-                    const float4 q1 = sc.triVerts[(size_t)p * 3 + 1];
-                    const float4 q2 = sc.triVerts[(size_t)p * 3 + 2];
-                    const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
-                    float t, u, v; bool bf;
-                    const bool h = watertight ? tri_watertight(lo, sh, tMin, tMax, v0, v1, v2, &t, &u, &v, &bf)
-                                              : tri_moller(lo, ld, tMin, tMax, v0, v1, v2, &t, &u, &v, &bf);
-                    if (h) {
-                        if (ANY_HIT) {
-                            if (stats) { stats->nodes = n; stats->tris = tris; stats->blas = blas; }
-                            return true;
-                        }
-                        tMax = t;
-                        hit->t = t; hit->u = u; hit->v = v;
-                        hit->tri = (p & 0x7FFFFFFFu) | (bf ? 0x80000000u : 0u);
-                        hit->inst = inst;
-                    }
+    HitRecord hit;
+};
+
+DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax)
+{
+    s.o = o; s.d = d; s.invW = inv_dir(d);
+    s.lo = o; s.ld = d; s.inv = s.invW;
+    s.tMin = tMin; s.tMax = tMax;
+    s.node = 0; s.count = 0; s.inst = 0;
+    s.inBlas = false; s.shearValid = false; s.found = false;
+    s.hit.t = 0.0f; s.hit.u = 0.0f; s.hit.v = 0.0f; s.hit.tri = 0u; s.hit.inst = 0u;
+}
+
+// Returns true when the ray is finished (stack empty, or first hit for ANY_HIT).
+template <bool ANY_HIT, bool INSTR>
+DEV bool trav_step(const DeviceScene& sc, TravState& s, bool watertight, bool f2b, uint32_t* lds, uint32_t stride,
+                   TraversalStats& st)
+{
+    if (INSTR) ++st.nodes;
+    const float4 a = sc.nodes[s.node * 2];
+    const float4 b = sc.nodes[s.node * 2 + 1];
+    bool pop = true;
+    if (ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a, b)) {
+        const uint32_t misc = asu(b.w);
+        const uint32_t primOrInst = (misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
+        if (misc & 0x4u) {                       // TLAS leaf: enter the instance's BLAS
+            const float4* M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
+            s.lo = mul43(s.o, 1.0f, M);
+            s.ld = mul43(s.d, 0.0f, M);
+            s.inv = inv_dir(s.ld);
+            s.shearValid = false;
+            s.inBlas = true;
+            s.inst = primOrInst;
+            s.node = asu(b.z);
+            if (INSTR) ++st.blas;
+            pop = false;
+        } else if (primOrInst == 0) {            // interior: near child next, far child pushed
+            const uint32_t axis = misc & 0x3u;
+            bool neg = false;
+            if (f2b) neg = axis == 0 ? s.ld.x < 0.0f : (axis == 1 ? s.ld.y < 0.0f : s.ld.z < 0.0f);
+            const uint32_t right = asu(b.z);
+            const uint32_t push = neg ? s.node + 1 : right;
+            s.node = neg ? right : s.node + 1;
+            if (s.count < sc.stackSize) lds[s.count * stride] = (push & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
+            ++s.count;
+            pop = false;
+        } else {                                 // BLAS leaf: triangles [begin, begin + count)
+            if (watertight && !s.shearValid) { s.sh = make_shear(s.ld); s.shearValid = true; }
+            const uint32_t begin = asu(b.z);
+            const uint32_t end = begin + primOrInst;
+            for (uint32_t p = begin; p < end; ++p) {
+                if (INSTR) ++st.tris;
+                const float4 q0 = sc.triVerts[(size_t)p * 3];
+                const float4 q1 = sc.triVerts[(size_t)p * 3 + 1];
+                const float4 q2 = sc.triVerts[(size_t)p * 3 + 2];
+                const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+                float t, u, v; bool bf;
+                const bool h = watertight ? tri_watertight(s.lo, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
+                                          : tri_moller(s.lo, s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
+                if (h) {
+                    s.found = true;
+                    if (ANY_HIT) return true;
+                    s.tMax = t;
+                    s.hit.t = t; s.hit.u = u; s.hit.v = v;
+                    s.hit.tri = (p & 0x7FFFFFFFu) | (bf ? 0x80000000u : 0u);
+                    s.hit.inst = s.inst;
                 }
-                pop = true;
             }
-        } else {
-            pop = true;
-        }
-        if (pop) {
-            if (count == 0) break;
-            --count;
-            const uint32_t packed = count < sc.stackSize ? lds[count * stride] : 0u;
-            const bool wasBlas = inBlas;
-            node = packed & 0x7FFFFFFFu;
-            inBlas = (packed & 0x80000000u) != 0;
-            if (wasBlas != inBlas) { lo = origin; ld = dir; inv = inv_dir(ld); shearValid = false; }
         }
     }
-    if (stats) { stats->nodes = n; stats->tris = tris; stats->blas = blas; }
-    if (ANY_HIT) return false;
-    return !isinf(tMax);
+    if (pop) {
+        if (s.count == 0) return true;
+        --s.count;
+        const uint32_t packed = s.count < sc.stackSize ? lds[s.count * stride] : 0u;
+        const bool wasBlas = s.inBlas;
+        s.node = packed & 0x7FFFFFFFu;
+        s.inBlas = (packed & 0x80000000u) != 0;
+        if (wasBlas != s.inBlas) { s.lo = s.o; s.ld = s.d; s.inv = s.invW; s.shearValid = false; }
+    }
+    return false;
 }
 
 // ---- texture emulation ----------------------------------------------------------

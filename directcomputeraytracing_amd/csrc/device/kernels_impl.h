@@ -58,10 +58,15 @@ __global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32
 {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= count) return;
+    V3 p[3];
     for (int k = 0; k < 3; ++k) {
         const dcrt_vertex& v = vertices[triangles[t * 3 + k]];
-        out[(size_t)t * 3 + k] = make_float4(v.position[0], v.position[1], v.position[2], 0.0f);
+        p[k] = mk(v.position[0], v.position[1], v.position[2]);
     }
+    // RayTriangleIntersect's degenerate test (RayPrimitiveIntersect.inc.hlsl), hoisted to upload time
+    const V3 cp = cross(p[1] - p[0], p[2] - p[0]);
+    const float degenerate = dot(cp, cp) == 0.0f ? 1.0f : 0.0f;
+    for (int k = 0; k < 3; ++k) out[(size_t)t * 3 + k] = make_float4(p[k].x, p[k].y, p[k].z, k == 0 ? degenerate : 0.0f);
 }
 
 // ---- CONTROL (+ NEW_PATH) -------------------------------------------------------
@@ -248,6 +253,49 @@ __global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScen
 }
 
 // ---- EXTENSION_RAY_CAST / SHADOW_RAY_CAST ----------------------------------------------
+// Persistent while-while loop with per-lane dynamic fetch: wave w owns items
+// [w*chunk, (w+1)*chunk) of the queue; every step, lanes whose ray finished take
+// the next items of the wave's range (ballot + mbcnt, no atomics), so all 64
+// lanes keep traversing until the range is drained.
+template <bool ANY_HIT, bool INSTR, typename Fetch, typename Emit>
+__device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t* lds,
+                                                 uint32_t stride, Fetch fetch, Emit emit, TraversalStats& st)
+{
+    const bool watertight = (features & DCRT_FEATURE_WATERTIGHT) != 0;
+    const bool f2b = (features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
+    const uint32_t wavesPerBlock = blockDim.x >> 6;
+    const uint32_t waves = gridDim.x * wavesPerBlock;
+    const uint32_t waveId = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
+    const uint32_t chunk = (n + waves - 1) / waves;
+    uint32_t cursor = min(waveId * chunk, n);
+    const uint32_t end = min(cursor + chunk, n);
+    TravState s;
+    bool active = false;
+    uint32_t item = 0;
+    for (;;) {
+        const unsigned long long need = __ballot(!active);
+        if (need != 0ull && cursor < end) {
+            const uint32_t idx = cursor + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            if (!active && idx < end) {
+                item = fetch(idx, s);
+                active = true;
+            }
+            cursor = min(cursor + (uint32_t)__popcll(need), end);
+        }
+        if (__ballot(active) == 0ull) break;
+        if (active && trav_step<ANY_HIT, INSTR>(sc, s, watertight, f2b, lds, stride, st)) {
+            emit(item, s);
+            active = false;
+        }
+    }
+}
+
+__device__ __forceinline__ void flush_stats(const TraversalStats& st, unsigned long long* dst)
+{
+    const unsigned long long a = wave_sum(st.nodes), b = wave_sum(st.tris), c = wave_sum(st.blas);
+    if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&dst[0], a); atomicAdd(&dst[1], b); atomicAdd(&dst[2], c); }
+}
+
 template <bool INSTR>
 __global__ __launch_bounds__(256) void extension_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, const Counters* cnt,
                                                          Globals* g, unsigned long long* instr)
@@ -255,24 +303,21 @@ __global__ __launch_bounds__(256) void extension_kernel(PathPool pool, DeviceSce
     extern __shared__ uint32_t stackMem[];
     QueueMap qm;
     qmap(cnt, kQExt, &qm);
-    const uint32_t n = qm.prefix[kShards];
-    uint32_t visits = 0, tris = 0, blas = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t path = qentry(pool.extQueue, pool.size, qm, i);
-        const float4 o = pool.rayO[path], d = pool.rayD[path];
-        HitRecord h;
-        h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.tri = 0u; h.inst = 0u;
-        TraversalStats st;
-        const bool hit = traverse_stats<false>(sc, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf(), fc->features,
-                                               stackMem + threadIdx.x, blockDim.x, &h, INSTR ? &st : nullptr);
-        pool.hit[path] = hit ? make_float4(h.t, h.u, h.v, asf(h.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
-        pool.hitInst[path] = hit ? h.inst : 0u;
-        if (INSTR) { visits += st.nodes; tris += st.tris; blas += st.blas; }
-    }
-    if (INSTR) {
-        const unsigned long long a = wave_sum(visits), b = wave_sum(tris), c = wave_sum(blas);
-        if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&instr[0], a); atomicAdd(&instr[1], b); atomicAdd(&instr[2], c); }
-    }
+    TraversalStats st = {0u, 0u, 0u};
+    persistent_trace<false, INSTR>(
+        sc, qm.prefix[kShards], fc->features, stackMem + threadIdx.x, blockDim.x,
+        [&](uint32_t i, TravState& s) {
+            const uint32_t path = qentry(pool.extQueue, pool.size, qm, i);
+            const float4 o = pool.rayO[path], d = pool.rayD[path];
+            trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf());
+            return path;
+        },
+        [&](uint32_t path, const TravState& s) {
+            pool.hit[path] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
+            pool.hitInst[path] = s.found ? s.hit.inst : 0u;
+        },
+        st);
+    if (INSTR) flush_stats(st, instr);
     (void)g;
 }
 
@@ -284,22 +329,21 @@ __global__ __launch_bounds__(256) void shadow_kernel(PathPool pool, DeviceScene 
     QueueMap qm;
     qmap(cnt, kQShadow, &qm);
     const uint32_t n = qm.prefix[kShards];
-    uint32_t visits = 0, tris = 0, blas = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t path = qentry(pool.shadowQueue, pool.size, qm, i);
-        const float4 o = pool.shadowO[path], d = pool.shadowD[path];
-        HitRecord h;
-        TraversalStats st;
-        const bool hit = traverse_stats<true>(sc, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, o.w, fc->features,
-                                              stackMem + threadIdx.x, blockDim.x, &h, INSTR ? &st : nullptr);
-        const uint32_t f = pool.flags[path];
-        pool.flags[path] = (hit ? kFlagShadowRayHit : 0u) | (f & 0xBFFFFFFFu);
-        if (INSTR) { visits += st.nodes; tris += st.tris; blas += st.blas; }
-    }
-    if (INSTR) {
-        const unsigned long long a = wave_sum(visits), b = wave_sum(tris), c = wave_sum(blas);
-        if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&instr[3], a); atomicAdd(&instr[4], b); atomicAdd(&instr[5], c); }
-    }
+    TraversalStats st = {0u, 0u, 0u};
+    persistent_trace<true, INSTR>(
+        sc, n, fc->features, stackMem + threadIdx.x, blockDim.x,
+        [&](uint32_t i, TravState& s) {
+            const uint32_t path = qentry(pool.shadowQueue, pool.size, qm, i);
+            const float4 o = pool.shadowO[path], d = pool.shadowD[path];
+            trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, o.w);
+            return path;
+        },
+        [&](uint32_t path, const TravState& s) {
+            const uint32_t f = pool.flags[path];
+            pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (f & 0xBFFFFFFFu);
+        },
+        st);
+    if (INSTR) flush_stats(st, instr + 3);
     // End of the iteration: account and clear the other parity's counters.
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
@@ -317,29 +361,26 @@ __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const 
                                                            dcrt_ray_hit* hits, uint32_t* occluded, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t visits = 0, tris = 0, blas = 0;
-    if (i < n) {
-        const dcrt_ray r = rays[i];
-        HitRecord h;
-        h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.tri = 0u; h.inst = 0u;
-        TraversalStats st;
-        const bool hit = traverse_stats<ANY>(sc, ld3(r.origin), ld3(r.direction), 0.0f, ANY ? r.t_max : inf(), features,
-                                             stackMem + threadIdx.x, blockDim.x, &h, &st);
-        visits = st.nodes; tris = st.tris; blas = st.blas;
-        if (ANY) {
-            occluded[i] = hit ? 1u : 0u;
-        } else {
-            dcrt_ray_hit o;
-            o.t = hit ? h.t : inf(); o.u = hit ? h.u : 0.0f; o.v = hit ? h.v : 0.0f;
-            o.triangle_id = hit ? h.tri : 0u; o.instance_index = hit ? h.inst : 0u;
-            hits[i] = o;
-        }
-    }
-    if (instr) {
-        const unsigned long long a = wave_sum(visits), b = wave_sum(tris), c = wave_sum(blas);
-        if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&instr[0], a); atomicAdd(&instr[1], b); atomicAdd(&instr[2], c); }
-    }
+    TraversalStats st = {0u, 0u, 0u};
+    persistent_trace<ANY, true>(
+        sc, n, features, stackMem + threadIdx.x, blockDim.x,
+        [&](uint32_t i, TravState& s) {
+            const dcrt_ray r = rays[i];
+            trav_init(s, ld3(r.origin), ld3(r.direction), 0.0f, ANY ? r.t_max : inf());
+            return i;
+        },
+        [&](uint32_t i, const TravState& s) {
+            if (ANY) {
+                occluded[i] = s.found ? 1u : 0u;
+            } else {
+                dcrt_ray_hit o;
+                o.t = s.found ? s.hit.t : inf(); o.u = s.found ? s.hit.u : 0.0f; o.v = s.found ? s.hit.v : 0.0f;
+                o.triangle_id = s.found ? s.hit.tri : 0u; o.instance_index = s.found ? s.hit.inst : 0u;
+                hits[i] = o;
+            }
+        },
+        st);
+    if (instr) flush_stats(st, instr);
 }
 
 __global__ void math_eval_kernel(int function, const float* x, uint32_t n, float* y)

@@ -148,7 +148,8 @@ struct dcrt_tracer {
         graphExec = nullptr;
         graphValid = false;
     }
-    uint32_t CastGrid(uint32_t block) const { return std::min<uint32_t>((poolSize + block - 1) / block, kMaxPersistentBlocks * (256 / block)); }
+    uint32_t castResident = 0;         // persistent cast grid: resident workgroups on the whole chip
+    uint32_t CastGrid(uint32_t block) const { return std::min<uint32_t>((poolSize + block - 1) / block, castResident); }
 };
 
 dcrt_tracer::~dcrt_tracer()
@@ -335,6 +336,14 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     while (castBlock > 64 && (size_t)d.stackSize * castBlock * 4 > 32768) castBlock >>= 1;
     castLds = (size_t)d.stackSize * castBlock * 4;
     if (castLds > 65536) { SetLastError("BVH traversal stack too deep for LDS"); return DCRT_E_LIMIT; }
+    {
+        // The persistent traversal kernels run exactly one resident wave of workgroups.
+        hipDeviceProp_t prop;
+        HIPCHECK(hipGetDeviceProperties(&prop, device));
+        int perCU = 0;
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false>, (int)castBlock, castLds));
+        castResident = (uint32_t)std::max(1, perCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
+    }
     HIPCHECK(hipStreamSynchronize(stream));
     hasScene = true;
     newImage = true;
@@ -860,7 +869,7 @@ DCRT_API int dcrt_tracer_set_luts(dcrt_tracer* t, const dcrt_bxdf_luts* luts)
 static int TraceBatch(dcrt_tracer* t, const dcrt_ray* d_rays, uint32_t n, dcrt_ray_hit* d_hits, uint32_t* d_occ, bool any, uint32_t features)
 {
     if (!t->hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
-    const uint32_t grid = (n + t->castBlock - 1) / t->castBlock;
+    const uint32_t grid = std::min<uint32_t>((n + t->castBlock - 1) / t->castBlock, t->castResident);
     if (n == 0) return DCRT_OK;
     unsigned long long* instr = t->instrCounters ? t->dInstr : nullptr;
     if (any)

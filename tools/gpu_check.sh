@@ -12,9 +12,5 @@ rc=$?; echo "pytest rc=$rc"; ok $rc || exit $rc
 timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 if [ -n "${PROFILE:-}" ]; then
-  ROOTDIR=$(pwd)
-  export TMPDIR=/tmp
-  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOTDIR/gpurun_out/prof" -o run -- \
-      python3 "$ROOTDIR/bench.py" --steps 16 --warmup 1 --no-cpu-baseline > "$ROOTDIR/gpurun_out/prof.log" 2>&1)
-  rc=$?; echo "rocprof rc=$rc"; exit $rc
+  bash tools/profile.sh; exit $?
 fi
