@@ -166,7 +166,7 @@ struct TravState {
 DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax)
 {
     s.o = o; s.d = d; s.invW = inv_dir(d);
-    s.lo = o; s.ld = d; s.inv = s.invW;
+    s.lo = o; s.ld = d; s.inv = inv_dir(d);
     s.tMin = tMin; s.tMax = tMax;
     s.node = 0; s.count = 0; s.inst = 0;
     s.inBlas = false; s.shearValid = false; s.found = false;
@@ -198,8 +198,10 @@ DEV bool trav_step(const DeviceScene& sc, TravState& s, bool watertight, bool f2
             pop = false;
         } else if (primOrInst == 0) {            // interior: near child next, far child pushed
             const uint32_t axis = misc & 0x3u;
-            bool neg = false;
-            if (f2b) neg = axis == 0 ? s.ld.x < 0.0f : (axis == 1 ? s.ld.y < 0.0f : s.ld.z < 0.0f);
+            // all three signs, combined with bit ops: a select over the components
+            // would become a variable-offset access that pins the state in scratch
+            const bool nx = s.ld.x < 0.0f, ny = s.ld.y < 0.0f, nz = s.ld.z < 0.0f;
+            const bool neg = f2b && ((axis == 0u && nx) | (axis == 1u && ny) | (axis == 2u && nz));
             const uint32_t right = asu(b.z);
             const uint32_t push = neg ? s.node + 1 : right;
             s.node = neg ? right : s.node + 1;
@@ -237,7 +239,14 @@ DEV bool trav_step(const DeviceScene& sc, TravState& s, bool watertight, bool f2
         const bool wasBlas = s.inBlas;
         s.node = packed & 0x7FFFFFFFu;
         s.inBlas = (packed & 0x80000000u) != 0;
-        if (wasBlas != s.inBlas) { s.lo = s.o; s.ld = s.d; s.inv = s.invW; s.shearValid = false; }
+        if (wasBlas != s.inBlas) {
+            // component-wise: a struct copy inside the state becomes an alloca-local
+            // memcpy that keeps SROA from promoting the state to registers
+            s.lo = mk(s.o.x, s.o.y, s.o.z);
+            s.ld = mk(s.d.x, s.d.y, s.d.z);
+            s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+            s.shearValid = false;
+        }
     }
     return false;
 }

@@ -56,10 +56,14 @@ DEV void qmap(const Counters* c, uint32_t q, QueueMap* m)
 }
 DEV uint32_t qentry(const uint32_t* queue, uint32_t cap, const QueueMap& m, uint32_t i)
 {
-    uint32_t s = 0;
+    uint32_t s = 0, base = 0;                 // static indices only: no scratch for the map
 #pragma unroll
-    for (uint32_t k = 1; k < kShards; ++k) s += i >= m.prefix[k] ? 1u : 0u;
-    return queue[(size_t)s * cap + (i - m.prefix[s])];
+    for (uint32_t k = 1; k < kShards; ++k) {
+        const bool ge = i >= m.prefix[k];
+        s += ge ? 1u : 0u;
+        base = ge ? m.prefix[k] : base;
+    }
+    return queue[(size_t)s * cap + (i - base)];
 }
 
 // Per-image constants, read from HBM so a captured graph can be replayed for

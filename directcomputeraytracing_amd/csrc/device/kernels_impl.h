@@ -257,6 +257,8 @@ __global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScen
 // [w*chunk, (w+1)*chunk) of the queue; every step, lanes whose ray finished take
 // the next items of the wave's range (ballot + mbcnt, no atomics), so all 64
 // lanes keep traversing until the range is drained.
+constexpr uint32_t kRefillLanes = 16;
+
 template <bool ANY_HIT, bool INSTR, typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t* lds,
                                                  uint32_t stride, Fetch fetch, Emit emit, TraversalStats& st)
@@ -273,8 +275,10 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
     bool active = false;
     uint32_t item = 0;
     for (;;) {
+        // refill only when at least kRefillLanes lanes are idle: the fetch (queue
+        // read, ray loads, three IEEE divisions) is then shared by many lanes
         const unsigned long long need = __ballot(!active);
-        if (need != 0ull && cursor < end) {
+        if ((uint32_t)__popcll(need) >= kRefillLanes && cursor < end) {
             const uint32_t idx = cursor + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
             if (!active && idx < end) {
                 item = fetch(idx, s);
@@ -283,9 +287,12 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             cursor = min(cursor + (uint32_t)__popcll(need), end);
         }
         if (__ballot(active) == 0ull) break;
-        if (active && trav_step<ANY_HIT, INSTR>(sc, s, watertight, f2b, lds, stride, st)) {
-            emit(item, s);
-            active = false;
+        for (;;) {
+            if (active && trav_step<ANY_HIT, INSTR>(sc, s, watertight, f2b, lds, stride, st)) {
+                emit(item, s);
+                active = false;
+            }
+            if ((uint32_t)__popcll(__ballot(!active)) >= kRefillLanes) break;
         }
     }
 }
@@ -306,13 +313,13 @@ __global__ __launch_bounds__(256) void extension_kernel(PathPool pool, DeviceSce
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<false, INSTR>(
         sc, qm.prefix[kShards], fc->features, stackMem + threadIdx.x, blockDim.x,
-        [&](uint32_t i, TravState& s) {
+        [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const uint32_t path = qentry(pool.extQueue, pool.size, qm, i);
             const float4 o = pool.rayO[path], d = pool.rayD[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf());
             return path;
         },
-        [&](uint32_t path, const TravState& s) {
+        [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
             pool.hit[path] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
             pool.hitInst[path] = s.found ? s.hit.inst : 0u;
         },
@@ -332,13 +339,13 @@ __global__ __launch_bounds__(256) void shadow_kernel(PathPool pool, DeviceScene 
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<true, INSTR>(
         sc, n, fc->features, stackMem + threadIdx.x, blockDim.x,
-        [&](uint32_t i, TravState& s) {
+        [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const uint32_t path = qentry(pool.shadowQueue, pool.size, qm, i);
             const float4 o = pool.shadowO[path], d = pool.shadowD[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, o.w);
             return path;
         },
-        [&](uint32_t path, const TravState& s) {
+        [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
             const uint32_t f = pool.flags[path];
             pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (f & 0xBFFFFFFFu);
         },
@@ -364,12 +371,12 @@ __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const 
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<ANY, true>(
         sc, n, features, stackMem + threadIdx.x, blockDim.x,
-        [&](uint32_t i, TravState& s) {
+        [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const dcrt_ray r = rays[i];
             trav_init(s, ld3(r.origin), ld3(r.direction), 0.0f, ANY ? r.t_max : inf());
             return i;
         },
-        [&](uint32_t i, const TravState& s) {
+        [&](uint32_t i, const TravState& s) __attribute__((always_inline)) {
             if (ANY) {
                 occluded[i] = s.found ? 1u : 0u;
             } else {
