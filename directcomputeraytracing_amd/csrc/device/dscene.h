@@ -158,7 +158,8 @@ struct TravState {
     V3 lo, ld, inv;       // ray in the current space (world or instance)
     float tMin, tMax;
     uint32_t node, count, inst;
-    bool inBlas, shearValid, found;
+    uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked)
+    bool inBlas, shearValid, found, parked;
     Shear sh;
     HitRecord hit;
 };
@@ -169,86 +170,107 @@ DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax)
     s.lo = o; s.ld = d; s.inv = inv_dir(d);
     s.tMin = tMin; s.tMax = tMax;
     s.node = 0; s.count = 0; s.inst = 0;
-    s.inBlas = false; s.shearValid = false; s.found = false;
+    s.leafRef = 0; s.leafMisc = 0;
+    s.inBlas = false; s.shearValid = false; s.found = false; s.parked = false;
     s.hit.t = 0.0f; s.hit.u = 0.0f; s.hit.v = 0.0f; s.hit.tri = 0u; s.hit.inst = 0u;
 }
 
-// Returns true when the ray is finished (stack empty, or first hit for ANY_HIT).
-template <bool ANY_HIT, bool INSTR>
-DEV bool trav_step(const DeviceScene& sc, TravState& s, bool watertight, bool f2b, uint32_t* lds, uint32_t stride,
-                   TraversalStats& st)
+// Pop the next node (BVHAccel.inc.hlsl stack pop); true when the stack is empty.
+DEV bool trav_pop(const DeviceScene& sc, TravState& s, const uint32_t* lds, uint32_t stride)
+{
+    if (s.count == 0) return true;
+    --s.count;
+    const uint32_t packed = s.count < sc.stackSize ? lds[s.count * stride] : 0u;
+    const bool wasBlas = s.inBlas;
+    s.node = packed & 0x7FFFFFFFu;
+    s.inBlas = (packed & 0x80000000u) != 0;
+    if (wasBlas != s.inBlas) {
+        // component-wise: a struct copy inside the state becomes an alloca-local
+        // memcpy that keeps SROA from promoting the state to registers
+        s.lo = mk(s.o.x, s.o.y, s.o.z);
+        s.ld = mk(s.d.x, s.d.y, s.d.z);
+        s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+        s.shearValid = false;
+    }
+    return false;
+}
+
+// Phase A: visit one node (iterationCounter). A missed node pops; an interior node
+// descends to the near child and pushes the far one; a leaf (TLAS or BLAS) parks
+// the lane with its work pending. Returns true when the ray is finished.
+template <bool INSTR>
+DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds, uint32_t stride, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
     const float4 a = sc.nodes[s.node * 2];
     const float4 b = sc.nodes[s.node * 2 + 1];
-    bool pop = true;
+    asm volatile("" ::"v"(b.w));     // fetch the whole node now, not misc after the slab test
     if (ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a, b)) {
         const uint32_t misc = asu(b.w);
         const uint32_t primOrInst = (misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
-        if (misc & 0x4u) {                       // TLAS leaf: enter the instance's BLAS
-            const float4* M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
-            s.lo = mul43(s.o, 1.0f, M);
-            s.ld = mul43(s.d, 0.0f, M);
-            s.inv = inv_dir(s.ld);
-            s.shearValid = false;
-            s.inBlas = true;
-            s.inst = primOrInst;
-            s.node = asu(b.z);
-            if (INSTR) ++st.blas;
-            pop = false;
-        } else if (primOrInst == 0) {            // interior: near child next, far child pushed
-            const uint32_t axis = misc & 0x3u;
-            // all three signs, combined with bit ops: a select over the components
-            // would become a variable-offset access that pins the state in scratch
-            const bool nx = s.ld.x < 0.0f, ny = s.ld.y < 0.0f, nz = s.ld.z < 0.0f;
-            const bool neg = f2b && ((axis == 0u && nx) | (axis == 1u && ny) | (axis == 2u && nz));
-            const uint32_t right = asu(b.z);
-            const uint32_t push = neg ? s.node + 1 : right;
-            s.node = neg ? right : s.node + 1;
-            if (s.count < sc.stackSize) lds[s.count * stride] = (push & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
-            ++s.count;
-            pop = false;
-        } else {                                 // BLAS leaf: triangles [begin, begin + count)
-            if (watertight && !s.shearValid) { s.sh = make_shear(s.ld); s.shearValid = true; }
-            const uint32_t begin = asu(b.z);
-            const uint32_t end = begin + primOrInst;
-            for (uint32_t p = begin; p < end; ++p) {
-                if (INSTR) ++st.tris;
-                const float4 q0 = sc.triVerts[(size_t)p * 3];
-                const float4 q1 = sc.triVerts[(size_t)p * 3 + 1];
-                const float4 q2 = sc.triVerts[(size_t)p * 3 + 2];
-                const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
-                float t, u, v; bool bf;
-                const bool h = watertight ? tri_watertight(s.lo, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
-                                          : tri_moller(s.lo, s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
-                if (h) {
-                    s.found = true;
-                    if (ANY_HIT) return true;
-                    s.tMax = t;
-                    s.hit.t = t; s.hit.u = u; s.hit.v = v;
-                    s.hit.tri = (p & 0x7FFFFFFFu) | (bf ? 0x80000000u : 0u);
-                    s.hit.inst = s.inst;
-                }
-            }
+        if ((misc & 0x4u) || primOrInst != 0) {          // TLAS leaf or BLAS leaf
+            s.parked = true;
+            s.leafRef = asu(b.z);
+            s.leafMisc = misc;
+            return false;
+        }
+        // interior: near child next, far child pushed. All three signs, combined with
+        // bit ops: a select over the components would become a variable-offset access
+        // that pins the state in scratch.
+        const uint32_t axis = misc & 0x3u;
+        const bool nx = s.ld.x < 0.0f, ny = s.ld.y < 0.0f, nz = s.ld.z < 0.0f;
+        const bool neg = f2b && ((axis == 0u && nx) | (axis == 1u && ny) | (axis == 2u && nz));
+        const uint32_t right = asu(b.z);
+        const uint32_t push = neg ? s.node + 1 : right;
+        s.node = neg ? right : s.node + 1;
+        if (s.count < sc.stackSize) lds[s.count * stride] = (push & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
+        ++s.count;
+        return false;
+    }
+    return trav_pop(sc, s, lds, stride);
+}
+
+// Phase B: the parked leaf's work. TLAS leaf: move the ray into the instance and
+// continue at its BLAS root. BLAS leaf: test triangles [ref, ref + count), then pop.
+template <bool ANY_HIT, bool INSTR>
+DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t stride, TraversalStats& st)
+{
+    s.parked = false;
+    const uint32_t primOrInst = (s.leafMisc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
+    if (s.leafMisc & 0x4u) {
+        const float4* M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
+        s.lo = mul43(s.o, 1.0f, M);
+        s.ld = mul43(s.d, 0.0f, M);
+        s.inv = inv_dir(s.ld);
+        s.shearValid = false;
+        s.inBlas = true;
+        s.inst = primOrInst;
+        s.node = s.leafRef;
+        if (INSTR) ++st.blas;
+        return false;
+    }
+    if (watertight && !s.shearValid) { s.sh = make_shear(s.ld); s.shearValid = true; }
+    const uint32_t begin = s.leafRef;
+    const uint32_t end = begin + primOrInst;
+    for (uint32_t p = begin; p < end; ++p) {
+        if (INSTR) ++st.tris;
+        const float4 q0 = sc.triVerts[(size_t)p * 3];
+        const float4 q1 = sc.triVerts[(size_t)p * 3 + 1];
+        const float4 q2 = sc.triVerts[(size_t)p * 3 + 2];
+        const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+        float t, u, v; bool bf;
+        const bool h = watertight ? tri_watertight(s.lo, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
+                                  : tri_moller(s.lo, s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
+        if (h) {
+            s.found = true;
+            if (ANY_HIT) return true;
+            s.tMax = t;
+            s.hit.t = t; s.hit.u = u; s.hit.v = v;
+            s.hit.tri = (p & 0x7FFFFFFFu) | (bf ? 0x80000000u : 0u);
+            s.hit.inst = s.inst;
         }
     }
-    if (pop) {
-        if (s.count == 0) return true;
-        --s.count;
-        const uint32_t packed = s.count < sc.stackSize ? lds[s.count * stride] : 0u;
-        const bool wasBlas = s.inBlas;
-        s.node = packed & 0x7FFFFFFFu;
-        s.inBlas = (packed & 0x80000000u) != 0;
-        if (wasBlas != s.inBlas) {
-            // component-wise: a struct copy inside the state becomes an alloca-local
-            // memcpy that keeps SROA from promoting the state to registers
-            s.lo = mk(s.o.x, s.o.y, s.o.z);
-            s.ld = mk(s.d.x, s.d.y, s.d.z);
-            s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
-            s.shearValid = false;
-        }
-    }
-    return false;
+    return trav_pop(sc, s, lds, stride);
 }
 
 // ---- texture emulation ----------------------------------------------------------

@@ -33,7 +33,10 @@ struct Globals {
     uint32_t nextBlock[kShards * kShardStride];        // per-shard pixel-block cursors
     uint32_t totalBlocks;
     uint32_t stackOverflow;
-    uint32_t pad0[2];
+    // device-side image sequencing (RenderImages): no host round trip between images
+    uint32_t imageComplete;   // SHADOW: this iteration's CONTROL found every path idle and nothing to claim
+    uint32_t stopped;         // all requested images are done: CONTROL claims nothing more
+    uint32_t imagesDone, imageTarget, seedBase, pad1;
     unsigned long long extRays, shadowRays, newPaths, iterations;
 };
 

@@ -51,7 +51,13 @@ __global__ void set_idle_kernel(PathPool pool, Counters* counters, Globals* g, u
     if (tid < pool.size) pool.flags[tid] = kFlagIdle;
     if (tid < 2 * (uint32_t)(sizeof(Counters) / 4)) ((uint32_t*)counters)[tid] = 0u;
     if (tid < kShards) g->nextBlock[tid * kShardStride] = 0u;
-    if (tid == 0) g->totalBlocks = totalBlocks;
+    if (tid == 0) {
+        g->totalBlocks = totalBlocks;
+        g->imageComplete = 0u;
+        g->stopped = 0u;
+        g->imagesDone = 0u;
+        g->imageTarget = 1u;
+    }
 }
 
 __global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32_t* triangles, uint32_t count, float4* out)
@@ -74,6 +80,7 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
                                                        Globals* g, uint32_t debugRng)
 {
     __shared__ uint32_t sm[64];
+    if (g->stopped) return;                    // RenderImages finished: nothing live, nothing to claim
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t shard = blockIdx.x % kShards;
     uint32_t* cursor = &g->nextBlock[shard * kShardStride];
@@ -258,6 +265,7 @@ __global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScen
 // the next items of the wave's range (ballot + mbcnt, no atomics), so all 64
 // lanes keep traversing until the range is drained.
 constexpr uint32_t kRefillLanes = 16;
+constexpr uint32_t kParkLanes = 32;
 
 template <bool ANY_HIT, bool INSTR, typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t* lds,
@@ -287,12 +295,22 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             cursor = min(cursor + (uint32_t)__popcll(need), end);
         }
         if (__ballot(active) == 0ull) break;
+        // phase A: node visits only, until enough lanes are parked at leaves (or
+        // enough are idle to refill, or none can advance)
         for (;;) {
-            if (active && trav_step<ANY_HIT, INSTR>(sc, s, watertight, f2b, lds, stride, st)) {
+            if (active && !s.parked && trav_visit<INSTR>(sc, s, f2b, lds, stride, st)) {
                 emit(item, s);
                 active = false;
             }
-            if ((uint32_t)__popcll(__ballot(!active)) >= kRefillLanes) break;
+            const unsigned long long runnable = __ballot(active && !s.parked);
+            const uint32_t parked = (uint32_t)__popcll(__ballot(active && s.parked));
+            const uint32_t idle = (uint32_t)__popcll(__ballot(!active));
+            if (runnable == 0ull || parked >= kParkLanes || (idle >= kRefillLanes && cursor < end)) break;
+        }
+        // phase B: the parked lanes' leaf work, shared by many lanes at once
+        if (active && s.parked && trav_leaf<ANY_HIT, INSTR>(sc, s, watertight, lds, stride, st)) {
+            emit(item, s);
+            active = false;
         }
     }
 }
@@ -354,9 +372,12 @@ __global__ __launch_bounds__(256) void shadow_kernel(PathPool pool, DeviceScene 
     // End of the iteration: account and clear the other parity's counters.
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
-            g->extRays += qtotal(cnt, kQExt);
+            const uint32_t ext = qtotal(cnt, kQExt), material = qtotal(cnt, kQMaterial);
+            g->extRays += ext;
             g->shadowRays += n;
             g->iterations += 1ull;
+            // IsImageComplete (WavefrontPathTracer.cpp:508-523), exact and on the device
+            g->imageComplete = (material == 0u && ext == 0u && !g->stopped) ? 1u : 0u;
         }
         if (threadIdx.x < kQueues * kShards) nextCnt->w[threadIdx.x * kShardStride] = 0u;
     }
@@ -439,34 +460,63 @@ __device__ __forceinline__ float evaluate_filter(const FilterConsts& c, float px
     }
 }
 
-__global__ void film_kernel(Film film, FilterConsts c, uint32_t worldSize, uint32_t rank, uint32_t stripeHeight)
+// SampleConvolution (SampleConvolution.hlsl:67-106), grid-stride over pixels. With
+// `guard` set it runs only in the iteration that completed an image (RenderImages).
+__global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t worldSize, uint32_t rank,
+                                                   uint32_t stripeHeight, const Globals* guard)
 {
-    const uint32_t px = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t py = blockIdx.y * blockDim.y + threadIdx.y;
+    if (guard && !guard->imageComplete) return;
+    const FilterConsts c = *fcon;
     const uint32_t W = film.width, H = film.height;
-    if (px >= W || py >= H) return;
-    if (worldSize > 1 && (py / stripeHeight) % worldSize != rank) return;
-    const float r = c.radius;
-    const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
-    int xs = (int)floorf(cx - r); xs = xs < 0 ? 0 : xs;
-    int xe = (int)floorf(cx + r); xe = xe > (int)W - 1 ? (int)W - 1 : xe;
-    int ys = (int)floorf(cy - r); ys = ys < 0 ? 0 : ys;
-    int ye = (int)floorf(cy + r); ye = ye > (int)H - 1 ? (int)H - 1 : ye;
-    float wsum = 0.0f;
-    V3 sum = mk(0.0f, 0.0f, 0.0f);
-    for (int y = ys; y <= ye; ++y)
-        for (int x = xs; x <= xe; ++x) {
-            const size_t q = (size_t)y * W + x;
-            const float2 sp = film.samplePosition[q];
-            const float4 sv = film.sampleValue[q];
-            const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
-            sum = sum + mk(sv.x, sv.y, sv.z) * w;
-            wsum = wsum + w;
-        }
-    const size_t p = (size_t)py * W + px;
-    float4 v = film.accum[p];
-    v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
-    film.accum[p] = v;
+    const uint32_t total = W * H;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
+        const uint32_t py = p / W, px = p - py * W;
+        if (worldSize > 1 && (py / stripeHeight) % worldSize != rank) continue;
+        const float r = c.radius;
+        const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
+        int xs = (int)floorf(cx - r); xs = xs < 0 ? 0 : xs;
+        int xe = (int)floorf(cx + r); xe = xe > (int)W - 1 ? (int)W - 1 : xe;
+        int ys = (int)floorf(cy - r); ys = ys < 0 ? 0 : ys;
+        int ye = (int)floorf(cy + r); ye = ye > (int)H - 1 ? (int)H - 1 : ye;
+        float wsum = 0.0f;
+        V3 sum = mk(0.0f, 0.0f, 0.0f);
+        for (int y = ys; y <= ye; ++y)
+            for (int x = xs; x <= xe; ++x) {
+                const size_t q = (size_t)y * W + x;
+                const float2 sp = film.samplePosition[q];
+                const float4 sv = film.sampleValue[q];
+                const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
+                sum = sum + mk(sv.x, sv.y, sv.z) * w;
+                wsum = wsum + w;
+            }
+        float4 v = film.accum[p];
+        v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
+        film.accum[p] = v;
+    }
+}
+
+// After the film pass of a completed image: next frame seed, rewind the block cursors.
+__global__ void advance_image_kernel(FrameConstants* fc, Globals* g)
+{
+    if (threadIdx.x != 0 || !g->imageComplete) return;
+    g->imageComplete = 0u;
+    g->imagesDone += 1u;
+    if (g->imagesDone < g->imageTarget) {
+        fc->frameSeed = g->seedBase + g->imagesDone;
+        for (uint32_t s = 0; s < kShards; ++s) g->nextBlock[s * kShardStride] = 0u;
+    } else {
+        g->stopped = 1u;
+    }
+}
+
+__global__ void begin_images_kernel(Globals* g, uint32_t count, uint32_t firstSeed)
+{
+    if (threadIdx.x != 0) return;
+    g->imagesDone = 0u;
+    g->imageTarget = count;
+    g->seedBase = firstSeed;
+    g->stopped = count == 0u ? 1u : 0u;
+    g->imageComplete = 0u;
 }
 
 // ---- BxDF LUT integration (BxDFTexturesBuilding.hlsl, "%f" defines) -------------------------

@@ -116,10 +116,17 @@ struct dcrt_tracer {
     bool filmClearTrigger = false;
     uint32_t parity = 0;
 
-    // graph of `graphIters` iterations (even), rebuilt when launch parameters change
-    hipGraphExec_t graphExec = nullptr;
-    uint32_t graphIters = 0;
-    bool graphValid = false;
+    // graphs of `iters` iterations (even), rebuilt when launch parameters change;
+    // [0] = plain iterations (Render), [1] = with the guarded film pass and image
+    // advance (RenderImages)
+    struct GraphCache {
+        hipGraphExec_t exec = nullptr;
+        uint32_t iters = 0;
+    } graphs[2];
+    FilterConsts* dFilter = nullptr;
+    FilterConsts* hFilter = nullptr;   // pinned staging
+    uint32_t* hStop = nullptr;         // pinned [kInflight]
+    hipEvent_t stopEvents[4] = {};
     bool instrCounters = false;
     bool extTiming = false;
     std::vector<hipEvent_t> events;
@@ -136,18 +143,23 @@ struct dcrt_tracer {
     int EnsureFilm(uint32_t w, uint32_t h);
     int BuildBands();
     int BeginImage();
-    int LaunchIteration(uint32_t par, bool timed);
+    int LaunchIteration(uint32_t par, bool timed, bool sequenced);
+    int LaunchGraph(bool sequenced, uint32_t iters);
     int RunIterations(uint32_t n);
+    int UploadFilter(const dcrt_filter_params& f);
     int ReadCompletion(bool* complete);
     int Render(uint32_t maxIterations);
     int RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_filter_params& filter);
     int Accumulate(const dcrt_filter_params& filter);
     void InvalidateGraph()
     {
-        if (graphExec) (void)hipGraphExecDestroy(graphExec);
-        graphExec = nullptr;
-        graphValid = false;
+        for (GraphCache& g : graphs) {
+            if (g.exec) (void)hipGraphExecDestroy(g.exec);
+            g.exec = nullptr;
+            g.iters = 0;
+        }
     }
+    uint32_t FilmGrid() const { return std::max<uint32_t>(1u, std::min<uint32_t>((filmW * filmH + 255) / 256, kMaxPersistentBlocks)); }
     uint32_t castResident = 0;         // persistent cast grid: resident workgroups on the whole chip
     uint32_t CastGrid(uint32_t block) const { return std::min<uint32_t>((poolSize + block - 1) / block, castResident); }
 };
@@ -158,6 +170,9 @@ dcrt_tracer::~dcrt_tracer()
     if (stream) (void)hipStreamSynchronize(stream);
     InvalidateGraph();
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : stopEvents) if (e) (void)hipEventDestroy(e);
+    if (hFilter) (void)hipHostFree(hFilter);
+    if (hStop) (void)hipHostFree(hStop);
     FreeAll(&poolAllocs);
     FreeAll(&sceneAllocs);
     FreeAll(&filmAllocs);
@@ -213,6 +228,10 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     HIPCHECK(hipMemsetAsync(dGlobals, 0, sizeof(Globals), stream));
     HIPCHECK(hipMemsetAsync(dInstr, 0, 8 * sizeof(unsigned long long), stream));
     HIPCHECK(hipHostMalloc((void**)&hCounters, 2 * sizeof(Counters), hipHostMallocDefault));
+    CHECKED(DeviceAlloc(&dFilter, 1, &poolAllocs));
+    HIPCHECK(hipHostMalloc((void**)&hFilter, sizeof(FilterConsts), hipHostMallocDefault));
+    HIPCHECK(hipHostMalloc((void**)&hStop, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    for (hipEvent_t& e : stopEvents) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     CHECKED(BuildLuts());
     HIPCHECK(hipStreamSynchronize(stream));
     return DCRT_OK;
@@ -469,7 +488,9 @@ int dcrt_tracer::BeginImage()
 // RenderOneIteration (WavefrontPathTracer.cpp:622-1162): CONTROL(+NEW_PATH) ->
 // MATERIAL -> EXTENSION_RAY_CAST -> SHADOW_RAY_CAST. Queue sizes are read on the
 // device, so no indirect-argument pass and no host round trip is needed.
-int dcrt_tracer::LaunchIteration(uint32_t par, bool timed)
+// `sequenced` appends the film pass and the image advance, both no-ops unless
+// this iteration completed an image (RenderImages runs images back to back).
+int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
 {
     Counters* cnt = dCounters + par;
     Counters* next = dCounters + (par ^ 1u);
@@ -503,55 +524,50 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed)
     else
         hipLaunchKernelGGL(shadow_kernel<false>, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
                            next, dGlobals, dInstr);
+    if (sequenced) {
+        hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, partition.world_size,
+                           partition.rank, std::max<uint32_t>(partition.stripe_height, 1), (const Globals*)dGlobals);
+        hipLaunchKernelGGL(advance_image_kernel, dim3(1), dim3(64), 0, stream, dFrame, dGlobals);
+    }
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
 }
 
-// n iterations; when n is even and event timing is off they replay a captured graph.
+// Replay `iters` iterations (even, starting at parity 0) as one captured graph.
+int dcrt_tracer::LaunchGraph(bool sequenced, uint32_t iters)
+{
+    GraphCache& gc = graphs[sequenced ? 1 : 0];
+    if (!gc.exec || gc.iters != iters) {
+        if (gc.exec) (void)hipGraphExecDestroy(gc.exec);
+        gc.exec = nullptr;
+        hipGraph_t g = nullptr;
+        HIPCHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        int rc = DCRT_OK;
+        for (uint32_t i = 0; i < iters && rc == DCRT_OK; ++i) rc = LaunchIteration(i & 1u, false, sequenced);
+        hipError_t ec = hipStreamEndCapture(stream, &g);
+        if (rc != DCRT_OK) return rc;
+        HIPCHECK(ec);
+        HIPCHECK(hipGraphInstantiate(&gc.exec, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+        gc.iters = iters;
+    }
+    HIPCHECK(hipGraphLaunch(gc.exec, stream));
+    return DCRT_OK;
+}
+
+// n plain iterations (Render); even chunks replay a captured graph.
 int dcrt_tracer::RunIterations(uint32_t n)
 {
-    if (extTiming) {
-        for (uint32_t i = 0; i < n; ++i) {
-            CHECKED(LaunchIteration(parity, true));
-            parity ^= 1u;
-        }
-        return DCRT_OK;
-    }
-    while (n >= 2) {
-        const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
-        if (n >= chunk) {
-            if (!graphValid || graphIters != chunk) {
-                InvalidateGraph();
-                hipGraph_t g = nullptr;
-                HIPCHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-                int rc = DCRT_OK;
-                for (uint32_t i = 0; i < chunk && rc == DCRT_OK; ++i) rc = LaunchIteration(i & 1u, false);
-                hipError_t ec = hipStreamEndCapture(stream, &g);
-                if (rc != DCRT_OK) return rc;
-                HIPCHECK(ec);
-                HIPCHECK(hipGraphInstantiate(&graphExec, g, nullptr, nullptr, 0));
-                (void)hipGraphDestroy(g);
-                graphIters = chunk;
-                graphValid = true;
-            }
-            if (parity != 0) {   // keep the graph's parity pattern aligned
-                CHECKED(LaunchIteration(parity, false));
-                parity ^= 1u;
-                --n;
-                continue;
-            }
-            HIPCHECK(hipGraphLaunch(graphExec, stream));
+    const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
+    while (n > 0) {
+        if (!extTiming && parity == 0 && n >= chunk) {
+            CHECKED(LaunchGraph(false, chunk));
             n -= chunk;
         } else {
-            CHECKED(LaunchIteration(parity, false));
+            CHECKED(LaunchIteration(parity, extTiming, false));
             parity ^= 1u;
             --n;
         }
-    }
-    while (n > 0) {
-        CHECKED(LaunchIteration(parity, false));
-        parity ^= 1u;
-        --n;
     }
     return DCRT_OK;
 }
@@ -585,37 +601,80 @@ int dcrt_tracer::Render(uint32_t maxIterations)
     return DCRT_OK;
 }
 
+int dcrt_tracer::UploadFilter(const dcrt_filter_params& f)
+{
+    HIPCHECK(hipStreamSynchronize(stream));     // the pinned staging buffer is reused
+    *hFilter = MakeFilter(f);
+    HIPCHECK(hipMemcpyAsync(dFilter, hFilter, sizeof(FilterConsts), hipMemcpyHostToDevice, stream));
+    return DCRT_OK;
+}
+
 int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
 {
     if (!film.accum) { SetLastError("no film"); return DCRT_E_INVALID_ARG; }
-    const FilterConsts c = MakeFilter(f);
-    const dim3 block(16, 16), grid((filmW + 15) / 16, (filmH + 15) / 16);
-    hipLaunchKernelGGL(film_kernel, grid, block, 0, stream, film, c, partition.world_size, partition.rank,
-                       std::max<uint32_t>(partition.stripe_height, 1));
+    CHECKED(UploadFilter(f));
+    hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, partition.world_size,
+                       partition.rank, std::max<uint32_t>(partition.stripe_height, 1), (const Globals*)nullptr);
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
 }
 
+// Images firstSeed .. firstSeed+count-1 back to back: the device detects each
+// image's completion, convolves it into the film and starts the next one, so the
+// host only enqueues graphs and polls a pinned "stopped" word two graphs behind.
 int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_filter_params& filter)
 {
     if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
-    const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
-    for (uint32_t img = 0; img < count; ++img) {
-        frame.frame_seed = firstSeed + img;
-        CHECKED(BeginImage());
-        for (uint32_t guard = 0;; ++guard) {
-            CHECKED(RunIterations(chunk));
-            bool complete = false;
-            CHECKED(ReadCompletion(&complete));
-            if (complete) break;
-            if (guard > 100000) { SetLastError("image did not complete"); return DCRT_E_LIMIT; }
+    if (count == 0) return DCRT_OK;
+    frame.frame_seed = firstSeed;
+    CHECKED(UploadFilter(filter));
+    CHECKED(BeginImage());
+    hipLaunchKernelGGL(begin_images_kernel, dim3(1), dim3(64), 0, stream, dGlobals, count, firstSeed);
+    HIPCHECK(hipGetLastError());
+    // a path needs maxBounce + 3 iterations; cap the total so a broken scene cannot spin forever
+    const uint64_t maxIterations = ((uint64_t)count + 2) * (frame.max_bounce_count + 8) * (1 + (filmW * (uint64_t)filmH) / poolSize) + 64;
+    uint64_t launched = 0;
+    bool stopped = false;
+    if (extTiming) {
+        while (!stopped && launched < maxIterations) {
+            for (uint32_t i = 0; i < 8; ++i, ++launched) {
+                CHECKED(LaunchIteration(parity, true, true));
+                parity ^= 1u;
+            }
+            HIPCHECK(hipMemcpyAsync(hStop, &dGlobals->stopped, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+            HIPCHECK(hipStreamSynchronize(stream));
+            stopped = hStop[0] != 0;
         }
-        CHECKED(Accumulate(filter));
+    } else {
+        const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
+        uint32_t inflight[4];
+        uint32_t head = 0, size = 0, slot = 0;
+        while (!stopped && launched < maxIterations) {
+            CHECKED(LaunchGraph(true, chunk));
+            launched += chunk;
+            HIPCHECK(hipMemcpyAsync(&hStop[slot], &dGlobals->stopped, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+            HIPCHECK(hipEventRecord(stopEvents[slot], stream));
+            inflight[(head + size) % 4] = slot;
+            ++size;
+            slot = (slot + 1) % 4;
+            if (size >= 2) {
+                const uint32_t s0 = inflight[head];
+                HIPCHECK(hipEventSynchronize(stopEvents[s0]));
+                stopped = hStop[s0] != 0;
+                head = (head + 1) % 4;
+                --size;
+            }
+        }
+        // graphs still in flight after `stopped` find no work (CONTROL returns at once)
+    }
+    HIPCHECK(hipStreamSynchronize(stream));
+    if (!stopped) {
+        HIPCHECK(hipMemcpy(hStop, &dGlobals->stopped, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (!hStop[0]) { SetLastError("images did not complete"); return DCRT_E_LIMIT; }
     }
     imageComplete = true;
     newImage = true;
-    HIPCHECK(hipStreamSynchronize(stream));
     return DCRT_OK;
 }
 
