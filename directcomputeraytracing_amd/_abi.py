@@ -196,7 +196,7 @@ def load_library(path: os.PathLike | str | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    p = Path(path) if path else Path(os.environ.get("DCRT_LIB", LIB_PATH))
     if not p.exists():
         raise DCRTError(f"native library {p} is missing: run __graft_entry__.build() (no CPU fallback exists)")
     lib = C.CDLL(str(p))

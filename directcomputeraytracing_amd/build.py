@@ -59,19 +59,21 @@ def _digest(paths) -> str:
     return h.hexdigest()
 
 
-def build_native(force: bool = False, verbose: bool = False) -> Path:
+def build_native(force: bool = False, verbose: bool = False, out: Path | None = None, extra_flags=()) -> Path:
+    """Compile libdcrt.so (or an experimental variant at `out` with `extra_flags`)."""
+    lib_path = Path(out) if out else LIB_PATH
     sources = HOST_SOURCES + DEVICE_SOURCES
-    digest = _digest(sources + HEADERS)
-    stamp = LIB_PATH.with_suffix(".so.sha256")
-    if not force and LIB_PATH.exists() and stamp.exists() and stamp.read_text().strip() == digest:
-        return LIB_PATH
-    objdir = PKG_DIR / "_build"
+    digest = _digest(sources + HEADERS) + " ".join(extra_flags)
+    stamp = lib_path.with_suffix(".so.sha256")
+    if not force and lib_path.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+        return lib_path
+    objdir = PKG_DIR / ("_build" if out is None else "_build_" + lib_path.stem)
     objdir.mkdir(exist_ok=True)
     objs = []
     procs = []
     for src in sources:
         obj = objdir / (src.stem + (".dev.o" if src.suffix == ".hip" else ".o"))
-        cmd = [_hipcc(), *HIPCC_FLAGS, "-c", str(src), "-o", str(obj)]
+        cmd = [_hipcc(), *HIPCC_FLAGS, *extra_flags, "-c", str(src), "-o", str(obj)]
         if src.suffix == ".cpp":
             cmd = [_hipcc(), *[f for f in HIPCC_FLAGS if f not in ("--offload-arch=gfx950", "-fno-gpu-rdc")],
                    "-x", "c++", "-c", str(src), "-o", str(obj)]
@@ -89,12 +91,12 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
     if failed:
         msg = "\n".join(f"--- {s} ---\n{o}" for s, o in failed)
         raise RuntimeError(f"native build failed:\n{msg}")
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+    tmp = lib_path.with_suffix(".so.tmp")
     cmd = [_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB_PATH)
+    os.replace(tmp, lib_path)
     stamp.write_text(digest)
-    return LIB_PATH
+    return lib_path
 
 
 def build_oracle(force: bool = False) -> Path:

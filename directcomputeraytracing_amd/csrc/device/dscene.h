@@ -25,6 +25,7 @@ struct DeviceScene {
     const float4* transforms;     // 3 x float4 per matrix, 2N matrices (forward, inverse)
     const uint32_t* instanceLightIndices;
     const uint32_t* instanceFlags;
+    const uint32_t* instanceIdentity;   // 1: inverse transform is exactly the identity
     const uint32_t* overrides;
     const dcrt_material* materials;
     const dcrt_light* lights;
@@ -159,7 +160,7 @@ struct TravState {
     float tMin, tMax;
     uint32_t node, count, inst;
     uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked)
-    bool inBlas, shearValid, found, parked;
+    bool inBlas, shearValid, found, parked, noZero;   // noZero: no component of o, d is +-0
     Shear sh;
     HitRecord hit;
 };
@@ -172,6 +173,7 @@ DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax)
     s.node = 0; s.count = 0; s.inst = 0;
     s.leafRef = 0; s.leafMisc = 0;
     s.inBlas = false; s.shearValid = false; s.found = false; s.parked = false;
+    s.noZero = o.x != 0.0f && o.y != 0.0f && o.z != 0.0f && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
     s.hit.t = 0.0f; s.hit.u = 0.0f; s.hit.v = 0.0f; s.hit.tri = 0u; s.hit.inst = 0u;
 }
 
@@ -198,36 +200,45 @@ DEV bool trav_pop(const DeviceScene& sc, TravState& s, const uint32_t* lds, uint
 // Phase A: visit one node (iterationCounter). A missed node pops; an interior node
 // descends to the near child and pushes the far one; a leaf (TLAS or BLAS) parks
 // the lane with its work pending. Returns true when the ray is finished.
+// Written without divergent branches: the push always stores (slot `count`, or the
+// spare slot `stackSize` past the end, which nothing reads), the pop always loads
+// the top, and selects pick the outcome; the lanes of a wave stay convergent.
 template <bool INSTR>
 DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds, uint32_t stride, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
     const float4 a = sc.nodes[s.node * 2];
     const float4 b = sc.nodes[s.node * 2 + 1];
-    asm volatile("" ::"v"(b.w));     // fetch the whole node now, not misc after the slab test
-    if (ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a, b)) {
-        const uint32_t misc = asu(b.w);
-        const uint32_t primOrInst = (misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
-        if ((misc & 0x4u) || primOrInst != 0) {          // TLAS leaf or BLAS leaf
-            s.parked = true;
-            s.leafRef = asu(b.z);
-            s.leafMisc = misc;
-            return false;
-        }
-        // interior: near child next, far child pushed. All three signs, combined with
-        // bit ops: a select over the components would become a variable-offset access
-        // that pins the state in scratch.
-        const uint32_t axis = misc & 0x3u;
-        const bool nx = s.ld.x < 0.0f, ny = s.ld.y < 0.0f, nz = s.ld.z < 0.0f;
-        const bool neg = f2b && ((axis == 0u && nx) | (axis == 1u && ny) | (axis == 2u && nz));
-        const uint32_t right = asu(b.z);
-        const uint32_t push = neg ? s.node + 1 : right;
-        s.node = neg ? right : s.node + 1;
-        if (s.count < sc.stackSize) lds[s.count * stride] = (push & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
-        ++s.count;
-        return false;
-    }
-    return trav_pop(sc, s, lds, stride);
+    const bool hit = ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a, b);
+    const uint32_t misc = asu(b.w);
+    const uint32_t right = asu(b.z);
+    const bool leaf = (misc & 0x4u) != 0u || ((misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT) != 0u;
+    const bool descend = hit && !leaf;
+    // near/far by the split axis' direction sign. All three signs, combined with bit
+    // ops: a select over the components would become a variable-offset access that
+    // pins the state in scratch.
+    const uint32_t axis = misc & 0x3u;
+    const bool nx = s.ld.x < 0.0f, ny = s.ld.y < 0.0f, nz = s.ld.z < 0.0f;
+    const bool neg = f2b && ((axis == 0u && nx) | (axis == 1u && ny) | (axis == 2u && nz));
+    const uint32_t nearChild = neg ? right : s.node + 1;
+    const uint32_t farChild = neg ? s.node + 1 : right;
+    const uint32_t top = lds[(s.count > 0u ? min(s.count - 1u, sc.stackSize) : sc.stackSize) * stride];
+    lds[min(s.count, sc.stackSize) * stride] = (farChild & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
+    const bool pop = !hit && s.count > 0u;
+    const bool done = !hit && s.count == 0u;
+    const bool popBlas = (top & 0x80000000u) != 0u;
+    const bool restore = pop && s.inBlas && !popBlas;    // BLAS -> TLAS: back to the world ray
+    s.node = descend ? nearChild : (pop ? (top & 0x7FFFFFFFu) : s.node);
+    s.count = descend ? s.count + 1u : (pop ? s.count - 1u : s.count);
+    s.inBlas = pop ? popBlas : s.inBlas;
+    s.lo = mk(restore ? s.o.x : s.lo.x, restore ? s.o.y : s.lo.y, restore ? s.o.z : s.lo.z);
+    s.ld = mk(restore ? s.d.x : s.ld.x, restore ? s.d.y : s.ld.y, restore ? s.d.z : s.ld.z);
+    s.inv = mk(restore ? s.invW.x : s.inv.x, restore ? s.invW.y : s.inv.y, restore ? s.invW.z : s.inv.z);
+    s.shearValid = s.shearValid && !restore;
+    s.parked = hit && leaf;
+    s.leafRef = right;
+    s.leafMisc = misc;
+    return done;
 }
 
 // Phase B: the parked leaf's work. TLAS leaf: move the ray into the instance and
@@ -238,10 +249,17 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
     s.parked = false;
     const uint32_t primOrInst = (s.leafMisc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
     if (s.leafMisc & 0x4u) {
-        const float4* M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
-        s.lo = mul43(s.o, 1.0f, M);
-        s.ld = mul43(s.d, 0.0f, M);
-        s.inv = inv_dir(s.ld);
+        if (s.noZero && sc.instanceIdentity[primOrInst]) {
+            // x*1 + y*0 + z*0 + w*0 == x exactly for finite nonzero components
+            s.lo = mk(s.o.x, s.o.y, s.o.z);
+            s.ld = mk(s.d.x, s.d.y, s.d.z);
+            s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+        } else {
+            const float4* M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
+            s.lo = mul43(s.o, 1.0f, M);
+            s.ld = mul43(s.d, 0.0f, M);
+            s.inv = inv_dir(s.ld);
+        }
         s.shearValid = false;
         s.inBlas = true;
         s.inst = primOrInst;

@@ -82,6 +82,7 @@ struct FrameConstants {
     uint32_t frameSeed;
     uint32_t maxBounce, lightCount, envLightIndex, features;
     uint32_t blocksX, bandCount;     // blocks per row, number of 8-row bands
+    uint32_t refillLanes, parkLanes; // persistent traversal thresholds (lanes of a wave64)
 };
 
 // SampleAperture + GenerateRay (RayTracingCommon.inc.hlsl:38-86).

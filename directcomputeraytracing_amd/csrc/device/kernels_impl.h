@@ -259,17 +259,24 @@ __global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScen
     }
 }
 
+// Occupancy experiments only (tools/ab_libs.sh): forcing more waves spills the
+// traversal state and measured slower, so by default the compiler chooses.
+#ifdef DCRT_CAST_WAVES_PER_EU
+#define DCRT_CAST_OCCUPANCY __attribute__((amdgpu_waves_per_eu(DCRT_CAST_WAVES_PER_EU, 8)))
+#else
+#define DCRT_CAST_OCCUPANCY
+#endif
+
 // ---- EXTENSION_RAY_CAST / SHADOW_RAY_CAST ----------------------------------------------
 // Persistent while-while loop with per-lane dynamic fetch: wave w owns items
 // [w*chunk, (w+1)*chunk) of the queue; every step, lanes whose ray finished take
 // the next items of the wave's range (ballot + mbcnt, no atomics), so all 64
 // lanes keep traversing until the range is drained.
-constexpr uint32_t kRefillLanes = 16;
-constexpr uint32_t kParkLanes = 32;
 
 template <bool ANY_HIT, bool INSTR, typename Fetch, typename Emit>
-__device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t* lds,
-                                                 uint32_t stride, Fetch fetch, Emit emit, TraversalStats& st)
+__device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
+                                                 uint32_t kParkLanes, uint32_t* lds, uint32_t stride, Fetch fetch, Emit emit,
+                                                 TraversalStats& st)
 {
     const bool watertight = (features & DCRT_FEATURE_WATERTIGHT) != 0;
     const bool f2b = (features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
@@ -322,7 +329,7 @@ __device__ __forceinline__ void flush_stats(const TraversalStats& st, unsigned l
 }
 
 template <bool INSTR>
-__global__ __launch_bounds__(256) void extension_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, const Counters* cnt,
+__global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, const Counters* cnt,
                                                          Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
@@ -330,7 +337,7 @@ __global__ __launch_bounds__(256) void extension_kernel(PathPool pool, DeviceSce
     qmap(cnt, kQExt, &qm);
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<false, INSTR>(
-        sc, qm.prefix[kShards], fc->features, stackMem + threadIdx.x, blockDim.x,
+        sc, qm.prefix[kShards], fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, blockDim.x,
         [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const uint32_t path = qentry(pool.extQueue, pool.size, qm, i);
             const float4 o = pool.rayO[path], d = pool.rayD[path];
@@ -347,7 +354,7 @@ __global__ __launch_bounds__(256) void extension_kernel(PathPool pool, DeviceSce
 }
 
 template <bool INSTR>
-__global__ __launch_bounds__(256) void shadow_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
+__global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
                                                       Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
@@ -356,7 +363,7 @@ __global__ __launch_bounds__(256) void shadow_kernel(PathPool pool, DeviceScene 
     const uint32_t n = qm.prefix[kShards];
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<true, INSTR>(
-        sc, n, fc->features, stackMem + threadIdx.x, blockDim.x,
+        sc, n, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, blockDim.x,
         [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const uint32_t path = qentry(pool.shadowQueue, pool.size, qm, i);
             const float4 o = pool.shadowO[path], d = pool.shadowD[path];
@@ -391,7 +398,7 @@ __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const 
     extern __shared__ uint32_t stackMem[];
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<ANY, true>(
-        sc, n, features, stackMem + threadIdx.x, blockDim.x,
+        sc, n, features, 16u, 32u, stackMem + threadIdx.x, blockDim.x,
         [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const dcrt_ray r = rays[i];
             trav_init(s, ld3(r.origin), ld3(r.direction), 0.0f, ANY ? r.t_max : inf());

@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -88,6 +90,7 @@ struct dcrt_tracer {
     uint32_t poolSize = 0;
     uint32_t iterationsPerRender = kDefaultIterations;
     bool debugRng = false;
+    uint32_t refillLanes = 16, parkLanes = 32;   // DCRT_TRAVERSAL_TUNE="refill,park" overrides
 
     std::vector<void*> poolAllocs, sceneAllocs, filmAllocs;
     PathPool pool{};
@@ -200,6 +203,13 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     poolSize = (poolSize + 255u) & ~255u;   // whole 256-thread workgroups of whole waves
     iterationsPerRender = cfg.iterations_per_render ? cfg.iterations_per_render : kDefaultIterations;
     debugRng = cfg.debug_rng != 0;
+    if (const char* tune = std::getenv("DCRT_TRAVERSAL_TUNE")) {
+        unsigned r = 0, p = 0;
+        if (std::sscanf(tune, "%u,%u", &r, &p) == 2 && r >= 1 && r <= 64 && p >= 1 && p <= 64) {
+            refillLanes = r;
+            parkLanes = p;
+        }
+    }
     // WavefrontPathTracer.cpp:120-264 (SoA instead of AoS)
     const size_t P = poolSize;
     CHECKED(DeviceAlloc(&pool.rayO, P, &poolAllocs));
@@ -293,6 +303,19 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     CHECKED(upload(&lidx, s.instance_light_indices, s.instance_count));
     CHECKED(upload(&iflags, s.instance_flags, s.instance_count));
     CHECKED(upload(&ovr, s.instance_material_overrides, s.instance_count));
+    // instances whose world->instance matrix is exactly the identity (every OBJ shape):
+    // traversal then reuses the world ray instead of transforming it (bit-identical
+    // when no ray component is zero, which the kernel checks per ray)
+    std::vector<uint32_t> identity(s.instance_count, 0u);
+    for (uint32_t i = 0; i < s.instance_count; ++i) {
+        const float* m = s.instance_transforms[s.instance_count + i].m;
+        bool id = true;
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) id = id && m[r * 4 + c] == (r == c ? 1.0f : 0.0f);
+        identity[i] = id ? 1u : 0u;
+    }
+    uint32_t* ident = nullptr;
+    CHECKED(upload(&ident, identity.data(), s.instance_count));
     CHECKED(upload(&mats, s.materials, s.material_count));
     CHECKED(upload(&lights, s.lights, std::max<uint32_t>(s.light_count, 1)));
     float4* triVerts = nullptr;
@@ -331,6 +354,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     d.transforms = (const float4*)xf;
     d.instanceLightIndices = lidx;
     d.instanceFlags = iflags;
+    d.instanceIdentity = ident;
     d.overrides = ovr;
     d.materials = mats;
     d.lights = lights;
@@ -351,9 +375,10 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     d.stackSize = std::max<uint32_t>(s.bvh_traversal_stack_size, 1u);
     scene = d;
     // LDS stack: [stackSize][block] u32; keep a workgroup's stack <= 32 KiB
+    // (+1: a spare slot per lane that the branch-free push may write, never read)
     castBlock = 256;
-    while (castBlock > 64 && (size_t)d.stackSize * castBlock * 4 > 32768) castBlock >>= 1;
-    castLds = (size_t)d.stackSize * castBlock * 4;
+    while (castBlock > 64 && (size_t)(d.stackSize + 1) * castBlock * 4 > 32768) castBlock >>= 1;
+    castLds = (size_t)(d.stackSize + 1) * castBlock * 4;
     if (castLds > 65536) { SetLastError("BVH traversal stack too deep for LDS"); return DCRT_E_LIMIT; }
     {
         // The persistent traversal kernels run exactly one resident wave of workgroups.
@@ -361,6 +386,10 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         HIPCHECK(hipGetDeviceProperties(&prop, device));
         int perCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false>, (int)castBlock, castLds));
+        if (const char* b = std::getenv("DCRT_CAST_BLOCKS_PER_CU")) {   // tuning experiments
+            const int v = std::atoi(b);
+            if (v >= 1 && v < perCU) perCU = v;
+        }
         castResident = (uint32_t)std::max(1, perCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
     }
     HIPCHECK(hipStreamSynchronize(stream));
@@ -474,6 +503,8 @@ int dcrt_tracer::BeginImage()
     fc.features = frame.features;
     fc.blocksX = (frame.resolution[0] + kBlockW - 1) / kBlockW;
     fc.bandCount = bandCount;
+    fc.refillLanes = refillLanes;
+    fc.parkLanes = parkLanes;
     hipLaunchKernelGGL(set_frame_kernel, dim3(1), dim3(1), 0, stream, dFrame, fc);
     const uint32_t total = fc.blocksX * bandCount;
     const uint32_t idleThreads = std::max<uint32_t>(poolSize, 2u * (uint32_t)(sizeof(Counters) / 4));
