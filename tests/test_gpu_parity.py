@@ -9,7 +9,7 @@ comparison is not bit-exact the tolerance is stated in the assertion.
 import numpy as np
 import pytest
 
-from conftest import cornell
+from conftest import MATERIAL_CASES, configure_lights, cornell
 
 pytestmark = pytest.mark.gpu
 
@@ -194,3 +194,25 @@ def test_missing_scene_fails_loudly(native_lib):
             t.render()
     finally:
         t.destroy()
+
+
+# ---- BSDF / light coverage: every material type and light type, GPU vs oracle ----------
+@pytest.mark.parametrize("case", sorted(MATERIAL_CASES))
+def test_materials_bit_exact(gpu_tracer, golden_luts, oracle_mod, case):
+    s = cornell(48, 40, 5)
+    for args in MATERIAL_CASES[case]:
+        s.set_material(*args)
+    list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 3]))
+
+
+@pytest.mark.parametrize("env", ["constant", "cube", "directional"])
+def test_lights_bit_exact(gpu_tracer, golden_luts, oracle_mod, env):
+    s = cornell(48, 40, 4)
+    configure_lights(s, env)     # the room is open towards the camera: escaping rays see the sky
+    list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [1, 2]))
+
+
+def test_pinhole_and_filters(gpu_tracer, golden_luts, oracle_mod):
+    s = cornell(40, 40, 3)
+    s.set_lens(camera_type=0, fov_x=1.0)
+    list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [4]))
