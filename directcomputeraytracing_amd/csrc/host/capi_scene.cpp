@@ -59,8 +59,10 @@ DCRT_API int dcrt_scene_load_from_file(dcrt_scene* s, const char* path)
 {
     if (!s || !path) return DCRT_E_INVALID_ARG;
     DCRT_GUARD_BEGIN
+    SetLastError("");
     if (!s->scene.LoadFromFile(path)) {
-        SetLastError(std::string("failed to load scene ") + path);
+        const std::string detail = dcrt_last_error();
+        SetLastError(std::string("failed to load scene ") + path + (detail.empty() ? "" : ": " + detail));
         return DCRT_E_IO;
     }
     return DCRT_OK;

@@ -216,3 +216,13 @@ def test_pinhole_and_filters(gpu_tracer, golden_luts, oracle_mod):
     s = cornell(40, 40, 3)
     s.set_lens(camera_type=0, fov_x=1.0)
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [4]))
+
+
+def test_xml_scene_mesh_lights_bit_exact(gpu_tracer, golden_luts, oracle_mod):
+    """Mitsuba XML fixture: area (triangle) light, env + directional, twosided roughplastic,
+    roughconductor, roughdielectric, instanced OBJ, shared rectangle, thin lens."""
+    from conftest import GOLDEN
+    from directcomputeraytracing_amd import Scene
+    s = Scene((32, 32))
+    s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
+    list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 7]))
