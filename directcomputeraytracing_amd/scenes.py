@@ -142,3 +142,226 @@ def env_cube(size: int = 16, seed: int = 1234) -> np.ndarray:
                          indexing="ij")
     grad = (0.5 + 0.5 * np.sin(6.0 * xx + 3.0 * yy))[None, :, :, None]
     return np.ascontiguousarray(base * grad, dtype=np.float32)
+
+
+# ---------------------------------------------------------------------------------------
+# Mitsuba 3 XML scenes for configs 3-5 (coffee-like, spaceship-like, lamp-like). All
+# geometry is procedural with a fixed seed; OBJ meshes are loaded through the XML path
+# (one mesh per file, instanced by repeated <shape type="obj">, SceneXMLLoading.cpp).
+# Coordinates are Mitsuba's (right-handed, y up); the loader converts them.
+
+def mitsuba_matrix(translate=(0.0, 0.0, 0.0), yaw=0.0, pitch=0.0, scale=(1.0, 1.0, 1.0)) -> str:
+    """Row-major 4x4 (column-vector convention) = T * Ry(yaw) * Rx(pitch) * S, degrees."""
+    cy, sy = math.cos(math.radians(yaw)), math.sin(math.radians(yaw))
+    cp, sp = math.cos(math.radians(pitch)), math.sin(math.radians(pitch))
+    ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    rx = np.array([[1, 0, 0], [0, cp, -sp], [0, sp, cp]])
+    m = np.eye(4)
+    m[:3, :3] = ry @ rx @ np.diag(scale)
+    m[:3, 3] = translate
+    # single spaces only: the reference splits the value on ' ' and needs exactly 16 fields
+    return " ".join(f"{v:.6g}" for v in m.reshape(-1))
+
+
+def lathe(profile, segments: int):
+    """Surface of revolution about +y. profile: [(r, y), ...]. Returns V, N, UV, F (0-based)."""
+    prof = np.asarray(profile, np.float64)
+    n = len(prof)
+    # profile tangents -> outward 2D normals (r, y) rotated by -90 degrees
+    t = np.gradient(prof, axis=0)
+    t /= np.maximum(np.linalg.norm(t, axis=1, keepdims=True), 1e-12)
+    n2 = np.stack([t[:, 1], -t[:, 0]], axis=1)
+    phi = np.linspace(0.0, 2 * math.pi, segments, endpoint=False)
+    c, s = np.cos(phi), np.sin(phi)
+    V = np.stack([np.outer(prof[:, 0], c), np.repeat(prof[:, 1:2], segments, 1), np.outer(prof[:, 0], s)], -1).reshape(-1, 3)
+    N = np.stack([np.outer(n2[:, 0], c), np.repeat(n2[:, 1:2], segments, 1), np.outer(n2[:, 0], s)], -1).reshape(-1, 3)
+    N /= np.maximum(np.linalg.norm(N, axis=1, keepdims=True), 1e-12)
+    u = np.tile(np.arange(segments) / segments, n)
+    v = np.repeat(np.linspace(0, 1, n), segments)
+    UV = np.stack([u, v], 1)
+    i = np.arange(n - 1)[:, None] * segments
+    j = np.arange(segments)[None, :]
+    a = (i + j).reshape(-1)
+    b = (i + (j + 1) % segments).reshape(-1)
+    F = np.concatenate([np.stack([a, b, a + segments], 1), np.stack([b, b + segments, a + segments], 1)])
+    # drop triangles collapsed on the axis (r == 0 rings)
+    area = np.linalg.norm(np.cross(V[F[:, 1]] - V[F[:, 0]], V[F[:, 2]] - V[F[:, 0]]), axis=1)
+    return V, N, UV, F[area > 1e-12]
+
+
+def write_obj(path: Path, V, N, UV, F) -> Path:
+    """Vertices/normals/texcoords share indices (f a/a/a ...); 1-based."""
+    path = Path(path)
+    lines = [f"# procedural mesh, {len(F)} triangles"]
+    lines += [f"v {x:.6f} {y:.6f} {z:.6f}" for x, y, z in V]
+    lines += [f"vn {x:.6f} {y:.6f} {z:.6f}" for x, y, z in N]
+    lines += [f"vt {x:.6f} {y:.6f}" for x, y in UV]
+    F1 = np.asarray(F) + 1
+    lines += [f"f {a}/{a}/{a} {b}/{b}/{b} {c}/{c}/{c}" for a, b, c in F1]
+    text = "\n".join(lines) + "\n"
+    if not path.exists() or path.read_text() != text:
+        path.write_text(text)
+    return path
+
+
+def _xml(body: str) -> str:
+    return '<?xml version="1.0" encoding="utf-8"?>\n<scene version="3.0.0">\n' + body + "</scene>\n"
+
+
+def _sensor(kind, width, height, to_world, extra="", rfilter='<rfilter type="gaussian"><float name="stddev" value="0.5"/></rfilter>'):
+    return (f'  <sensor type="{kind}">\n{extra}'
+            f'    <transform name="to_world"><matrix value="{to_world}"/></transform>\n'
+            f'    <film type="hdrfilm"><integer name="width" value="{width}"/><integer name="height" value="{height}"/>\n'
+            f'      {rfilter}</film>\n  </sensor>\n')
+
+
+def write_coffee(directory: Path | str, width: int = 1920, height: int = 1080, segments: int = 96) -> Path:
+    """Config 3: roughconductor / roughplastic / roughdielectric, MIS, constant env (+ cube map
+    set through the API, the HAS_ENV_TEXTURE path), path max_depth 8."""
+    d = Path(directory)
+    d.mkdir(parents=True, exist_ok=True)
+    cup = [(0.0, 0.0), (0.26, 0.0), (0.30, 0.02), (0.32, 0.2), (0.35, 0.45), (0.38, 0.68), (0.385, 0.7),
+           (0.36, 0.7), (0.355, 0.66), (0.33, 0.45), (0.30, 0.2), (0.27, 0.06), (0.0, 0.06)]
+    write_obj(d / "cup.obj", *lathe(_densify(cup, 40), segments))
+    write_obj(d / "coffee.obj", *lathe([(0.34, 0.6), (0.17, 0.6), (0.0, 0.6)], segments))   # normal up
+    saucer = [(0.0, 0.0), (0.45, 0.0), (0.6, 0.06), (0.62, 0.08), (0.6, 0.08), (0.45, 0.03), (0.0, 0.03)]
+    write_obj(d / "saucer.obj", *lathe(_densify(saucer, 30), segments))
+    glass = [(0.0, 0.0), (0.2, 0.0), (0.22, 0.9), (0.2, 0.9), (0.18, 0.05), (0.0, 0.05)]
+    write_obj(d / "glass.obj", *lathe(_densify(glass, 30), segments))
+    body = (
+        '  <integrator type="path"><integer name="max_depth" value="8"/></integrator>\n'
+        + _sensor("perspective", width, height, mitsuba_matrix((0.3, 1.35, -3.2), yaw=-5, pitch=18),
+                  '    <float name="fov" value="38"/>\n')
+        + '  <bsdf type="twosided" id="wood"><bsdf type="roughplastic"><rgb name="diffuse_reflectance" value="0.35, 0.2, 0.1"/>'
+          '<float name="alpha" value="0.2"/><boolean name="nonlinear" value="true"/></bsdf></bsdf>\n'
+          '  <bsdf type="diffuse" id="wall"><rgb name="reflectance" value="0.7, 0.7, 0.65"/></bsdf>\n'
+          '  <bsdf type="roughplastic" id="porcelain"><rgb name="diffuse_reflectance" value="0.9, 0.9, 0.85"/>'
+          '<float name="alpha" value="0.05"/><float name="int_ior" value="1.5"/></bsdf>\n'
+          '  <bsdf type="plastic" id="coffee"><rgb name="diffuse_reflectance" value="0.15, 0.07, 0.03"/>'
+          '<float name="int_ior" value="1.33"/></bsdf>\n'
+          '  <bsdf type="roughconductor" id="gold"><rgb name="eta" value="0.143, 0.374, 1.442"/>'
+          '<rgb name="k" value="3.983, 2.385, 1.603"/><float name="alpha" value="0.05"/></bsdf>\n'
+          '  <bsdf type="roughdielectric" id="glass"><float name="int_ior" value="1.5"/><float name="alpha" value="0.01"/></bsdf>\n'
+        f'  <shape type="rectangle" id="shape_table"><ref id="wood"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 0, 0), pitch=-90, scale=(4, 4, 1))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_backwall"><ref id="wall"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 1.5, 3), yaw=180, scale=(5, 3, 1))}"/></transform></shape>\n'
+        f'  <shape type="obj" id="shape_saucer"><string name="filename" value="saucer.obj"/><ref id="gold"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 0.001, 0))}"/></transform></shape>\n'
+        f'  <shape type="obj" id="shape_cup"><string name="filename" value="cup.obj"/><ref id="porcelain"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 0.031, 0))}"/></transform></shape>\n'
+        f'  <shape type="obj" id="shape_coffee"><string name="filename" value="coffee.obj"/><ref id="coffee"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 0.0, 0))}"/></transform></shape>\n'
+        f'  <shape type="obj" id="shape_glass"><string name="filename" value="glass.obj"/><ref id="glass"/><transform name="to_world"><matrix value="{mitsuba_matrix((0.9, 0.0, 0.4))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_softbox"><emitter type="area"><rgb name="radiance" value="6, 5.6, 5"/></emitter><transform name="to_world"><matrix value="{mitsuba_matrix((-1.2, 2.6, -0.5), pitch=90, scale=(0.6, 0.6, 1))}"/></transform></shape>\n'
+        '  <emitter type="constant"><rgb name="radiance" value="0.6, 0.65, 0.75"/></emitter>\n'
+    )
+    p = d / "coffee.xml"
+    p.write_text(_xml(body))
+    return p
+
+
+def _densify(profile, n):
+    """Resample a polyline profile to about n points (keeps corners)."""
+    pts = np.asarray(profile, np.float64)
+    seg = np.linalg.norm(np.diff(pts, axis=0), axis=1)
+    out = [pts[0]]
+    per = max(1, n // max(1, len(seg)))
+    for k in range(len(seg)):
+        for t in np.linspace(0, 1, per + 1)[1:]:
+            out.append(pts[k] * (1 - t) + pts[k + 1] * t)
+    return [tuple(p) for p in out]
+
+
+def hull_mesh(nu: int, nv: int, seed: int = 1234):
+    """Spaceship-like hull: an elongated ellipsoid with panelled, greebled displacement."""
+    rng = np.random.default_rng(seed)
+    u = np.linspace(0, 2 * math.pi, nu, endpoint=False)
+    v = np.linspace(0.02, math.pi - 0.02, nv)
+    U, Vv = np.meshgrid(u, v)
+    panels = rng.uniform(-1, 1, size=(16, 32))
+    pu = (U / (2 * math.pi) * 32).astype(int) % 32
+    pv = (Vv / math.pi * 16).astype(int).clip(0, 15)
+    disp = 1 + 0.04 * panels[pv, pu] + 0.03 * np.sin(7 * U) * np.sin(5 * Vv)
+    x = 0.55 * np.sin(Vv) * np.cos(U) * disp
+    y = 0.35 * np.sin(Vv) * np.sin(U) * disp
+    z = 2.0 * np.cos(Vv) * (1 + 0.02 * panels[pv, pu])
+    V = np.stack([x, y, z], -1).reshape(-1, 3)
+    # normals from the grid
+    P = V.reshape(nv, nu, 3)
+    du = np.roll(P, -1, axis=1) - np.roll(P, 1, axis=1)
+    dv = np.concatenate([P[1:2] - P[0:1], P[2:] - P[:-2], P[-1:] - P[-2:-1]], axis=0)
+    N = np.cross(dv, du).reshape(-1, 3)
+    N /= np.maximum(np.linalg.norm(N, axis=1, keepdims=True), 1e-12)
+    UV = np.stack([(U / (2 * math.pi)).reshape(-1), (Vv / math.pi).reshape(-1)], 1)
+    i = np.arange(nv - 1)[:, None] * nu
+    j = np.arange(nu)[None, :]
+    a = (i + j).reshape(-1)
+    b = (i + (j + 1) % nu).reshape(-1)
+    F = np.concatenate([np.stack([a, a + nu, b], 1), np.stack([b, a + nu, b + nu], 1)])
+    return V, N, UV, F
+
+
+def write_spaceship(directory: Path | str, width: int = 3840, height: int = 2160, nu: int = 512, nv: int = 256,
+                    ships: int = 8, seed: int = 1234) -> Path:
+    """Config 4: one procedural hull mesh (2*nu*(nv-1) triangles) instanced `ships` times
+    through repeated <shape type="obj"> with the same filename; engine glows are area lights."""
+    d = Path(directory)
+    d.mkdir(parents=True, exist_ok=True)
+    write_obj(d / f"hull_{nu}x{nv}.obj", *hull_mesh(nu, nv, seed))
+    rng = np.random.default_rng(seed)
+    shapes = []
+    for k in range(ships):
+        pos = (float(rng.uniform(-4, 4)), float(rng.uniform(-1.5, 1.5)), float(rng.uniform(2, 14)))
+        yaw = float(rng.uniform(-60, 60))
+        pitch = float(rng.uniform(-15, 15))
+        shapes.append(f'  <shape type="obj" id="shape_ship{k}"><string name="filename" value="hull_{nu}x{nv}.obj"/><ref id="hullmetal"/>'
+                      f'<transform name="to_world"><matrix value="{mitsuba_matrix(pos, yaw=yaw, pitch=pitch)}"/></transform></shape>\n')
+        # engine glow at the stern (local z = -2.02), facing backwards
+        yr = math.radians(yaw)
+        back = (pos[0] - 2.02 * math.sin(yr), pos[1], pos[2] - 2.02 * math.cos(yr))
+        shapes.append(f'  <shape type="rectangle" id="shape_engine{k}"><emitter type="area"><rgb name="radiance" value="4, 6, 12"/></emitter>'
+                      f'<transform name="to_world"><matrix value="{mitsuba_matrix(back, yaw=yaw + 180, scale=(0.15, 0.1, 1))}"/></transform></shape>\n')
+    body = (
+        '  <integrator type="path"><integer name="max_depth" value="8"/></integrator>\n'
+        + _sensor("perspective", width, height, mitsuba_matrix((0, 0.5, -6), pitch=3), '    <float name="fov" value="55"/>\n',
+                  '<rfilter type="box"><float name="radius" value="1"/></rfilter>')
+        + '  <bsdf type="roughconductor" id="hullmetal"><rgb name="eta" value="1.657, 0.880, 0.521"/>'
+          '<rgb name="k" value="9.224, 6.270, 4.837"/><float name="alpha" value="0.09"/></bsdf>\n'
+        + "".join(shapes)
+        + '  <emitter type="constant"><rgb name="radiance" value="0.02, 0.03, 0.06"/></emitter>\n'
+          '  <emitter type="directional"><vector name="direction" value="-0.4, -0.5, 0.75"/><rgb name="irradiance" value="3, 2.9, 2.7"/></emitter>\n'
+    )
+    p = d / f"spaceship_{nu}x{nv}.xml"
+    p.write_text(_xml(body))
+    return p
+
+
+def write_lamp(directory: Path | str, width: int = 3840, height: int = 2160, segments: int = 96) -> Path:
+    """Config 5: thinlens sensor (aperture_radius, focus_distance), rectangle area emitters
+    (triangle lights), a rough dielectric shade."""
+    d = Path(directory)
+    d.mkdir(parents=True, exist_ok=True)
+    base = [(0.0, 0.0), (0.35, 0.0), (0.36, 0.04), (0.08, 0.08), (0.05, 0.3), (0.04, 1.2), (0.06, 1.25), (0.0, 1.25)]
+    write_obj(d / "lamp_base.obj", *lathe(_densify(base, 40), segments))
+    shade = [(0.45, 1.0), (0.22, 1.5)]                     # open truncated cone
+    write_obj(d / "lamp_shade.obj", *lathe(_densify(shade, 24), segments))
+    body = (
+        '  <integrator type="path"><integer name="max_depth" value="8"/></integrator>\n'
+        + _sensor("thinlens", width, height, mitsuba_matrix((0.2, 1.2, -3.0), yaw=-4, pitch=6),
+                  '    <string name="focal_length" value="50mm"/>\n    <float name="aperture_radius" value="0.012"/>\n'
+                  '    <float name="focus_distance" value="3.1"/>\n',
+                  '<rfilter type="tent"><float name="radius" value="1"/></rfilter>')
+        + '  <bsdf type="roughplastic" id="floor"><rgb name="diffuse_reflectance" value="0.45, 0.3, 0.2"/><float name="alpha" value="0.15"/></bsdf>\n'
+          '  <bsdf type="diffuse" id="wall"><rgb name="reflectance" value="0.75, 0.72, 0.7"/></bsdf>\n'
+          '  <bsdf type="roughconductor" id="brass"><rgb name="eta" value="0.444, 0.527, 1.094"/>'
+          '<rgb name="k" value="3.695, 2.765, 1.829"/><float name="alpha" value="0.1"/></bsdf>\n'
+          '  <bsdf type="twosided" id="shade"><bsdf type="roughdielectric"><float name="int_ior" value="1.5"/><float name="alpha" value="0.3"/></bsdf></bsdf>\n'
+          '  <bsdf type="thindielectric" id="pane"><float name="int_ior" value="1.5"/></bsdf>\n'
+        f'  <shape type="rectangle" id="shape_floor"><ref id="floor"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 0, 1), pitch=-90, scale=(5, 5, 1))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_wall"><ref id="wall"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 2, 2.5), yaw=180, scale=(5, 2, 1))}"/></transform></shape>\n'
+        f'  <shape type="obj" id="shape_base"><string name="filename" value="lamp_base.obj"/><ref id="brass"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 0, 1))}"/></transform></shape>\n'
+        f'  <shape type="obj" id="shape_shade"><string name="filename" value="lamp_shade.obj"/><ref id="shade"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 0, 1))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_pane"><ref id="pane"/><transform name="to_world"><matrix value="{mitsuba_matrix((-1.1, 0.6, 0.6), yaw=30, scale=(0.4, 0.6, 1))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_bulb_a"><emitter type="area"><rgb name="radiance" value="40, 34, 26"/></emitter><transform name="to_world"><matrix value="{mitsuba_matrix((0, 1.3, 1), yaw=0, scale=(0.06, 0.1, 1))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_bulb_b"><emitter type="area"><rgb name="radiance" value="40, 34, 26"/></emitter><transform name="to_world"><matrix value="{mitsuba_matrix((0, 1.3, 1), yaw=90, scale=(0.06, 0.1, 1))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_ceiling"><emitter type="area"><rgb name="radiance" value="1.5, 1.6, 1.8"/></emitter><transform name="to_world"><matrix value="{mitsuba_matrix((1.5, 3.2, 1.5), pitch=90, scale=(0.8, 0.8, 1))}"/></transform></shape>\n'
+    )
+    p = d / "lamp.xml"
+    p.write_text(_xml(body))
+    return p

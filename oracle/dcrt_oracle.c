@@ -19,6 +19,7 @@
 #include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 
 /* ------------------------------------------------------------------ */
@@ -1459,9 +1460,22 @@ static void sample_bsdf(v3 wo, f2 sample, float sel, const isect* it, v3* wiOut,
 /* One path, wavefront semantics (WavefrontPathTracing.hlsl:176-607)   */
 /* or megakernel semantics (MegakernelPathTracing.hlsl:110-208).       */
 /* ------------------------------------------------------------------ */
+/* Debug aid: DCRT_ORACLE_TRACE="x,y" prints each bounce of that pixel's path to stderr. */
+static int trace_enabled(uint32_t px, uint32_t py)
+{
+    static int parsed = 0, tx = -1, ty = -1;
+    if (!parsed) {
+        const char* e = getenv("DCRT_ORACLE_TRACE");
+        if (e) sscanf(e, "%d,%d", &tx, &ty);
+        parsed = 1;
+    }
+    return (int)px == tx && (int)py == ty;
+}
+
 static void trace_path(const dcrt_flat_scene* sc, const dcrt_frame_params* f, int mode, uint32_t px, uint32_t py,
                        float outPos[2], float outVal[3], uint32_t outRng[4], oracle_counters* cnt)
 {
+    const int dbg = trace_enabled(px, py);
     uint32_t s[4];
     oracle_rng_init(px, py, f->frame_seed, s);
     /* NEW_PATH :214-237 */
@@ -1527,6 +1541,9 @@ static void trace_path(const dcrt_flat_scene* sc, const dcrt_frame_params* f, in
                     tmp = vscale(tmp, NdotWI);
                     tmp = vscale(tmp, weight);
                     lsr = vdivs(tmp, ls.pdf);
+                    if (dbg)
+                        fprintf(stderr, "  nee wi(%g %g %g) Le(%g %g %g) pdf %g dist %g delta %d f(%g %g %g) bsdfPdf %g w %g\n", ls.wi.x, ls.wi.y, ls.wi.z,
+                                ls.radiance.x, ls.radiance.y, ls.radiance.z, ls.pdf, ls.distance, ls.isDeltaLight, bsdf.x, bsdf.y, bsdf.z, bsdfPdf, weight);
                     sd = ls.wi;
                     so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
                     sdist = ls.distance;
@@ -1539,6 +1556,10 @@ static void trace_path(const dcrt_flat_scene* sc, const dcrt_frame_params* f, in
                 f2 bs = next2d(s);
                 v3 wi, bsdf;
                 sample_bsdf(wo, bs, sel, &it, &wi, &bsdf, &bsdfPdf, &isDeltaB);
+                if (dbg)
+                    fprintf(stderr, "b%u mat%u n(%g %g %g) wo(%g %g %g) sel %g bs(%g %g) -> wi(%g %g %g) f(%g %g %g) pdf %g delta %d T(%g %g %g) lsr(%g %g %g) Li(%g %g %g)\n",
+                            bounce, it.materialType, it.normal.x, it.normal.y, it.normal.z, wo.x, wo.y, wo.z, sel, bs.x, bs.y,
+                            wi.x, wi.y, wi.z, bsdf.x, bsdf.y, bsdf.z, bsdfPdf, isDeltaB, T.x, T.y, T.z, lsr.x, lsr.y, lsr.z, Li.x, Li.y, Li.z);
                 if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
                     float NdotWI = fabsf(vdot(it.normal, wi));
                     T = vdivs(vscale(vmul(T, bsdf), NdotWI), bsdfPdf);

@@ -14,6 +14,14 @@ from conftest import MATERIAL_CASES, configure_lights, cornell
 pytestmark = pytest.mark.gpu
 
 
+def same_bits(a, b):
+    """Bit-identical, except that a NaN matches any NaN: the reference's own arithmetic makes
+    NaN (e.g. the power heuristic's inf/inf at grazing light samples), and the default NaN
+    payload differs between x86 (sign set) and gfx950."""
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    return (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+
+
 def _rays(n, seed, room=True):
     from directcomputeraytracing_amd import make_rays
     rng = np.random.default_rng(seed)
@@ -84,8 +92,8 @@ def _render_and_compare(tracer, oracle_mod, luts, scene, seeds):
         p_ref, v_ref, r_ref, c_ref = oracle_mod.render(flat, luts, fr, oracle_mod.WAVEFRONT, rng=True)
         assert np.array_equal(rng, r_ref), f"seed {seed}: RNG state differs at {np.count_nonzero((rng != r_ref).any(-1))} px"
         assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32)), f"seed {seed}: sample positions"
-        bad = np.count_nonzero((val.view(np.uint32) != v_ref.view(np.uint32)).any(-1))
-        assert bad == 0, f"seed {seed}: {bad} pixels differ; max |d| {np.abs(val - v_ref).max()}"
+        bad = np.count_nonzero(~same_bits(val, v_ref).all(-1))
+        assert bad == 0, f"seed {seed}: {bad} pixels differ; max |d| {np.nanmax(np.abs(val - v_ref))}"
         c = tracer.counters()
         yield c, c_ref
 
@@ -133,7 +141,7 @@ def test_film_accumulation_matches_oracle(native_lib, golden_luts, oracle_mod):
             for seed in range(3):
                 p, v, _, _ = oracle_mod.render(flat, golden_luts, s.frame_params(seed), oracle_mod.WAVEFRONT)
                 oracle_mod.sample_convolution(filt, p, v, ref)
-            assert np.array_equal(film.view(np.uint32), ref.view(np.uint32)), \
+            assert same_bits(film, ref).all(), \
                 f"filter {filt.filter}: max |d| {np.abs(film - ref).max()}"
     finally:
         t.destroy()
@@ -156,7 +164,7 @@ def test_film_partition_sums_to_single_gpu(native_lib, golden_luts):
         finally:
             t.destroy()
     total = films[1] + films[2] + films[3]
-    assert np.array_equal(total.view(np.uint32), films[0].view(np.uint32))
+    assert same_bits(total, films[0]).all()
 
 
 def test_traversal_counters_match_oracle(native_lib, golden_luts, oracle_mod):
@@ -226,3 +234,11 @@ def test_xml_scene_mesh_lights_bit_exact(gpu_tracer, golden_luts, oracle_mod):
     s = Scene((32, 32))
     s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 7]))
+
+
+@pytest.mark.parametrize("name,cube", [("coffee", True), ("spaceship", False), ("lamp", False)])
+def test_config_scenes_bit_exact(gpu_tracer, golden_luts, oracle_mod, name, cube):
+    """configs[2..4] (coffee / spaceship / lamp, procedural XML fixtures) at 160x90, 8 bounces."""
+    from test_oracle import load_fixture_scene
+    s = load_fixture_scene(name, env_cube=cube)
+    list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 1]))

@@ -303,3 +303,42 @@ def test_xml_scene_oracle_renders(oracle_mod, golden_luts):
     assert np.isfinite(a[1]).all() and a[1][..., :3].mean() > 0
     diff = (a[1] != b[1]).any(-1)
     assert diff.mean() < 0.25
+
+
+# ---- configs 3-5 as procedural XML fixtures (tests/golden/scenes, scenes.write_*) ------------
+SCENE_FIXTURES = {"coffee": "coffee.xml", "spaceship": "spaceship_64x32.xml", "lamp": "lamp.xml"}
+
+
+def load_fixture_scene(name, env_cube=False):
+    from directcomputeraytracing_amd import Scene, scenes
+    s = Scene((8, 8))
+    s.load_from_file(GOLDEN / "scenes" / SCENE_FIXTURES[name])
+    if env_cube:
+        s.set_environment_light((1.0, 1.0, 1.0), scenes.env_cube(16))
+    return s
+
+
+def test_scene_fixtures_are_reproducible(tmp_path):
+    """The committed fixtures are exactly what the deterministic generators write."""
+    from directcomputeraytracing_amd import scenes
+    scenes.write_coffee(tmp_path, width=160, height=90, segments=48)
+    scenes.write_spaceship(tmp_path, width=160, height=90, nu=64, nv=32, ships=4)
+    scenes.write_lamp(tmp_path, width=160, height=90, segments=48)
+    for f in (GOLDEN / "scenes").iterdir():
+        assert (tmp_path / f.name).read_text() == f.read_text(), f.name
+
+
+@pytest.mark.parametrize("name", sorted(SCENE_FIXTURES))
+def test_scene_fixture_loads_and_renders(oracle_mod, golden_luts, name):
+    s = load_fixture_scene(name)
+    a = s.arrays()
+    assert s.resolution == (160, 90)
+    fr = s.frame_params(0)
+    assert fr.max_bounce_count == 8
+    expect = {"coffee": (2, 1), "spaceship": (6, 4), "lamp": (3, 3)}[name]      # lights, mesh lights
+    assert a["lights"].shape[0] == expect[0]
+    assert int(np.count_nonzero((a["lights"][:, 6] & 0x7) == 0)) >= 0
+    pos, val, rng, cnt = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rng=True)
+    finite = np.isfinite(val[..., :3])
+    assert finite.mean() > 0.99 and val[..., :3][finite].mean() > 0
+    assert cnt["extension_rays"] >= 160 * 90
