@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Secondary benchmark: Mrays/s, ms/spp and the EXTENSION_RAY_CAST roofline on every
+BASELINE.json config that fits one GPU (configs[1..4]; the multi-GPU film split of
+configs 4/5 is exercised by bench.py --gpus N). Scenes are generated procedurally
+(deterministic) into --scene-dir. Prints one JSON line per config.
+
+  python tools/bench_configs.py [--spp K] [--configs cornell,coffee,spaceship,lamp]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0
+
+
+def setup(name, scene_dir: Path, small: bool):
+    from directcomputeraytracing_amd import Scene, scenes
+    s = Scene((1920, 1080))
+    if name == "cornell":
+        scenes.setup_cornell(s, 1920, 1080, 8)
+        return s, "Cornell box OBJ 1920x1080, 8 bounces (configs[1])"
+    if name == "coffee":
+        p = scenes.write_coffee(scene_dir, 1920, 1080, segments=48 if small else 96)
+        s.load_from_file(p)
+        s.set_environment_light((1.0, 1.0, 1.0), scenes.env_cube(64))
+        return s, "coffee-like XML 1920x1080, env cube + constant, max_depth 8 (configs[2])"
+    if name == "spaceship":
+        nu, nv = (64, 32) if small else (512, 256)
+        p = scenes.write_spaceship(scene_dir, 3840, 2160, nu=nu, nv=nv, ships=8)
+        s.load_from_file(p)
+        return s, f"spaceship-like XML 3840x2160, {2 * nu * (nv - 1)} tris x 8 instances (configs[3], 1 GPU)"
+    if name == "lamp":
+        p = scenes.write_lamp(scene_dir, 3840, 2160, segments=48 if small else 96)
+        s.load_from_file(p)
+        return s, "lamp-like XML 3840x2160, thin lens, triangle emitters (configs[4], 1 GPU)"
+    raise ValueError(name)
+
+
+def run(name, args):
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    t0 = time.perf_counter()
+    scene, desc = setup(name, Path(args.scene_dir), args.small)
+    load_s = time.perf_counter() - t0
+    W, H = scene.resolution
+    pool = 1 << 21 if W * H <= (1 << 21) else 1 << 23
+    tr = WavefrontPathTracer(path_pool_size=pool, iterations_per_render=16)
+    try:
+        tr.on_scene_loaded(scene)
+        filt = scene.filter_params()
+        tr.clear_film()
+        tr.render_images(10_000, args.warmup, filt)
+        tr.reset_stats()
+        tr.synchronize()
+        t0 = time.perf_counter()
+        tr.render_images(0, args.spp, filt)
+        tr.synchronize()
+        el = time.perf_counter() - t0
+        c = tr.counters()
+        rays = c["extension_rays"] + c["shadow_rays"]
+        # roofline leg (same seeds): counts from the instrumented casts, time from HIP events
+        tr.set_instrumentation(True, False)
+        tr.reset_stats()
+        tr.render_images(0, 2, filt)
+        st = tr.traversal_stats()
+        cr = tr.counters()
+        tr.set_instrumentation(False, True)
+        tr.reset_stats()
+        tr.render_images(0, 2, filt)
+        tm = tr.traversal_stats()
+        tr.set_instrumentation(False, False)
+        ext_bytes = (56 * cr["extension_rays"] + 32 * st["ext_node_visits"] + 48 * st["ext_triangle_tests"]
+                     + 56 * st["ext_blas_entries"])
+        achieved = ext_bytes / (tm["ext_kernel_ms"] * 1e-3) / 1e9
+        info = scene.bvh_info()
+        return {"config": name, "workload": desc, "resolution": [W, H], "spp": args.spp,
+                "value": round(rays / el / 1e6, 1), "unit": "Mrays/s", "ms_per_spp": round(el * 1e3 / args.spp, 2),
+                "rays_per_spp": int(rays / args.spp), "triangles_bvh_nodes": info["total_nodes"],
+                "scene_load_s": round(load_s, 2),
+                "roofline": {"kernel": "extension_kernel", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                             "avg_launch_us": round(tm["ext_kernel_ms"] * 1e3 / max(1, tm["ext_launches"]), 1),
+                             "nodes_per_ray": round(st["ext_node_visits"] / max(1, cr["extension_rays"]), 2),
+                             "tris_per_ray": round(st["ext_triangle_tests"] / max(1, cr["extension_rays"]), 2)}}
+    finally:
+        tr.destroy()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--configs", default="cornell,coffee,spaceship,lamp")
+    ap.add_argument("--scene-dir", default="/tmp/dcrt_scenes")
+    ap.add_argument("--small", action="store_true", help="small meshes (CI smoke)")
+    args = ap.parse_args()
+    for name in args.configs.split(","):
+        print(json.dumps(run(name, args)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
