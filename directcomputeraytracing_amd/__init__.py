@@ -9,7 +9,9 @@ from ._abi import (DCRTError, FEATURE_DEFAULT, FEATURE_GGX_SAMPLE_VNDF, FEATURE_
                    FEATURE_NO_FRONT_TO_BACK, FEATURE_WATERTIGHT, FILTER_BOX, FILTER_GAUSSIAN, FILTER_LANCZOS,
                    FILTER_MITCHELL, FILTER_TRIANGLE, FilterParams, FrameParams, LIB_PATH, load_library)
 from .scene import Scene  # noqa: F401
-from .tracer import HIT_DTYPE, RAY_DTYPE, WavefrontPathTracer, device_count, make_rays  # noqa: F401
+from ._abi import PostFxParams  # noqa: F401
+from .tracer import (HIT_DTYPE, RAY_DTYPE, WavefrontPathTracer, device_count, make_rays, save_bmp,  # noqa: F401
+                     srgb_thresholds)
 
 __version__ = "0.1.0"
 

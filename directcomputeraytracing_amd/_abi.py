@@ -104,6 +104,10 @@ class RayHit(C.Structure):
                 ("instance_index", C.c_uint32)]
 
 
+class PostFxParams(C.Structure):
+    _fields_ = [("enabled", C.c_int32), ("auto_exposure", C.c_int32), ("ev100", C.c_float), ("luminance_white", C.c_float)]
+
+
 class TracerConfig(C.Structure):
     _fields_ = [("path_pool_size", C.c_uint32), ("iterations_per_render", C.c_uint32), ("device", C.c_int32),
                 ("stream", C.c_void_p), ("debug_rng", C.c_uint32)]
@@ -181,6 +185,10 @@ SIGNATURES = [
     ("dcrt_tracer_trace_rays", _I, [_P, C.POINTER(Ray), _U, C.POINTER(RayHit), _U]),
     ("dcrt_tracer_occluded", _I, [_P, C.POINTER(Ray), _U, C.POINTER(C.c_uint32), _U]),
     ("dcrt_tracer_trace_rays_device", _I, [_P, _P, _U, _P, _U]),
+    ("dcrt_scene_get_postfx_params", _I, [_P, C.POINTER(PostFxParams)]),
+    ("dcrt_srgb_encode_thresholds", _I, [_FP]),
+    ("dcrt_tracer_resolve_image", _I, [_P, C.POINTER(PostFxParams), C.POINTER(C.c_uint8), _FP]),
+    ("dcrt_write_bmp", _I, [C.c_char_p, _U, _U, C.POINTER(C.c_uint8)]),
     ("dcrt_device_math_eval", _I, [_P, _I, _FP, _U, _FP]),
 ]
 

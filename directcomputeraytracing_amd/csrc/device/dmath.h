@@ -96,6 +96,37 @@ DEV float det_exp(float x)
     y = y * asf((uint32_t)(n2 + 127) << 23);
     return y;
 }
+// Cephes logf restated; the same code in the oracle (post-processing luminance).
+DEV float det_log(float x)
+{
+    if (x != x) return x;
+    if (x < 0.0f) return asf(0x7FC00000u);
+    if (x == 0.0f) return -inf();
+    if (x == inf()) return x;
+    int e = 0;
+    if (x < 1.17549435e-38f) { x = x * 8388608.0f; e = -23; }          // denormal: scale by 2^23
+    const uint32_t bits = asu(x);
+    e += (int)((bits >> 23) & 0xFFu) - 126;
+    float m = asf((bits & 0x007FFFFFu) | 0x3F000000u);                   // [0.5, 1)
+    if (m < 0.707106781186547524f) { e -= 1; m = m + m - 1.0f; } else { m = m - 1.0f; }
+    const float z = m * m;
+    float y = 7.0376836292e-2f * m;
+    y = y - 1.1514610310e-1f; y = y * m;
+    y = y + 1.1676998740e-1f; y = y * m;
+    y = y - 1.2420140846e-1f; y = y * m;
+    y = y + 1.4249322787e-1f; y = y * m;
+    y = y - 1.6668057665e-1f; y = y * m;
+    y = y + 2.0000714765e-1f; y = y * m;
+    y = y - 2.4999993993e-1f; y = y * m;
+    y = y + 3.3333331174e-1f; y = y * m;
+    y = y * z;
+    const float fe = (float)e;
+    y = y + -2.12194440e-4f * fe;
+    y = y + -0.5f * z;
+    float r = m + y;
+    r = r + 0.693359375f * fe;
+    return r;
+}
 DEV float det_atan(float x)
 {
     if (x != x) return x;

@@ -426,6 +426,7 @@ __global__ void math_eval_kernel(int function, const float* x, uint32_t n, float
     case 0: y[i] = det_sin(x[i]); break;
     case 1: y[i] = det_cos(x[i]); break;
     case 2: y[i] = det_exp(x[i]); break;
+    case 4: y[i] = det_log(x[i]); break;
     default: y[i] = det_atan(x[i]); break;
     }
 }
@@ -524,6 +525,88 @@ __global__ void begin_images_kernel(Globals* g, uint32_t count, uint32_t firstSe
     g->seedBase = firstSeed;
     g->stopped = count == 0u ? 1u : 0u;
     g->imageComplete = 0u;
+}
+
+// ---- post-processing: SumLuminance.hlsl + PostProcessings.hlsl ---------------------------
+__device__ __forceinline__ float4 film_load(const float4* film, uint32_t W, uint32_t H, uint32_t x, uint32_t y)
+{
+    return (x < W && y < H) ? film[(size_t)y * W + x] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // OOB Load -> 0
+}
+__device__ __forceinline__ float lum_log(float4 s)            // SumLuminance.hlsl:29-44
+{
+    V3 c = mk(0.0f, 0.0f, 0.0f);
+    if (s.w > 0.0f) c = mk(s.x / s.w, s.y / s.w, s.z / s.w);
+    c = mk(fminf(fmaxf(c.x, 0.0f), 65000.0f), fminf(fmaxf(c.y, 0.0f), 65000.0f), fminf(fmaxf(c.z, 0.0f), 65000.0f));
+    const float lum = c.x * 0.299f + c.y * 0.587f + c.z * 0.114f;
+    return det_log(0.0001f + lum);
+}
+// REDUCE_TO_1D: 8x8 groups, each thread four film texels, LDS tree 64 -> 1 (same order as the shader)
+__global__ __launch_bounds__(64) void luminance_1d_kernel(const float4* film, uint32_t W, uint32_t H, uint32_t bx, uint32_t by, float* out)
+{
+    __shared__ float acc[64];
+    const uint32_t tx = threadIdx.x & 7u, ty = threadIdx.x >> 3;
+    const uint32_t x = blockIdx.x * 8 + tx, y = blockIdx.y * 8 + ty;
+    float v = lum_log(film_load(film, W, H, x, y));
+    v = v + lum_log(film_load(film, W, H, x + 8 * bx, y));
+    v = v + lum_log(film_load(film, W, H, x, y + 8 * by));
+    v = v + lum_log(film_load(film, W, H, x + 8 * bx, y + 8 * by));
+    acc[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t k = 32; k >= 1; k >>= 1) {
+        if (threadIdx.x < k) acc[threadIdx.x] = acc[threadIdx.x] + acc[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.y * bx + blockIdx.x] = acc[0];
+}
+// REDUCE_TO_SINGLE: 128-thread groups, LDS tree 128 -> 1
+__global__ __launch_bounds__(128) void luminance_single_kernel(const float* in, uint32_t count, float* out)
+{
+    __shared__ float acc[128];
+    const uint32_t i = blockIdx.x * 128 + threadIdx.x;
+    acc[threadIdx.x] = i < count ? in[i] : 0.0f;
+    __syncthreads();
+    for (uint32_t k = 64; k >= 1; k >>= 1) {
+        if (threadIdx.x < k) acc[threadIdx.x] = acc[threadIdx.x] + acc[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = acc[0];
+}
+// MainPS: rgb / w -> exposure -> Reinhard -> R8G8B8A8_UNORM_SRGB (encode by host-made thresholds)
+__global__ __launch_bounds__(256) void postfx_kernel(const float4* film, uint32_t W, uint32_t H, int enabled, int autoExposure,
+                                                     float ev100, float maxWhiteSqr, const float* sumLogLum,
+                                                     const float* thresholds, uchar4* out)
+{
+    __shared__ float th[255];
+    for (uint32_t t = threadIdx.x; t < 255; t += blockDim.x) th[t] = thresholds[t];
+    __syncthreads();
+    float exposure = 1.0f;
+    if (enabled) {
+        float e = ev100;
+        if (autoExposure) {
+            const float recip = 1.0f / (float)(W * H);
+            const float avgLum = det_exp(sumLogLum[0] * recip);
+            e = det_log(avgLum * 100.0f / 12.5f) * 1.44269504088896341f;
+        }
+        const float maxLuminance = 1.2f * det_exp(e * 0.693147180559945309f);
+        exposure = 1.0f / maxLuminance;
+    }
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < W * H; p += gridDim.x * blockDim.x) {
+        const float4 f = film[p];
+        float c[3] = { f.x / f.w, f.y / f.w, f.z / f.w };
+        uint32_t code[3];
+        for (int k = 0; k < 3; ++k) {
+            float v = c[k];
+            if (enabled) {
+                v = v * exposure;
+                v = v * (1.0f + v / maxWhiteSqr) / (1.0f + v);
+            }
+            v = v != v ? 0.0f : fminf(fmaxf(v, 0.0f), 1.0f);
+            uint32_t n = 0;
+            for (int t = 0; t < 255; ++t) n += v >= th[t] ? 1u : 0u;
+            code[k] = n;
+        }
+        out[p] = make_uchar4((unsigned char)code[0], (unsigned char)code[1], (unsigned char)code[2], 255);
+    }
 }
 
 // ---- BxDF LUT integration (BxDFTexturesBuilding.hlsl, "%f" defines) -------------------------

@@ -1010,6 +1010,44 @@ DCRT_API int dcrt_tracer_trace_rays_device(dcrt_tracer* t, const void* d_rays, u
     return TraceBatch(t, (const dcrt_ray*)d_rays, n, (dcrt_ray_hit*)d_hits, nullptr, false, features);
 }
 
+DCRT_API int dcrt_tracer_resolve_image(dcrt_tracer* t, const dcrt_postfx_params* prm, uint8_t* out, float* outSumLogLum)
+{
+    TRACER_GUARD(t);
+    if (!prm || !out || !t->film.accum) return DCRT_E_INVALID_ARG;
+    const uint32_t W = t->filmW, H = t->filmH;
+    float hth[255];
+    dcrt_srgb_encode_thresholds(hth);
+    std::vector<void*> tmp;
+    struct Free { std::vector<void*>* v; ~Free() { FreeAll(v); } } guard{ &tmp };
+    float* dth = nullptr;
+    CHECKED(DeviceAlloc(&dth, 255, &tmp));
+    HIPCHECK(hipMemcpyAsync(dth, hth, sizeof(hth), hipMemcpyHostToDevice, t->stream));
+    // SumLuminance: REDUCE_TO_1D then REDUCE_TO_SINGLE until one value (SceneLuminance.cpp:110-190)
+    const uint32_t bx = (((W + 7) / 8) + 1) / 2, by = (((H + 7) / 8) + 1) / 2;
+    float *la = nullptr, *lb = nullptr;
+    CHECKED(DeviceAlloc(&la, (size_t)bx * by + 1, &tmp));
+    CHECKED(DeviceAlloc(&lb, (size_t)bx * by + 1, &tmp));
+    hipLaunchKernelGGL(luminance_1d_kernel, dim3(bx, by), dim3(64), 0, t->stream, (const float4*)t->film.accum, W, H, bx, by, la);
+    uint32_t count = bx * by;
+    while (count != 1) {
+        const uint32_t groups = (count + 127) / 128;
+        hipLaunchKernelGGL(luminance_single_kernel, dim3(groups), dim3(128), 0, t->stream, (const float*)la, count, lb);
+        std::swap(la, lb);
+        count = groups;
+    }
+    uchar4* dout = nullptr;
+    CHECKED(DeviceAlloc(&dout, (size_t)W * H, &tmp));
+    const uint32_t grid = std::max<uint32_t>(1u, std::min<uint32_t>((W * H + 255) / 256, kMaxPersistentBlocks));
+    hipLaunchKernelGGL(postfx_kernel, dim3(grid), dim3(256), 0, t->stream, (const float4*)t->film.accum, W, H, prm->enabled,
+                       prm->auto_exposure, prm->ev100, prm->luminance_white * prm->luminance_white, (const float*)la,
+                       (const float*)dth, dout);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipMemcpyAsync(out, dout, (size_t)W * H * 4, hipMemcpyDeviceToHost, t->stream));
+    if (outSumLogLum) HIPCHECK(hipMemcpyAsync(outSumLogLum, la, sizeof(float), hipMemcpyDeviceToHost, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    return DCRT_OK;
+}
+
 DCRT_API int dcrt_device_math_eval(dcrt_tracer* t, int function, const float* x, uint32_t n, float* y)
 {
     TRACER_GUARD(t);

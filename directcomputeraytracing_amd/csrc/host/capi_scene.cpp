@@ -1,5 +1,8 @@
 // capi_scene.cpp -- extern "C" surface of the host scene (include/dcrt.h).
+#include <cmath>
+#include <cstdio>
 #include <cstring>
+#include <vector>
 #include <exception>
 #include <string>
 
@@ -227,6 +230,62 @@ DCRT_API int dcrt_bvh_build_blas(const dcrt_vertex* vertices, const uint32_t* in
     if (out_max_stack_size) *out_max_stack_size = r.maxStackSize;
     return DCRT_OK;
     DCRT_GUARD_END
+}
+
+}  // extern "C"
+
+extern "C" {
+
+DCRT_API int dcrt_scene_get_postfx_params(const dcrt_scene* s, dcrt_postfx_params* out)
+{
+    if (!s || !out) return DCRT_E_INVALID_ARG;
+    const dcrt::CScene& sc = s->scene;
+    out->enabled = 1;
+    out->auto_exposure = 1;
+    // CalculateEV100 (PostProcessing.cpp:39-42)
+    out->ev100 = std::log2(sc.relativeAperture * sc.relativeAperture / sc.shutterTime * 100 / sc.iso);
+    out->luminance_white = 1.0f;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_srgb_encode_thresholds(float out[255])
+{
+    if (!out) return DCRT_E_INVALID_ARG;
+    for (int k = 0; k < 255; ++k) {
+        const double c = (k + 0.5) / 255.0;
+        const double lin = c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4);
+        out[k] = (float)lin;
+    }
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_write_bmp(const char* path, uint32_t w, uint32_t h, const uint8_t* rgba)
+{
+    if (!path || !rgba || !w || !h) return DCRT_E_INVALID_ARG;
+    const uint32_t stride = (w * 3 + 3) & ~3u;
+    const uint32_t imageSize = stride * h, fileSize = 54 + imageSize;
+    std::vector<uint8_t> buf(fileSize, 0);
+    auto put32 = [&](size_t o, uint32_t v) { for (int i = 0; i < 4; ++i) buf[o + i] = (uint8_t)(v >> (8 * i)); };
+    auto put16 = [&](size_t o, uint16_t v) { buf[o] = (uint8_t)v; buf[o + 1] = (uint8_t)(v >> 8); };
+    buf[0] = 'B'; buf[1] = 'M';
+    put32(2, fileSize); put32(10, 54);
+    put32(14, 40); put32(18, w); put32(22, h); put16(26, 1); put16(28, 24);
+    put32(34, imageSize); put32(38, 2835); put32(42, 2835);
+    for (uint32_t y = 0; y < h; ++y) {
+        const uint8_t* src = rgba + (size_t)(h - 1 - y) * w * 4;    // bottom-up rows
+        uint8_t* dst = buf.data() + 54 + (size_t)y * stride;
+        for (uint32_t x = 0; x < w; ++x) {
+            dst[x * 3 + 0] = src[x * 4 + 2];
+            dst[x * 3 + 1] = src[x * 4 + 1];
+            dst[x * 3 + 2] = src[x * 4 + 0];
+        }
+    }
+    FILE* f = std::fopen(path, "wb");
+    if (!f) { SetLastError(std::string("cannot write ") + path); return DCRT_E_IO; }
+    const bool ok = std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+    std::fclose(f);
+    if (!ok) { SetLastError(std::string("short write ") + path); return DCRT_E_IO; }
+    return DCRT_OK;
 }
 
 }  // extern "C"

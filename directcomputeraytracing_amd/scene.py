@@ -116,6 +116,12 @@ class Scene:
         check(self._lib.dcrt_scene_get_flat(self._h, C.byref(f)), "GetFlat")
         return f
 
+    def postfx_params(self) -> _abi.PostFxParams:
+        """Scene.h:181-185 defaults, EV100 from the camera (PostProcessing.cpp:39-42)."""
+        p = _abi.PostFxParams()
+        check(self._lib.dcrt_scene_get_postfx_params(self._h, C.byref(p)), "GetPostFxParams")
+        return p
+
     def frame_params(self, frame_seed: int = 0) -> _abi.FrameParams:
         p = _abi.FrameParams()
         check(self._lib.dcrt_scene_get_frame_params(self._h, int(frame_seed), C.byref(p)), "GetFrameParams")

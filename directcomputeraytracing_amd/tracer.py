@@ -129,6 +129,15 @@ class WavefrontPathTracer:
     def copy_film_device(self, d_dst: int) -> None:
         check(self._lib.dcrt_tracer_copy_film_device(self._h, C.c_void_p(d_dst)), "CopyFilmDevice")
 
+    def resolve_image(self, params: _abi.PostFxParams | None = None, with_luminance: bool = False):
+        """Post-processing (exposure + Reinhard) into sRGB8 RGBA, H x W x 4 uint8."""
+        p = params or _abi.PostFxParams(1, 1, 15.0, 1.0)
+        out = np.empty((self.height, self.width, 4), np.uint8)
+        lum = C.c_float()
+        check(self._lib.dcrt_tracer_resolve_image(self._h, C.byref(p), out.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                  C.byref(lum)), "ResolveImage")
+        return (out, lum.value) if with_luminance else out
+
     # ---- statistics ----------------------------------------------------------
     def counters(self) -> dict:
         s = _abi.RayStats()
@@ -182,6 +191,19 @@ class WavefrontPathTracer:
         check(self._lib.dcrt_device_math_eval(self._h, int(function), x.ctypes.data_as(_abi._FP), x.size,
                                               y.ctypes.data_as(_abi._FP)), "MathEval")
         return y
+
+
+def srgb_thresholds() -> np.ndarray:
+    out = np.empty(255, np.float32)
+    check(_abi.load_library().dcrt_srgb_encode_thresholds(out.ctypes.data_as(_abi._FP)), "SrgbThresholds")
+    return out
+
+
+def save_bmp(path, rgba8: np.ndarray) -> None:
+    """24-bit BMP (SaveImageToFile.cpp:92-182)."""
+    a = np.ascontiguousarray(rgba8, np.uint8)
+    h, w = a.shape[:2]
+    check(_abi.load_library().dcrt_write_bmp(str(path).encode(), w, h, a.ctypes.data_as(C.POINTER(C.c_uint8))), "WriteBmp")
 
 
 def device_count() -> int:

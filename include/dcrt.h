@@ -356,6 +356,24 @@ DCRT_API int dcrt_tracer_occluded(dcrt_tracer* tracer, const dcrt_ray* rays, uin
 DCRT_API int dcrt_tracer_trace_rays_device(dcrt_tracer* tracer, const void* d_rays, uint32_t count, void* d_hits,
                                            uint32_t features);
 
+/* ===== post-processing + image output (PostProcessing.cpp, PostProcessings.hlsl,
+ *       SumLuminance.hlsl, SaveImageToFile.cpp) ============================== */
+typedef struct dcrt_postfx_params {
+    int32_t enabled;          /* m_IsPostFXEnabled (default 1); 0 = rgb / w only          */
+    int32_t auto_exposure;    /* m_IsAutoExposureEnabled (default 1): log-average luminance */
+    float ev100;              /* manual EV100: CalculateEV100(N, t, ISO) or m_ManualEV100  */
+    float luminance_white;    /* m_LuminanceWhite (default 1), Reinhard max white          */
+} dcrt_postfx_params;
+/* Defaults of Scene.h:181-185 with EV100 from the scene's camera (PostProcessing.cpp:39-42). */
+DCRT_API int dcrt_scene_get_postfx_params(const dcrt_scene* scene, dcrt_postfx_params* out_params);
+/* The 255 linear thresholds between consecutive sRGB8 codes (R8G8B8A8_UNORM_SRGB encode). */
+DCRT_API int dcrt_srgb_encode_thresholds(float out_thresholds[255]);
+/* Tone-map the film into sRGB8 RGBA (W*H*4 bytes); optional sum of log luminance (auto exposure). */
+DCRT_API int dcrt_tracer_resolve_image(dcrt_tracer* tracer, const dcrt_postfx_params* params, uint8_t* out_rgba8,
+                                       float* out_sum_log_luminance);
+/* 24-bit BMP writer ("Save Image to File", SaveImageToFile.cpp:92-182). */
+DCRT_API int dcrt_write_bmp(const char* path, uint32_t width, uint32_t height, const uint8_t* rgba8);
+
 /* Deterministic transcendental helpers shared by kernels (parity tests). */
 DCRT_API int dcrt_device_math_eval(dcrt_tracer* tracer, int function, const float* x, uint32_t count, float* out_y);
 

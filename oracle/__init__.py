@@ -73,6 +73,11 @@ def load():
     lib.oracle_offset_ray_origin.argtypes = [P(C.c_float)] * 4
     lib.oracle_generate_camera_ray.restype = None
     lib.oracle_generate_camera_ray.argtypes = [P(A.FrameParams), U, U, P(C.c_float), P(C.c_float), P(U)]
+    lib.oracle_sum_log_luminance.restype = C.c_float
+    lib.oracle_sum_log_luminance.argtypes = [P(C.c_float), U, U]
+    lib.oracle_resolve_image.restype = None
+    lib.oracle_resolve_image.argtypes = [P(C.c_float), U, U, C.c_int, C.c_int, C.c_float, C.c_float, P(C.c_float),
+                                         P(C.c_uint8)]
     lib.oracle_math_eval.restype = None
     lib.oracle_math_eval.argtypes = [C.c_int, P(C.c_float), U, P(C.c_float)]
     _lib = lib
@@ -195,3 +200,19 @@ def camera_ray(frame, px, py):
     r = np.zeros(4, np.uint32)
     load().oracle_generate_camera_ray(C.byref(frame), px, py, _fp(o), _fp(d), _up(r))
     return o, d, r
+
+
+def resolve_image(film, params, thresholds):
+    """PostProcessings.hlsl + SumLuminance.hlsl restated: H x W x 4 sRGB8."""
+    film = np.ascontiguousarray(film, np.float32)
+    H, W = film.shape[:2]
+    out = np.empty((H, W, 4), np.uint8)
+    th = np.ascontiguousarray(thresholds, np.float32)
+    load().oracle_resolve_image(_fp(film), W, H, params.enabled, params.auto_exposure, params.ev100,
+                                params.luminance_white, _fp(th), out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out
+
+
+def sum_log_luminance(film):
+    film = np.ascontiguousarray(film, np.float32)
+    return load().oracle_sum_log_luminance(_fp(film), film.shape[1], film.shape[0])

@@ -118,6 +118,37 @@ static float det_expf(float x)
     y = y * asfloat((uint32_t)(n2 + 127) << 23);
     return y;
 }
+/* Cephes logf restated (same code as det_log in csrc/device/dmath.h) */
+static float det_logf(float x)
+{
+    if (x != x) return x;
+    if (x < 0.0f) return asfloat(0x7FC00000u);
+    if (x == 0.0f) return -o_inf();
+    if (x == o_inf()) return x;
+    int e = 0;
+    if (x < 1.17549435e-38f) { x = x * 8388608.0f; e = -23; }
+    const uint32_t bits = asuint(x);
+    e += (int)((bits >> 23) & 0xFFu) - 126;
+    float m = asfloat((bits & 0x007FFFFFu) | 0x3F000000u);
+    if (m < 0.707106781186547524f) { e -= 1; m = m + m - 1.0f; } else { m = m - 1.0f; }
+    const float z = m * m;
+    float y = 7.0376836292e-2f * m;
+    y = y - 1.1514610310e-1f; y = y * m;
+    y = y + 1.1676998740e-1f; y = y * m;
+    y = y - 1.2420140846e-1f; y = y * m;
+    y = y + 1.4249322787e-1f; y = y * m;
+    y = y - 1.6668057665e-1f; y = y * m;
+    y = y + 2.0000714765e-1f; y = y * m;
+    y = y - 2.4999993993e-1f; y = y * m;
+    y = y + 3.3333331174e-1f; y = y * m;
+    y = y * z;
+    const float fe = (float)e;
+    y = y + -2.12194440e-4f * fe;
+    y = y + -0.5f * z;
+    float r = m + y;
+    r = r + 0.693359375f * fe;
+    return r;
+}
 static float det_atanf(float x)
 {
     if (x != x) return x;
@@ -145,6 +176,7 @@ void oracle_math_eval(int function, const float* x, uint32_t count, float* y)
         case 0: y[i] = det_sinf(x[i]); break;
         case 1: y[i] = det_cosf(x[i]); break;
         case 2: y[i] = det_expf(x[i]); break;
+        case 4: y[i] = det_logf(x[i]); break;
         default: y[i] = det_atanf(x[i]); break;
         }
     }
@@ -1923,4 +1955,93 @@ int oracle_build_luts(dcrt_bxdf_luts* L, int num_threads)
     oracle_lut_finalize(brdf, brdfd, bsdf, L);
     free(brdf); free(brdfd); free(bsdf);
     return DCRT_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* Post-processing: SumLuminance.hlsl (two-stage log-luminance tree    */
+/* reduction), PostProcessings.hlsl (exposure + Reinhard), and the     */
+/* R8G8B8A8_UNORM_SRGB render-target encode (host-made thresholds).     */
+/* ------------------------------------------------------------------ */
+typedef struct float4_t { float x, y, z, w; } float4_t;
+static float4_t film_load(const float* film, uint32_t W, uint32_t H, uint32_t x, uint32_t y)
+{
+    float4_t r = { 0.0f, 0.0f, 0.0f, 0.0f };          /* out-of-range Load returns 0 */
+    if (x < W && y < H) { const float* p = film + ((size_t)y * W + x) * 4; r.x = p[0]; r.y = p[1]; r.z = p[2]; r.w = p[3]; }
+    return r;
+}
+static float lum_log(float4_t s)                       /* SumLuminance.hlsl:29-44 */
+{
+    v3 c = V3(0.0f, 0.0f, 0.0f);
+    if (s.w > 0.0f) c = V3(s.x / s.w, s.y / s.w, s.z / s.w);
+    c.x = fminf(fmaxf(c.x, 0.0f), 65000.0f); c.y = fminf(fmaxf(c.y, 0.0f), 65000.0f); c.z = fminf(fmaxf(c.z, 0.0f), 65000.0f);
+    const float lum = c.x * 0.299f + c.y * 0.587f + c.z * 0.114f;
+    return det_logf(0.0001f + lum);
+}
+float oracle_sum_log_luminance(const float* film, uint32_t W, uint32_t H)
+{
+    const uint32_t bx = (((W + 7) / 8) + 1) / 2, by = (((H + 7) / 8) + 1) / 2;
+    uint32_t count = bx * by;
+    float* a = (float*)malloc(sizeof(float) * (count + 128));
+    float* b = (float*)malloc(sizeof(float) * (count + 128));
+    float acc[128];
+    for (uint32_t gy = 0; gy < by; ++gy)
+        for (uint32_t gx = 0; gx < bx; ++gx) {
+            for (uint32_t t = 0; t < 64; ++t) {
+                const uint32_t x = gx * 8 + (t % 8), y = gy * 8 + (t / 8);
+                float v = lum_log(film_load(film, W, H, x, y));
+                v = v + lum_log(film_load(film, W, H, x + 8 * bx, y));
+                v = v + lum_log(film_load(film, W, H, x, y + 8 * by));
+                v = v + lum_log(film_load(film, W, H, x + 8 * bx, y + 8 * by));
+                acc[t] = v;
+            }
+            for (uint32_t k = 32; k >= 1; k >>= 1)
+                for (uint32_t t = 0; t < k; ++t) acc[t] = acc[t] + acc[t + k];
+            a[gy * bx + gx] = acc[0];
+        }
+    while (count != 1) {
+        const uint32_t groups = (count + 127) / 128;
+        for (uint32_t g = 0; g < groups; ++g) {
+            for (uint32_t t = 0; t < 128; ++t) acc[t] = g * 128 + t < count ? a[g * 128 + t] : 0.0f;
+            for (uint32_t k = 64; k >= 1; k >>= 1)
+                for (uint32_t t = 0; t < k; ++t) acc[t] = acc[t] + acc[t + k];
+            b[g] = acc[0];
+        }
+        float* tmp = a; a = b; b = tmp;
+        count = groups;
+    }
+    const float r = a[0];
+    free(a); free(b);
+    return r;
+}
+void oracle_resolve_image(const float* film, uint32_t W, uint32_t H, int enabled, int autoExposure, float ev100,
+                          float luminanceWhite, const float* srgbThresholds, uint8_t* out)
+{
+    float exposure = 1.0f;
+    if (enabled) {
+        float e = ev100;
+        if (autoExposure) {
+            const float recip = 1.0f / (float)(W * H);
+            const float avgLum = det_expf(oracle_sum_log_luminance(film, W, H) * recip);
+            e = det_logf(avgLum * 100.0f / 12.5f) * 1.44269504088896341f;   /* log2 */
+        }
+        const float maxLuminance = 1.2f * det_expf(e * 0.693147180559945309f);  /* pow(2, EV100) */
+        exposure = 1.0f / maxLuminance;
+    }
+    const float maxWhiteSqr = luminanceWhite * luminanceWhite;
+    for (uint32_t p = 0; p < W * H; ++p) {
+        const float* f = film + (size_t)p * 4;
+        float c[3] = { f[0] / f[3], f[1] / f[3], f[2] / f[3] };
+        for (int k = 0; k < 3; ++k) {
+            float v = c[k];
+            if (enabled) {
+                v = v * exposure;
+                v = v * (1.0f + v / maxWhiteSqr) / (1.0f + v);
+            }
+            v = v != v ? 0.0f : fminf(fmaxf(v, 0.0f), 1.0f);
+            uint32_t code = 0;
+            for (int t = 0; t < 255; ++t) code += v >= srgbThresholds[t] ? 1u : 0u;
+            out[(size_t)p * 4 + k] = (uint8_t)code;
+        }
+        out[(size_t)p * 4 + 3] = 255;
+    }
 }

@@ -71,8 +71,13 @@ void oracle_xoshiro_jump(uint32_t state[4]);
 void oracle_offset_ray_origin(const float p[3], const float n[3], const float d[3], float out[3]);
 void oracle_generate_camera_ray(const dcrt_frame_params* frame, uint32_t px, uint32_t py, float origin[3],
                                 float direction[3], uint32_t rng_out[4]);
-/* function: 0 sin, 1 cos, 2 exp, 3 atan */
+/* function: 0 sin, 1 cos, 2 exp, 3 atan, 4 log */
 void oracle_math_eval(int function, const float* x, uint32_t count, float* y);
+
+/* Post-processing (PostProcessings.hlsl, SumLuminance.hlsl): tone-mapped sRGB8 RGBA. */
+float oracle_sum_log_luminance(const float* film_rgba, uint32_t width, uint32_t height);
+void oracle_resolve_image(const float* film_rgba, uint32_t width, uint32_t height, int enabled, int auto_exposure, float ev100,
+                          float luminance_white, const float* srgb_thresholds, uint8_t* out_rgba8);
 
 #ifdef __cplusplus
 }

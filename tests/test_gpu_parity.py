@@ -45,10 +45,10 @@ def test_device_math_matches_oracle(gpu_tracer, oracle_mod):
     xs = [rng.uniform(-7, 7, 100000), rng.uniform(-100, 100, 20000), rng.uniform(-20, 20, 20000),
           rng.standard_normal(20000) * 1e-3, np.array([0.0, -0.0, 1.0, -1.0, 3.14159265, 1e-30, 88.0, -88.0])]
     x = np.concatenate(xs).astype(np.float32)
-    for fn in range(4):
+    for fn in range(5):
         y_gpu = gpu_tracer.math_eval(fn, x)
         y_cpu = oracle_mod.math_eval(fn, x)
-        assert np.array_equal(y_gpu.view(np.uint32), y_cpu.view(np.uint32)), f"function {fn}"
+        assert same_bits(y_gpu, y_cpu).all(), f"function {fn}"
 
 
 def test_bxdf_luts_match_golden(gpu_tracer, golden_luts, oracle_mod):
@@ -242,3 +242,25 @@ def test_config_scenes_bit_exact(gpu_tracer, golden_luts, oracle_mod, name, cube
     from test_oracle import load_fixture_scene
     s = load_fixture_scene(name, env_cube=cube)
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 1]))
+
+
+def test_postfx_resolve_bit_exact(native_lib, golden_luts, oracle_mod):
+    """Exposure (manual / auto via the two-stage log-luminance reduction) + Reinhard + sRGB8."""
+    from directcomputeraytracing_amd import PostFxParams, WavefrontPathTracer, srgb_thresholds
+    t = WavefrontPathTracer(path_pool_size=1 << 16)
+    try:
+        s = cornell(100, 70, 3)
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        t.clear_film()
+        t.render_images(0, 2)
+        film = t.read_film()
+        th = srgb_thresholds()
+        for prm in (PostFxParams(1, 1, 0.0, 1.0), PostFxParams(1, 0, s.postfx_params().ev100, 2.0),
+                    PostFxParams(0, 0, 0.0, 1.0)):
+            img, lum = t.resolve_image(prm, with_luminance=True)
+            ref = oracle_mod.resolve_image(film, prm, th)
+            assert np.array_equal(img, ref)
+        assert same_bits(np.float32(lum), np.float32(oracle_mod.sum_log_luminance(film)))
+    finally:
+        t.destroy()

@@ -342,3 +342,64 @@ def test_scene_fixture_loads_and_renders(oracle_mod, golden_luts, name):
     finite = np.isfinite(val[..., :3])
     assert finite.mean() > 0.99 and val[..., :3][finite].mean() > 0
     assert cnt["extension_rays"] >= 160 * 90
+
+
+# ---- post-processing + image output (PostProcessings.hlsl, SumLuminance.hlsl) -----------------
+def _film(oracle_mod, golden_luts, w=48, h=40):
+    from directcomputeraytracing_amd import FILTER_BOX, FilterParams
+    s = cornell(w, h, 3)
+    film = np.zeros((h, w, 4), np.float32)
+    for seed in range(2):
+        p, v, _, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(seed), oracle_mod.WAVEFRONT)
+        oracle_mod.sample_convolution(FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3), p, v, film)
+    return s, film
+
+
+def _srgb_encode(x):
+    x = np.clip(np.nan_to_num(x, nan=0.0), 0.0, 1.0)
+    return np.where(x <= 0.0031308, 12.92 * x, 1.055 * np.power(x, 1 / 2.4) - 0.055)
+
+
+def test_postfx_matches_float64_model(oracle_mod, golden_luts):
+    from directcomputeraytracing_amd import PostFxParams, srgb_thresholds
+    s, film = _film(oracle_mod, golden_luts)
+    th = srgb_thresholds()
+    assert np.all(np.diff(th) > 0) and th[0] > 0 and th[-1] < 1
+    rgb = film[..., :3].astype(np.float64) / film[..., 3:4]
+    # manual exposure, EV100 from the camera (f/8, 1 s, ISO 100 -> log2(64 * 100 / 100) = 6)
+    prm = s.postfx_params()
+    assert abs(prm.ev100 - 6.0) < 1e-6 and prm.enabled == 1 and prm.auto_exposure == 1
+    manual = PostFxParams(1, 0, prm.ev100, 1.0)
+    out = oracle_mod.resolve_image(film, manual, th)
+    c = rgb / (1.2 * 2.0 ** prm.ev100)
+    c = c * (1 + c / 1.0) / (1 + c)
+    ref = np.rint(_srgb_encode(c) * 255)
+    assert np.abs(out[..., :3].astype(int) - ref).max() <= 1 and np.all(out[..., 3] == 255)
+    # auto exposure: log-average luminance over the padded reduction domain
+    H, W = film.shape[:2]
+    bx, by = ((W + 7) // 8 + 1) // 2, ((H + 7) // 8 + 1) // 2
+    lum = np.zeros((16 * by, 16 * bx))
+    l = np.clip(rgb, 0, 65000) @ np.array([0.299, 0.587, 0.114])
+    lum[:H, :W] = l
+    total = np.log(1e-4 + lum).sum()
+    got = oracle_mod.sum_log_luminance(film)
+    assert abs(got - total) <= 1e-4 * abs(total)
+    out_auto = oracle_mod.resolve_image(film, PostFxParams(1, 1, 0.0, 1.0), th)
+    ev = np.log2(np.exp(total / (W * H)) * 100 / 12.5)
+    c = rgb / (1.2 * 2.0 ** ev)
+    c = c * (1 + c) / (1 + c)
+    assert np.abs(out_auto[..., :3].astype(int) - np.rint(_srgb_encode(c) * 255)).max() <= 1
+    # post-FX disabled: rgb / w straight to sRGB
+    out_off = oracle_mod.resolve_image(film, PostFxParams(0, 0, 0.0, 1.0), th)
+    assert np.abs(out_off[..., :3].astype(int) - np.rint(_srgb_encode(rgb) * 255)).max() <= 1
+
+
+def test_bmp_writer_roundtrip(tmp_path):
+    from PIL import Image
+    from directcomputeraytracing_amd import save_bmp
+    rng = np.random.default_rng(0)
+    img = rng.integers(0, 256, size=(7, 13, 4), dtype=np.uint8)
+    img[..., 3] = 255
+    save_bmp(tmp_path / "x.bmp", img)
+    back = np.asarray(Image.open(tmp_path / "x.bmp").convert("RGB"))
+    assert np.array_equal(back, img[..., :3])
