@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
     ap.add_argument("--roofline-images", type=int, default=4)
+    ap.add_argument("--mode", choices=["wavefront", "megakernel"], default="wavefront",
+                    help="A/B: the reference's two tracers (the contract line is the wavefront)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
@@ -104,6 +106,7 @@ def main():
     scenes.setup_cornell(scene, args.width, args.height, args.bounces)
     tracer = WavefrontPathTracer(path_pool_size=args.pool, iterations_per_render=args.iterations, device=local_rank)
     tracer.on_scene_loaded(scene)
+    tracer.set_mode(args.mode)
     if world > 1:
         tracer.set_film_partition(world, rank, args.stripe)
     filt = scene.filter_params()

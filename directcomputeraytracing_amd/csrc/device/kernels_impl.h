@@ -390,6 +390,153 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
     }
 }
 
+// ---- GPU megakernel (MegakernelPathTracing.hlsl:65-208) -------------------------------------
+// One lane traces one pixel's whole path; a fully finished wave claims the next 8x8
+// pixel block (same per-shard cursors as CONTROL). Shares every device function with
+// the wavefront kernels; differs from them only in the bounce-0 triangle-light
+// emission, exactly like the reference's two tracers.
+template <bool ANY_HIT>
+__device__ __forceinline__ bool trace_full(const DeviceScene& sc, V3 o, V3 d, float tMax, bool watertight, bool f2b,
+                                           uint32_t* lds, uint32_t stride, HitRecord* hit)
+{
+    TravState s;
+    trav_init(s, o, d, 0.0f, tMax);
+    TraversalStats st = {0u, 0u, 0u};
+    for (;;) {
+        if (trav_visit<false>(sc, s, f2b, lds, stride, st)) break;
+        if (s.parked && trav_leaf<ANY_HIT, false>(sc, s, watertight, lds, stride, st)) break;
+    }
+    *hit = s.hit;
+    return s.found;
+}
+
+__global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameConstants* fcp, Film film, Globals* g, uint32_t debugRng)
+{
+    extern __shared__ uint32_t stackMem[];
+    __shared__ uint32_t sm[64];
+    const FrameConstants& fc = *fcp;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t shard = blockIdx.x % kShards;
+    uint32_t* cursor = &g->nextBlock[shard * kShardStride];
+    const uint32_t shardBlocks = g->totalBlocks > shard ? (g->totalBlocks - shard + kShards - 1) / kShards : 0u;
+    const bool watertight = (fc.features & DCRT_FEATURE_WATERTIGHT) != 0;
+    const bool f2b = (fc.features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
+    const bool vndf = (fc.features & DCRT_FEATURE_GGX_SAMPLE_VNDF) != 0;
+    const bool lightVisible = (fc.features & DCRT_FEATURE_LIGHT_VISIBLE) != 0;
+    uint32_t* lds = stackMem + threadIdx.x;
+    const uint32_t stride = blockDim.x;
+    unsigned long long extRays = 0, shadowRays = 0;
+    for (;;) {
+        // every wave of the block claims one block per round (one atomic per workgroup)
+        bool want = false;
+        if (lane == 0) want = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shardBlocks;
+        const uint32_t bslot = block_append(want, cursor, sm);
+        const uint32_t claimed = (uint32_t)__shfl((int)bslot, 0, 64);
+        const bool got = __shfl((int)want, 0, 64) != 0 && claimed < shardBlocks;
+        if (__syncthreads_or(got ? 1 : 0) == 0) break;
+        if (!got) continue;
+        const uint32_t block = shard + claimed * kShards;
+        const uint32_t band = block / fc.blocksX, bx = block % fc.blocksX;
+        const uint32_t px = bx * kBlockW + (lane % kBlockW);
+        const uint32_t py = film.bandY[band] + lane / kBlockW;
+        if (px >= fc.resolution[0] || py >= fc.resolution[1]) continue;
+        Rng rng = rng_init(px, py, fc.frameSeed);
+        const float psx = next1(rng), psy = next1(rng);
+        const float fsx = (psx + (float)px) / (float)fc.resolution[0];
+        const float fsy = (psy + (float)py) / (float)fc.resolution[1];
+        const float a0 = next1(rng), a1 = next1(rng), a2 = next1(rng);
+        V3 ro, rd;
+        generate_ray(fc, fsx, fsy, a0, a1, a2, &ro, &rd);
+        V3 T = mk(1.0f, 1.0f, 1.0f), L = mk(0.0f, 0.0f, 0.0f);
+        float bsdfPdfPrev = 0.0f;
+        bool isDeltaPrev = true;
+        uint32_t bounce = 0;
+        for (;;) {
+            HitRecord hit;
+            ++extRays;
+            const bool hasHit = trace_full<false>(sc, ro, rd, inf(), watertight, f2b, lds, stride, &hit);
+            const float hitT = hasHit ? hit.t : inf();
+            Intersection it;
+            it.lightIndex = DCRT_LIGHT_INDEX_INVALID; it.triangleIndex = 0;
+            it.geometryNormal = mk(0.0f, 0.0f, 0.0f);
+            if (hasHit) hit_to_intersection(sc, hit, it);
+            {
+                const uint32_t lightIndex = hasHit ? it.lightIndex : fc.envLightIndex;
+                const bool doEval = lightVisible ? lightIndex != DCRT_LIGHT_INDEX_INVALID : (bounce > 0 && lightIndex != DCRT_LIGHT_INDEX_INVALID);
+                if (doEval) {
+                    if (bounce == 0) {
+                        // MegakernelPathTracing.hlsl:135-140, 200-205
+                        const dcrt_light& Lt = sc.lights[lightIndex];
+                        const V3 rad = mk(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
+                        if (hasHit) L = dot(-rd, it.geometryNormal) > 0.0f ? rad : mk(0.0f, 0.0f, 0.0f);
+                        else L = sc.envCube ? sample_env(sc, rd) * rad : rad;
+                    } else {
+                        V3 radiance; float lightPdf;
+                        evaluate_light(sc, lightIndex, it.triangleIndex, it.geometryNormal, rd, hitT, fc.lightCount, &radiance, &lightPdf);
+                        if (lightPdf > 0.0f) {
+                            const float weight = !isDeltaPrev ? power_heuristic(bsdfPdfPrev, lightPdf) : 1.0f;
+                            L = L + T * radiance * weight;
+                        }
+                    }
+                }
+            }
+            if (bounce > fc.maxBounce || !hasHit) break;
+            const V3 wo = -rd;
+            V3 lsr = mk(0.0f, 0.0f, 0.0f);
+            bool hasShadow = false;
+            V3 so = mk(0.0f, 0.0f, 0.0f), sd = so;
+            float sdist = 0.0f;
+            if (fc.lightCount != 0) {
+                const LightSample ls = sample_light(sc, it.position, fc.lightCount, rng);
+                if (any_pos(ls.radiance) && ls.pdf > 0.0f) {
+                    const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, wo, it);
+                    const float NdotWI = fabsf(dot(it.normal, ls.wi));
+                    const float bsdfPdf = evaluate_bsdf_pdf(sc, vndf, ls.wi, wo, it);
+                    const float weight = ls.isDelta ? 1.0f : power_heuristic(ls.pdf, bsdfPdf);
+                    lsr = T * ls.radiance * bsdf * NdotWI * weight / ls.pdf;
+                    so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
+                    sd = ls.wi;
+                    sdist = ls.distance;
+                    hasShadow = true;
+                }
+            }
+            bool terminate = false;
+            {
+                const float sel = next1(rng);
+                const float sx = next1(rng), sy = next1(rng);
+                V3 wi, bsdf;
+                float bsdfPdf = 0.0f;
+                bool isDelta = false;
+                sample_bsdf(sc, vndf, wo, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
+                if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
+                    const float NdotWI = fabsf(dot(it.normal, wi));
+                    T = T * bsdf * NdotWI / bsdfPdf;
+                    ro = offset_ray_origin(it.position, it.geometryNormal, wi);
+                    rd = wi;
+                    ++bounce;
+                } else {
+                    terminate = true;
+                }
+                bsdfPdfPrev = bsdfPdf;
+                isDeltaPrev = isDelta;
+            }
+            if (hasShadow) {
+                ++shadowRays;
+                HitRecord sh;
+                const bool occluded = trace_full<true>(sc, so, sd, sdist, watertight, f2b, lds, stride, &sh);
+                if (!occluded) L = L + lsr;
+            }
+            if (terminate) break;
+        }
+        const size_t p = (size_t)py * film.width + px;
+        film.samplePosition[p] = make_float2(psx, psy);
+        film.sampleValue[p] = make_float4(L.x, L.y, L.z, 0.0f);
+        if (debugRng) film.debugRng[p] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+    }
+    const unsigned long long e = wave_sum((uint32_t)extRays), sh = wave_sum((uint32_t)shadowRays);
+    if (lane == 0) { atomicAdd(&g->extRays, e); atomicAdd(&g->shadowRays, sh); }
+}
+
 // ---- kernel-level batch entry points (tests / roofline) -----------------------------------
 template <bool ANY>
 __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const dcrt_ray* rays, uint32_t n, uint32_t features,

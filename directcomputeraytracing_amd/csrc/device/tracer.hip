@@ -164,6 +164,8 @@ struct dcrt_tracer {
     }
     uint32_t FilmGrid() const { return std::max<uint32_t>(1u, std::min<uint32_t>((filmW * filmH + 255) / 256, kMaxPersistentBlocks)); }
     uint32_t castResident = 0;         // persistent cast grid: resident workgroups on the whole chip
+    uint32_t megaResident = 0;         // persistent megakernel grid
+    int mode = 0;                      // 0 wavefront (WavefrontPathTracer), 1 megakernel (MegakernelPathTracer)
     uint32_t CastGrid(uint32_t block) const { return std::min<uint32_t>((poolSize + block - 1) / block, castResident); }
 };
 
@@ -391,6 +393,9 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
             if (v >= 1 && v < perCU) perCU = v;
         }
         castResident = (uint32_t)std::max(1, perCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        int megaPerCU = 0;
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel, (int)castBlock, castLds));
+        megaResident = (uint32_t)std::max(1, megaPerCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
     }
     HIPCHECK(hipStreamSynchronize(stream));
     hasScene = true;
@@ -658,6 +663,34 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
     if (count == 0) return DCRT_OK;
+    if (mode == 1) {   // MegakernelPathTracer::Render: one persistent launch + SampleConvolution per image
+        CHECKED(UploadFilter(filter));
+        for (uint32_t img = 0; img < count; ++img) {
+            frame.frame_seed = firstSeed + img;
+            CHECKED(BeginImage());
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (extTiming) {
+                while (events.size() < eventsUsed + 2) {
+                    hipEvent_t e;
+                    HIPCHECK(hipEventCreate(&e));
+                    events.push_back(e);
+                }
+                e0 = events[eventsUsed++];
+                e1 = events[eventsUsed++];
+                HIPCHECK(hipEventRecord(e0, stream));
+            }
+            hipLaunchKernelGGL(megakernel, dim3(megaResident), dim3(castBlock), castLds, stream, scene, (const FrameConstants*)dFrame, film,
+                               dGlobals, (uint32_t)(film.debugRng != nullptr));
+            if (extTiming) HIPCHECK(hipEventRecord(e1, stream));
+            hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, partition.world_size,
+                               partition.rank, std::max<uint32_t>(partition.stripe_height, 1), (const Globals*)nullptr);
+            HIPCHECK(hipGetLastError());
+        }
+        HIPCHECK(hipStreamSynchronize(stream));
+        imageComplete = true;
+        newImage = true;
+        return DCRT_OK;
+    }
     frame.frame_seed = firstSeed;
     CHECKED(UploadFilter(filter));
     CHECKED(BeginImage());
@@ -1008,6 +1041,14 @@ DCRT_API int dcrt_tracer_trace_rays_device(dcrt_tracer* t, const void* d_rays, u
 {
     TRACER_GUARD(t);
     return TraceBatch(t, (const dcrt_ray*)d_rays, n, (dcrt_ray_hit*)d_hits, nullptr, false, features);
+}
+
+DCRT_API int dcrt_tracer_set_mode(dcrt_tracer* t, int mode)
+{
+    TRACER_GUARD(t);
+    if (mode != 0 && mode != 1) return DCRT_E_INVALID_ARG;
+    t->mode = mode;
+    return DCRT_OK;
 }
 
 DCRT_API int dcrt_tracer_resolve_image(dcrt_tracer* t, const dcrt_postfx_params* prm, uint8_t* out, float* outSumLogLum)

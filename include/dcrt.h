@@ -324,6 +324,9 @@ DCRT_API int dcrt_tracer_render(dcrt_tracer* tracer, uint32_t max_iterations);
  * convolved into the film (SampleConvolution) before the next starts. */
 DCRT_API int dcrt_tracer_render_images(dcrt_tracer* tracer, uint32_t first_seed, uint32_t image_count,
                                        const dcrt_filter_params* filter);
+/* 0 = wavefront (CWavefrontPathTracer, default), 1 = megakernel (CMegakernelPathTracer,
+ * MegakernelPathTracing.hlsl) for dcrt_tracer_render_images. */
+DCRT_API int dcrt_tracer_set_mode(dcrt_tracer* tracer, int mode);
 DCRT_API int dcrt_tracer_reset_image(dcrt_tracer* tracer);                                     /* ResetImage() */
 DCRT_API int dcrt_tracer_is_image_complete(dcrt_tracer* tracer, int* out_complete);           /* IsImageComplete() */
 DCRT_API int dcrt_tracer_acquire_film_clear_trigger(dcrt_tracer* tracer, int* out_trigger);    /* AcquireFilmClearTrigger() */

@@ -264,3 +264,37 @@ def test_postfx_resolve_bit_exact(native_lib, golden_luts, oracle_mod):
         assert same_bits(np.float32(lum), np.float32(oracle_mod.sum_log_luminance(film)))
     finally:
         t.destroy()
+
+
+@pytest.mark.parametrize("scene_name", ["cornell", "xml_mix", "lamp"])
+def test_megakernel_matches_oracle_megakernel(native_lib, golden_luts, oracle_mod, scene_name):
+    """CMegakernelPathTracer on the GPU == the oracle's MegakernelPathTracing restatement,
+    including bounce-0 triangle emission (where it differs from the wavefront, Appendix A.6)."""
+    from conftest import GOLDEN
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer
+    if scene_name == "cornell":
+        s = cornell(96, 72, 6)
+    elif scene_name == "xml_mix":
+        s = Scene((8, 8))
+        s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
+    else:
+        from test_oracle import load_fixture_scene
+        s = load_fixture_scene("lamp")
+    t = WavefrontPathTracer(path_pool_size=1 << 15, debug_rng=True)
+    try:
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        t.set_mode("megakernel")
+        for seed in (0, 3):
+            t.clear_film()
+            t.render_images(seed, 1)
+            pos, val = t.read_samples()
+            rng = t.read_rng()
+            p_ref, v_ref, r_ref, c_ref = oracle_mod.render(s.flat(), golden_luts, s.frame_params(seed), oracle_mod.MEGAKERNEL,
+                                                           rng=True)
+            assert np.array_equal(rng, r_ref)
+            assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
+            bad = np.count_nonzero(~same_bits(val, v_ref).all(-1))
+            assert bad == 0, f"{scene_name} seed {seed}: {bad} pixels differ"
+    finally:
+        t.destroy()
