@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
     ap.add_argument("--roofline-images", type=int, default=4)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (CPU reduce, for tests)")
+    ap.add_argument("--save-film", default=None, help="rank 0 writes the reduced RGBA32F film (.npy)")
     ap.add_argument("--mode", choices=["wavefront", "megakernel"], default="wavefront",
                     help="A/B: the reference's two tracers (the contract line is the wavefront)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
@@ -92,11 +94,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local_rank
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        device = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import numpy as np
     from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
@@ -104,7 +111,7 @@ def main():
 
     scene = Scene((args.width, args.height))
     scenes.setup_cornell(scene, args.width, args.height, args.bounces)
-    tracer = WavefrontPathTracer(path_pool_size=args.pool, iterations_per_render=args.iterations, device=local_rank)
+    tracer = WavefrontPathTracer(path_pool_size=args.pool, iterations_per_render=args.iterations, device=device)
     tracer.on_scene_loaded(scene)
     tracer.set_mode(args.mode)
     if world > 1:
@@ -119,9 +126,19 @@ def main():
             dist.barrier()
 
     film_buf = None
+    on_device = args.dist_backend == "nccl"
     if dist is not None:
         import torch
-        film_buf = torch.empty(args.width * args.height * 4, dtype=torch.float32, device="cuda")
+        film_buf = torch.empty(args.width * args.height * 4, dtype=torch.float32, device="cuda" if on_device else "cpu")
+
+    def reduce_film():
+        # the one data-path collective: SUM of the disjointly-supported stripe films on rank 0
+        if on_device:
+            tracer.copy_film_device(film_buf.data_ptr())
+        else:
+            import torch
+            film_buf.copy_(torch.from_numpy(tracer.read_film().reshape(-1)))
+        dist.reduce(film_buf, dst=0, op=dist.ReduceOp.SUM)
 
     # warmup (also builds the graphs)
     tracer.clear_film()
@@ -134,8 +151,7 @@ def main():
     images = args.steps * world            # weak scaling: each step is one image per GPU-equivalent
     tracer.render_images(0, images, filt)
     if dist is not None:
-        tracer.copy_film_device(film_buf.data_ptr())
-        dist.reduce(film_buf, dst=0, op=dist.ReduceOp.SUM)
+        reduce_film()
     barrier_sync()
     elapsed = time.perf_counter() - t0
     c = tracer.counters()
@@ -143,12 +159,16 @@ def main():
 
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda" if on_device else "cpu")
         tmax = t[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t[1:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed, rays = float(tmax.item()), float(tsum.item())
+
+    if args.save_film and rank == 0:
+        film = film_buf.cpu().numpy() if dist is not None else tracer.read_film()
+        np.save(args.save_film, film.reshape(args.height, args.width, 4))
 
     # ---- roofline leg: same workload (seeds 0..R-1), counters then HIP-event timing
     R = max(1, args.roofline_images)

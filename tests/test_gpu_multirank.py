@@ -1,0 +1,46 @@
+"""Multi-rank bench path on one GPU box: two ranks (gloo, both on cuda:0) render their
+film stripes and reduce; the reduced film must equal the single-rank film bit for bit."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_bench_film_equals_single_rank(tmp_path):
+    common = ["--steps", "1", "--warmup", "0", "--width", "256", "--height", "144", "--bounces", "4",
+              "--pool", str(1 << 16), "--no-cpu-baseline", "--roofline-images", "1", "--stripe", "16"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    single = tmp_path / "single.npy"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *common, "--save-film", str(single)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    multi = tmp_path / "multi.npy"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
+                        "--gpus", "2", *common, "--dist-backend", "gloo", "--save-film", str(multi)],
+                       capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1 and '"n_gpus": 2' in line[0]
+    a, b = np.load(single), np.load(multi)
+    # 2 images on 2 ranks vs 1 image on 1 rank: compare the 1-rank film of the same 2 images
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *common, "--steps", "2", "--save-film", str(single)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    a = np.load(single)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
