@@ -22,6 +22,7 @@ FEATURE_GGX_SAMPLE_VNDF = 0x01
 FEATURE_NO_FRONT_TO_BACK = 0x02
 FEATURE_LIGHT_VISIBLE = 0x04
 FEATURE_WATERTIGHT = 0x08
+FEATURE_ALLOW_ANYHIT = 0x10
 FEATURE_DEFAULT = FEATURE_GGX_SAMPLE_VNDF | FEATURE_LIGHT_VISIBLE | FEATURE_WATERTIGHT
 FILTER_BOX, FILTER_TRIANGLE, FILTER_GAUSSIAN, FILTER_MITCHELL, FILTER_LANCZOS = range(5)
 MATERIAL_DIFFUSE, MATERIAL_PLASTIC, MATERIAL_CONDUCTOR, MATERIAL_DIELECTRIC, MATERIAL_THIN_DIELECTRIC = range(5)
@@ -152,6 +153,9 @@ SIGNATURES = [
     ("dcrt_scene_get_resolution", _I, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     ("dcrt_scene_get_material_count", _I, [_P, C.POINTER(C.c_uint32)]),
     ("dcrt_scene_set_material", _I, [_P, _U, _I, _FP, C.c_float, _FP, _FP, _I, _I]),
+    ("dcrt_scene_set_material_opacity", _I, [_P, _U, C.c_float, C.c_int32]),
+    ("dcrt_scene_set_features", _I, [_P, _U]),
+    ("dcrt_scene_get_features", _I, [_P, C.POINTER(C.c_uint32)]),
     ("dcrt_scene_get_flat", _I, [_P, C.POINTER(FlatScene)]),
     ("dcrt_scene_get_frame_params", _I, [_P, _U, C.POINTER(FrameParams)]),
     ("dcrt_scene_get_bvh_info", _I, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),

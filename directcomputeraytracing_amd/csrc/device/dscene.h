@@ -163,6 +163,10 @@ struct TravState {
     bool inBlas, shearValid, found, parked, noZero;   // noZero: no component of o, d is +-0
     Shear sh;
     HitRecord hit;
+    // ALLOW_ANYHIT_SHADER only (dead, and removed by the compiler, otherwise)
+    float opacitySample;
+    uint32_t matOverride;     // the current instance's material override
+    bool opaque;              // the current instance's INSTANCE_FLAG_OPAQUE
 };
 
 DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax)
@@ -175,6 +179,34 @@ DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax)
     s.inBlas = false; s.shearValid = false; s.found = false; s.parked = false;
     s.noZero = o.x != 0.0f && o.y != 0.0f && o.z != 0.0f && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
     s.hit.t = 0.0f; s.hit.u = 0.0f; s.hit.v = 0.0f; s.hit.tri = 0u; s.hit.inst = 0u;
+    s.opacitySample = 0.0f; s.matOverride = DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE; s.opaque = false;
+}
+
+DEV void sample_texture_wrap(const DeviceScene& s, uint32_t index, float u, float v, float* out);
+
+// AnyHitShader (HitShader.inc.hlsl:86-113): a hit on a non-opaque instance counts only
+// when the ray's opacity sample is below the material's (texture-modulated) opacity.
+DEV bool any_hit_shader(const DeviceScene& sc, uint32_t tri, uint32_t ov, float u, float v, float opacitySample)
+{
+    const uint32_t mid = ov != DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE ? ov : sc.materialIds[tri];
+    const dcrt_material& m = sc.materials[mid];
+    float opacity = m.opacity;
+    if (m.opacity_texture_index != -1) {
+        const dcrt_vertex& V0 = sc.vertices[sc.triangles[tri * 3]];
+        const dcrt_vertex& V1 = sc.vertices[sc.triangles[tri * 3 + 1]];
+        const dcrt_vertex& V2 = sc.vertices[sc.triangles[tri * 3 + 2]];
+        // VectorBaryCentric2 (Math.inc.hlsl:23-33), then texTiling
+        float r1x = V1.texcoord[0] - V0.texcoord[0], r1y = V1.texcoord[1] - V0.texcoord[1];
+        float r2x = V2.texcoord[0] - V0.texcoord[0], r2y = V2.texcoord[1] - V0.texcoord[1];
+        r1x = r1x * u; r1y = r1y * u; r2x = r2x * v; r2y = r2y * v;
+        r1x = r1x + V0.texcoord[0]; r1y = r1y + V0.texcoord[1];
+        float tcx = r1x + r2x, tcy = r1y + r2y;
+        tcx = tcx * m.tex_tiling[0]; tcy = tcy * m.tex_tiling[1];
+        float rgba[4];
+        sample_texture_wrap(sc, (uint32_t)m.opacity_texture_index, tcx, tcy, rgba);
+        opacity = opacity * rgba[0];
+    }
+    return opacitySample < opacity;
 }
 
 // Pop the next node (BVHAccel.inc.hlsl stack pop); true when the stack is empty.
@@ -243,7 +275,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds
 
 // Phase B: the parked leaf's work. TLAS leaf: move the ray into the instance and
 // continue at its BLAS root. BLAS leaf: test triangles [ref, ref + count), then pop.
-template <bool ANY_HIT, bool INSTR>
+template <bool ANY_HIT, bool INSTR, bool OPACITY = false>
 DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t stride, TraversalStats& st)
 {
     s.parked = false;
@@ -264,6 +296,10 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         s.inBlas = true;
         s.inst = primOrInst;
         s.node = s.leafRef;
+        if (OPACITY) {   // BVHAccel.inc.hlsl:136-139
+            s.opaque = (sc.instanceFlags[primOrInst] & DCRT_INSTANCE_FLAG_OPAQUE) != 0u;
+            s.matOverride = sc.overrides[primOrInst];
+        }
         if (INSTR) ++st.blas;
         return false;
     }
@@ -277,8 +313,9 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         const float4 q2 = sc.triVerts[(size_t)p * 3 + 2];
         const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
         float t, u, v; bool bf;
-        const bool h = watertight ? tri_watertight(s.lo, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
-                                  : tri_moller(s.lo, s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
+        bool h = watertight ? tri_watertight(s.lo, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
+                            : tri_moller(s.lo, s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
+        if (OPACITY && h && !s.opaque) h = any_hit_shader(sc, p, s.matOverride, u, v, s.opacitySample);
         if (h) {
             s.found = true;
             if (ANY_HIT) return true;

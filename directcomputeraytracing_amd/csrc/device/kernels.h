@@ -133,6 +133,8 @@ struct PathPool {
     float4* throughput;  // T.xyz, bsdfPdf
     float4* li;          // Li.xyz, isDeltaBxdf (0/1)
     uint32_t* flags;
+    float* extOpacity;         // ALLOW_ANYHIT_SHADER: g_ExtensionRayOpacitySamples
+    float* shadowOpacity;      //                      g_ShadowRayOpacitySamples
     uint32_t* extQueue;        // kShards x size entries each
     uint32_t* shadowQueue;
     uint32_t* materialQueue;

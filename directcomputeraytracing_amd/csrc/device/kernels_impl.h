@@ -136,6 +136,7 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
             const float a0 = next1(rng), a1 = next1(rng), a2 = next1(rng);
             V3 o, d;
             generate_ray(*fc, fsx, fsy, a0, a1, a2, &o, &d);
+            if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) pool.extOpacity[tid] = next1(rng);   // :223-226
             pool.pixel[tid] = px | (py << 16);
             pool.pixelSample[tid] = make_float2(psx, psy);
             pool.lsr[tid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -244,6 +245,10 @@ __global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScen
             }
             thr.w = bsdfPdf;
             li.w = isDelta ? 1.0f : 0.0f;
+            if (features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430
+                if (!terminate) pool.extOpacity[path] = next1(rng);
+                if (hasShadow) pool.shadowOpacity[path] = next1(rng);
+            }
         }
         if (!hasShadow) flags = flags & ~kFlagShadowRayHit;
         pool.flags[path] = flags;
@@ -273,7 +278,7 @@ __global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScen
 // the next items of the wave's range (ballot + mbcnt, no atomics), so all 64
 // lanes keep traversing until the range is drained.
 
-template <bool ANY_HIT, bool INSTR, typename Fetch, typename Emit>
+template <bool ANY_HIT, bool INSTR, bool OPACITY, typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
                                                  uint32_t kParkLanes, uint32_t* lds, uint32_t stride, Fetch fetch, Emit emit,
                                                  TraversalStats& st)
@@ -315,7 +320,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             if (runnable == 0ull || parked >= kParkLanes || (idle >= kRefillLanes && cursor < end)) break;
         }
         // phase B: the parked lanes' leaf work, shared by many lanes at once
-        if (active && s.parked && trav_leaf<ANY_HIT, INSTR>(sc, s, watertight, lds, stride, st)) {
+        if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY>(sc, s, watertight, lds, stride, st)) {
             emit(item, s);
             active = false;
         }
@@ -328,7 +333,9 @@ __device__ __forceinline__ void flush_stats(const TraversalStats& st, unsigned l
     if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&dst[0], a); atomicAdd(&dst[1], b); atomicAdd(&dst[2], c); }
 }
 
-template <bool INSTR>
+// OPACITY: the ALLOW_ANYHIT_SHADER variant (a separate instantiation, so the default
+// kernels carry none of its state).
+template <bool INSTR, bool OPACITY>
 __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, const Counters* cnt,
                                                          Globals* g, unsigned long long* instr)
 {
@@ -336,12 +343,13 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
     QueueMap qm;
     qmap(cnt, kQExt, &qm);
     TraversalStats st = {0u, 0u, 0u};
-    persistent_trace<false, INSTR>(
+    persistent_trace<false, INSTR, OPACITY>(
         sc, qm.prefix[kShards], fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, blockDim.x,
         [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const uint32_t path = qentry(pool.extQueue, pool.size, qm, i);
             const float4 o = pool.rayO[path], d = pool.rayD[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf());
+            if (OPACITY) s.opacitySample = pool.extOpacity[path];
             return path;
         },
         [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
@@ -353,7 +361,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
     (void)g;
 }
 
-template <bool INSTR>
+template <bool INSTR, bool OPACITY>
 __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
                                                       Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
@@ -362,12 +370,13 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
     qmap(cnt, kQShadow, &qm);
     const uint32_t n = qm.prefix[kShards];
     TraversalStats st = {0u, 0u, 0u};
-    persistent_trace<true, INSTR>(
+    persistent_trace<true, INSTR, OPACITY>(
         sc, n, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, blockDim.x,
         [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const uint32_t path = qentry(pool.shadowQueue, pool.size, qm, i);
             const float4 o = pool.shadowO[path], d = pool.shadowD[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, o.w);
+            if (OPACITY) s.opacitySample = pool.shadowOpacity[path];
             return path;
         },
         [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
@@ -395,21 +404,23 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
 // pixel block (same per-shard cursors as CONTROL). Shares every device function with
 // the wavefront kernels; differs from them only in the bounce-0 triangle-light
 // emission, exactly like the reference's two tracers.
-template <bool ANY_HIT>
+template <bool ANY_HIT, bool OPACITY>
 __device__ __forceinline__ bool trace_full(const DeviceScene& sc, V3 o, V3 d, float tMax, bool watertight, bool f2b,
-                                           uint32_t* lds, uint32_t stride, HitRecord* hit)
+                                           float opacitySample, uint32_t* lds, uint32_t stride, HitRecord* hit)
 {
     TravState s;
     trav_init(s, o, d, 0.0f, tMax);
+    s.opacitySample = opacitySample;
     TraversalStats st = {0u, 0u, 0u};
     for (;;) {
         if (trav_visit<false>(sc, s, f2b, lds, stride, st)) break;
-        if (s.parked && trav_leaf<ANY_HIT, false>(sc, s, watertight, lds, stride, st)) break;
+        if (s.parked && trav_leaf<ANY_HIT, false, OPACITY>(sc, s, watertight, lds, stride, st)) break;
     }
     *hit = s.hit;
     return s.found;
 }
 
+template <bool OPACITY>
 __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameConstants* fcp, Film film, Globals* g, uint32_t debugRng)
 {
     extern __shared__ uint32_t stackMem[];
@@ -454,7 +465,9 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
         for (;;) {
             HitRecord hit;
             ++extRays;
-            const bool hasHit = trace_full<false>(sc, ro, rd, inf(), watertight, f2b, lds, stride, &hit);
+            // IntersectScene draws the ray's opacity sample (MegakernelPathTracing.hlsl:27-28)
+            const float extOpacity = OPACITY ? next1(rng) : 0.0f;
+            const bool hasHit = trace_full<false, OPACITY>(sc, ro, rd, inf(), watertight, f2b, extOpacity, lds, stride, &hit);
             const float hitT = hasHit ? hit.t : inf();
             Intersection it;
             it.lightIndex = DCRT_LIGHT_INDEX_INVALID; it.triangleIndex = 0;
@@ -500,6 +513,8 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
                     hasShadow = true;
                 }
             }
+            // IsOcculuded draws its opacity sample before the BSDF sample (:57-58)
+            const float shadowOpacity = OPACITY && hasShadow ? next1(rng) : 0.0f;
             bool terminate = false;
             {
                 const float sel = next1(rng);
@@ -523,7 +538,7 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
             if (hasShadow) {
                 ++shadowRays;
                 HitRecord sh;
-                const bool occluded = trace_full<true>(sc, so, sd, sdist, watertight, f2b, lds, stride, &sh);
+                const bool occluded = trace_full<true, OPACITY>(sc, so, sd, sdist, watertight, f2b, shadowOpacity, lds, stride, &sh);
                 if (!occluded) L = L + lsr;
             }
             if (terminate) break;
@@ -544,7 +559,7 @@ __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const 
 {
     extern __shared__ uint32_t stackMem[];
     TraversalStats st = {0u, 0u, 0u};
-    persistent_trace<ANY, true>(
+    persistent_trace<ANY, true, false>(
         sc, n, features, 16u, 32u, stackMem + threadIdx.x, blockDim.x,
         [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const dcrt_ray r = rays[i];
@@ -851,10 +866,16 @@ __global__ void lut_finalize_kernel(const float* brdf, const float* brdfd, const
 }
 
 // ---- explicit instantiations used by tracer.hip ---------------------------------------
-template __global__ void extension_kernel<false>(PathPool, DeviceScene, const FrameConstants*, const Counters*, Globals*, unsigned long long*);
-template __global__ void extension_kernel<true>(PathPool, DeviceScene, const FrameConstants*, const Counters*, Globals*, unsigned long long*);
-template __global__ void shadow_kernel<false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void shadow_kernel<true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void extension_kernel<false, false>(PathPool, DeviceScene, const FrameConstants*, const Counters*, Globals*, unsigned long long*);
+template __global__ void extension_kernel<false, true>(PathPool, DeviceScene, const FrameConstants*, const Counters*, Globals*, unsigned long long*);
+template __global__ void extension_kernel<true, false>(PathPool, DeviceScene, const FrameConstants*, const Counters*, Globals*, unsigned long long*);
+template __global__ void extension_kernel<true, true>(PathPool, DeviceScene, const FrameConstants*, const Counters*, Globals*, unsigned long long*);
+template __global__ void shadow_kernel<false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void shadow_kernel<false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void shadow_kernel<true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void shadow_kernel<true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void megakernel<false>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
+template __global__ void megakernel<true>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void batch_trace_kernel<false>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
 template __global__ void batch_trace_kernel<true>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
 

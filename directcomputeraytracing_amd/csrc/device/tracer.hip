@@ -4,6 +4,7 @@
 // Reference: Source/WavefrontPathTracer.cpp:70-1162, Source/Scene.cpp:273-608,
 // Source/SampleConvolution.cpp:89-170, Source/BxDFTexturesBuilding.cpp:106-475.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -164,9 +165,13 @@ struct dcrt_tracer {
     }
     uint32_t FilmGrid() const { return std::max<uint32_t>(1u, std::min<uint32_t>((filmW * filmH + 255) / 256, kMaxPersistentBlocks)); }
     uint32_t castResident = 0;         // persistent cast grid: resident workgroups on the whole chip
+    uint32_t castResidentOpacity = 0;  // the same for the ALLOW_ANYHIT_SHADER variant
     uint32_t megaResident = 0;         // persistent megakernel grid
     int mode = 0;                      // 0 wavefront (WavefrontPathTracer), 1 megakernel (MegakernelPathTracer)
-    uint32_t CastGrid(uint32_t block) const { return std::min<uint32_t>((poolSize + block - 1) / block, castResident); }
+    uint32_t CastGrid(uint32_t block, bool opacity) const
+    {
+        return std::min<uint32_t>((poolSize + block - 1) / block, opacity ? castResidentOpacity : castResident);
+    }
 };
 
 dcrt_tracer::~dcrt_tracer()
@@ -227,6 +232,8 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.throughput, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.li, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.extOpacity, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.shadowOpacity, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.extQueue, (size_t)P * kShards, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowQueue, (size_t)P * kShards, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.materialQueue, (size_t)P * kShards, &poolAllocs));
@@ -387,14 +394,17 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         hipDeviceProp_t prop;
         HIPCHECK(hipGetDeviceProperties(&prop, device));
         int perCU = 0;
-        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false>, (int)castBlock, castLds));
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false, false>, (int)castBlock, castLds));
         if (const char* b = std::getenv("DCRT_CAST_BLOCKS_PER_CU")) {   // tuning experiments
             const int v = std::atoi(b);
             if (v >= 1 && v < perCU) perCU = v;
         }
         castResident = (uint32_t)std::max(1, perCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        int opacityPerCU = 0;
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLds));
+        castResidentOpacity = (uint32_t)std::max(1, std::min(opacityPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int megaPerCU = 0;
-        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel, (int)castBlock, castLds));
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel<false>, (int)castBlock, castLds));
         megaResident = (uint32_t)std::max(1, megaPerCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
     }
     HIPCHECK(hipStreamSynchronize(stream));
@@ -466,6 +476,10 @@ int dcrt_tracer::SetFrame(const dcrt_frame_params& p)
         return DCRT_E_INVALID_ARG;
     }
     CHECKED(EnsureFilm(p.resolution[0], p.resolution[1]));
+    if ((frame.features ^ p.features) & DCRT_FEATURE_ALLOW_ANYHIT) {   // captured graphs hold the other kernel variant
+        HIPCHECK(hipStreamSynchronize(stream));
+        InvalidateGraph();
+    }
     frame = p;
     hasFrame = true;
     return DCRT_OK;
@@ -532,7 +546,8 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     Counters* next = dCounters + (par ^ 1u);
     const uint32_t controlGrid = std::min<uint32_t>(poolSize / kControlBlock, kMaxPersistentBlocks);
     const uint32_t materialGrid = std::min<uint32_t>((poolSize + kMaterialBlock - 1) / kMaterialBlock, kMaxPersistentBlocks);
-    const uint32_t castGrid = CastGrid(castBlock);
+    const bool opacity = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) != 0;
+    const uint32_t castGrid = CastGrid(castBlock, opacity);
     hipLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, pool, film, (const FrameConstants*)dFrame, cnt,
                        dGlobals, (uint32_t)(film.debugRng != nullptr));
     hipLaunchKernelGGL(material_kernel, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt);
@@ -545,21 +560,18 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
         }
         e0 = events[eventsUsed++];
         e1 = events[eventsUsed++];
-        HIPCHECK(hipEventRecord(e0, stream));
     }
-    if (instrCounters)
-        hipLaunchKernelGGL(extension_kernel<true>, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame,
-                           (const Counters*)cnt, dGlobals, dInstr);
-    else
-        hipLaunchKernelGGL(extension_kernel<false>, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame,
-                           (const Counters*)cnt, dGlobals, dInstr);
-    if (timed) HIPCHECK(hipEventRecord(e1, stream));
-    if (instrCounters)
-        hipLaunchKernelGGL(shadow_kernel<true>, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
-                           next, dGlobals, dInstr);
-    else
-        hipLaunchKernelGGL(shadow_kernel<false>, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
-                           next, dGlobals, dInstr);
+    // Timed launches take their start/stop timestamps from the dispatch itself
+    // (hipExtLaunchKernelGGL), so the duration is the kernel's, as rocprofv3 reports it.
+    // kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER
+    auto ext = instrCounters ? (opacity ? extension_kernel<true, true> : extension_kernel<true, false>)
+                             : (opacity ? extension_kernel<false, true> : extension_kernel<false, false>);
+    auto shadow = instrCounters ? (opacity ? shadow_kernel<true, true> : shadow_kernel<true, false>)
+                                : (opacity ? shadow_kernel<false, true> : shadow_kernel<false, false>);
+    hipExtLaunchKernelGGL(ext, dim3(castGrid), dim3(castBlock), castLds, stream, e0, e1, 0, pool, scene,
+                          (const FrameConstants*)dFrame, (const Counters*)cnt, dGlobals, dInstr);
+    hipLaunchKernelGGL(shadow, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
+                       next, dGlobals, dInstr);
     if (sequenced) {
         hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, partition.world_size,
                            partition.rank, std::max<uint32_t>(partition.stripe_height, 1), (const Globals*)dGlobals);
@@ -677,11 +689,10 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
                 }
                 e0 = events[eventsUsed++];
                 e1 = events[eventsUsed++];
-                HIPCHECK(hipEventRecord(e0, stream));
             }
-            hipLaunchKernelGGL(megakernel, dim3(megaResident), dim3(castBlock), castLds, stream, scene, (const FrameConstants*)dFrame, film,
-                               dGlobals, (uint32_t)(film.debugRng != nullptr));
-            if (extTiming) HIPCHECK(hipEventRecord(e1, stream));
+            auto mk = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) ? megakernel<true> : megakernel<false>;
+            hipExtLaunchKernelGGL(mk, dim3(megaResident), dim3(castBlock), castLds, stream, e0, e1, 0, scene,
+                                  (const FrameConstants*)dFrame, film, dGlobals, (uint32_t)(film.debugRng != nullptr));
             hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, partition.world_size,
                                partition.rank, std::max<uint32_t>(partition.stripe_height, 1), (const Globals*)nullptr);
             HIPCHECK(hipGetLastError());
@@ -700,22 +711,21 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     const uint64_t maxIterations = ((uint64_t)count + 2) * (frame.max_bounce_count + 8) * (1 + (filmW * (uint64_t)filmH) / poolSize) + 64;
     uint64_t launched = 0;
     bool stopped = false;
-    if (extTiming) {
-        while (!stopped && launched < maxIterations) {
-            for (uint32_t i = 0; i < 8; ++i, ++launched) {
-                CHECKED(LaunchIteration(parity, true, true));
-                parity ^= 1u;
-            }
-            HIPCHECK(hipMemcpyAsync(hStop, &dGlobals->stopped, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-            HIPCHECK(hipStreamSynchronize(stream));
-            stopped = hStop[0] != 0;
-        }
-    } else {
+    {
+        // chunks of `chunk` iterations (a replayed graph, or plain timed launches when the
+        // EXT kernel is being timed), the "stopped" word polled two chunks behind
         const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
         uint32_t inflight[4];
         uint32_t head = 0, size = 0, slot = 0;
         while (!stopped && launched < maxIterations) {
-            CHECKED(LaunchGraph(true, chunk));
+            if (extTiming) {
+                for (uint32_t i = 0; i < chunk; ++i) {
+                    CHECKED(LaunchIteration(parity, true, true));
+                    parity ^= 1u;
+                }
+            } else {
+                CHECKED(LaunchGraph(true, chunk));
+            }
             launched += chunk;
             HIPCHECK(hipMemcpyAsync(&hStop[slot], &dGlobals->stopped, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
             HIPCHECK(hipEventRecord(stopEvents[slot], stream));

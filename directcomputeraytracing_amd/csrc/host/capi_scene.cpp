@@ -166,6 +166,19 @@ DCRT_API int dcrt_scene_get_material_count(const dcrt_scene* s, uint32_t* out)
     return DCRT_OK;
 }
 
+// Material edits: mesh OPAQUE flags (Scene.cpp:57-80) and the flattened buffers
+// (instance flags, Scene.cpp:785-800) follow the materials.
+static void RefreshMaterials(dcrt_scene* s)
+{
+    if (!s->scene.hasValidScene) return;
+    for (size_t i = 0; i < s->scene.meshes.size(); ++i) {
+        bool opaque = true;
+        for (uint32_t id : s->scene.meshes[i].materialIds) opaque = opaque && s->scene.materials[id].IsOpaque();
+        s->scene.meshOpaque[i] = opaque;
+    }
+    s->scene.Flatten();
+}
+
 DCRT_API int dcrt_scene_set_material(dcrt_scene* s, uint32_t index, int type, const float albedo[3], float roughness,
                                      const float ior[3], const float k[3], int multiscattering, int two_sided)
 {
@@ -178,14 +191,35 @@ DCRT_API int dcrt_scene_set_material(dcrt_scene* s, uint32_t index, int type, co
     if (k) m.k = dcrt::Float3(k[0], k[1], k[2]);
     m.multiscattering = multiscattering != 0;
     m.isTwoSided = two_sided != 0;
-    if (s->scene.hasValidScene) {
-        for (size_t i = 0; i < s->scene.meshes.size(); ++i) {
-            bool opaque = true;
-            for (uint32_t id : s->scene.meshes[i].materialIds) opaque = opaque && s->scene.materials[id].IsOpaque();
-            s->scene.meshOpaque[i] = opaque;
-        }
-        s->scene.Flatten();
-    }
+    RefreshMaterials(s);
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_set_material_opacity(dcrt_scene* s, uint32_t index, float opacity, int32_t opacity_texture_index)
+{
+    if (!s || index >= s->scene.materials.size()) return DCRT_E_INVALID_ARG;
+    if (opacity_texture_index < -1 || (opacity_texture_index >= 0 && (size_t)opacity_texture_index >= s->scene.textures.size()))
+        return DCRT_E_INVALID_ARG;
+    dcrt::SMaterial& m = s->scene.materials[index];
+    m.opacity = opacity;
+    m.opacityTextureIndex = opacity_texture_index;
+    RefreshMaterials(s);
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_set_features(dcrt_scene* s, uint32_t features)
+{
+    const uint32_t known = DCRT_FEATURE_GGX_SAMPLE_VNDF | DCRT_FEATURE_NO_FRONT_TO_BACK | DCRT_FEATURE_LIGHT_VISIBLE |
+                           DCRT_FEATURE_WATERTIGHT | DCRT_FEATURE_ALLOW_ANYHIT;
+    if (!s || (features & ~known)) return DCRT_E_INVALID_ARG;
+    s->scene.features = features;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_features(const dcrt_scene* s, uint32_t* out)
+{
+    if (!s || !out) return DCRT_E_INVALID_ARG;
+    *out = s->scene.features;
     return DCRT_OK;
 }
 

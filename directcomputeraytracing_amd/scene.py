@@ -94,6 +94,21 @@ class Scene:
                                                 f3(k) if k is not None else None,
                                                 int(multiscattering), int(two_sided)), "SetMaterial")
 
+    def set_material_opacity(self, index, opacity=1.0, opacity_texture_index=-1) -> None:   # ImGui.cpp:630-650
+        check(self._lib.dcrt_scene_set_material_opacity(self._h, int(index), float(opacity), int(opacity_texture_index)),
+              "SetMaterialOpacity")
+
+    @property
+    def features(self) -> int:
+        """DCRT_FEATURE_* toggles (Scene.h:141-145); frame_params() carries them."""
+        n = C.c_uint32()
+        check(self._lib.dcrt_scene_get_features(self._h, C.byref(n)))
+        return n.value
+
+    @features.setter
+    def features(self, value: int) -> None:
+        check(self._lib.dcrt_scene_set_features(self._h, int(value)), "SetFeatures")
+
     @property
     def material_count(self) -> int:
         n = C.c_uint32()
@@ -144,6 +159,8 @@ class Scene:
             "bvh_nodes": view(f.bvh_nodes, f.bvh_node_count, np.uint32, 8),
             "material_ids": view(f.material_ids, f.triangle_count, np.uint32),
             "instance_transforms": view(f.instance_transforms, f.instance_count * 2, np.float32, 12),
+            "instance_flags": view(f.instance_flags, f.instance_count, np.uint32),
+            "instance_material_overrides": view(f.instance_material_overrides, f.instance_count, np.uint32),
             "materials": view(f.materials, f.material_count, np.uint32, 13),
             "lights": view(f.lights, f.light_count, np.uint32, 7),
             "tlas_node_count": f.tlas_node_count,

@@ -365,3 +365,52 @@ def write_lamp(directory: Path | str, width: int = 3840, height: int = 2160, seg
     p = d / "lamp.xml"
     p.write_text(_xml(body))
     return p
+
+
+def _write_bytes(path: Path, data: bytes) -> Path:
+    if not path.exists() or path.read_bytes() != data:
+        path.write_bytes(data)
+    return path
+
+
+def write_anyhit(directory: Path | str, width: int = 64, height: int = 48) -> Path:
+    """ALLOW_ANYHIT_SHADER / texture fixture: a cut-out leaf (``mask`` BSDF with a PGM opacity
+    bitmap) on an OBJ quad, a half-transparent veil (``mask`` with a float opacity) on the
+    shared rectangle mesh (material via instance override; the reference's rectangle has zero
+    texcoords, Mesh.cpp:31-36), an opaque wall and a floor with a PPM albedo bitmap; an area
+    light and a constant environment. Textures are binary PGM/PPM."""
+    d = Path(directory)
+    d.mkdir(parents=True, exist_ok=True)
+    n = 16
+    yy, xx = np.mgrid[0:n, 0:n]
+    r = np.hypot(xx - (n - 1) / 2, yy - (n - 1) / 2) / (n / 2)
+    mask = np.clip(255 * (1.2 - r), 0, 255).astype(np.uint8)
+    mask[::4, :] = 0                                   # slits: fully cut-out rows
+    _write_bytes(d / "leaf_mask.pgm", f"P5 {n} {n} 255\n".encode() + mask.tobytes())
+    m = 8
+    checker = ((np.arange(m)[:, None] // 2 + np.arange(m)[None, :] // 2) % 2).astype(bool)
+    rgb = np.where(checker[..., None], np.array([200, 180, 60], np.uint8), np.array([40, 90, 160], np.uint8))
+    _write_bytes(d / "floor_albedo.ppm", f"P6 {m} {m} 255\n".encode() + rgb.astype(np.uint8).tobytes())
+    write_obj(d / "quad.obj", [(-1, 0, -1), (1, 0, -1), (1, 0, 1), (-1, 0, 1)], [(0, 1, 0)] * 4,
+              [(0, 0), (1, 0), (1, 1), (0, 1)], [(0, 1, 2), (0, 2, 3)])
+    body = (
+        '  <integrator type="path"><integer name="max_depth" value="6"/></integrator>\n'
+        + _sensor("perspective", width, height, mitsuba_matrix((0.0, 1.0, -3.5), pitch=8),
+                  '    <float name="fov" value="55"/>\n')
+        + '  <bsdf type="twosided" id="floor"><bsdf type="diffuse"><texture name="reflectance" type="bitmap">'
+          '<string name="filename" value="floor_albedo.ppm"/></texture></bsdf></bsdf>\n'
+          '  <bsdf type="mask" id="leaf"><texture name="opacity" type="bitmap"><string name="filename" value="leaf_mask.pgm"/>'
+          '</texture><bsdf type="twosided"><bsdf type="diffuse"><rgb name="reflectance" value="0.2, 0.7, 0.25"/></bsdf></bsdf></bsdf>\n'
+          '  <bsdf type="mask" id="veil"><float name="opacity" value="0.4"/><bsdf type="roughplastic">'
+          '<rgb name="diffuse_reflectance" value="0.8, 0.3, 0.3"/><float name="alpha" value="0.1"/></bsdf></bsdf>\n'
+          '  <bsdf type="diffuse" id="wall"><rgb name="reflectance" value="0.7, 0.7, 0.7"/></bsdf>\n'
+        f'  <shape type="obj" id="shape_floor"><string name="filename" value="quad.obj"/><ref id="floor"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 0, 0), scale=(3, 1, 3))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_wall"><ref id="wall"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 1.5, 2.0), yaw=180, scale=(3, 1.5, 1))}"/></transform></shape>\n'
+        f'  <shape type="obj" id="shape_leaf"><string name="filename" value="quad.obj"/><ref id="leaf"/><transform name="to_world"><matrix value="{mitsuba_matrix((-0.5, 1.0, 0.0), pitch=-90, scale=(0.7, 1, 0.7))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_veil"><ref id="veil"/><transform name="to_world"><matrix value="{mitsuba_matrix((0.6, 0.9, 0.6), yaw=180, scale=(0.6, 0.6, 1))}"/></transform></shape>\n'
+        f'  <shape type="rectangle" id="shape_light"><emitter type="area"><rgb name="radiance" value="7, 6.5, 6"/></emitter><transform name="to_world"><matrix value="{mitsuba_matrix((0.3, 2.4, -0.5), pitch=90, scale=(0.5, 0.5, 1))}"/></transform></shape>\n'
+        '  <emitter type="constant"><rgb name="radiance" value="0.25, 0.3, 0.4"/></emitter>\n'
+    )
+    p = d / "anyhit.xml"
+    p.write_text(_xml(body))
+    return p

@@ -82,6 +82,8 @@ extern "C" {
 #define DCRT_FEATURE_NO_FRONT_TO_BACK         0x02u  /* BVH_NO_FRONT_TO_BACK_TRAVERSAL (off)    */
 #define DCRT_FEATURE_LIGHT_VISIBLE            0x04u  /* LIGHT_VISIBLE (default on)              */
 #define DCRT_FEATURE_WATERTIGHT               0x08u  /* WATERTIGHT_RAY_TRIANGLE_INTERSECTION(on)*/
+#define DCRT_FEATURE_ALLOW_ANYHIT             0x10u  /* ALLOW_ANYHIT_SHADER (off): opacity test on
+                                                        non-opaque instances (HitShader.inc.hlsl:86-113) */
 #define DCRT_FEATURE_DEFAULT (DCRT_FEATURE_GGX_SAMPLE_VNDF | DCRT_FEATURE_LIGHT_VISIBLE | DCRT_FEATURE_WATERTIGHT)
 
 /* ---- Appendix-B layouts ------------------------------------------------ */
@@ -295,6 +297,16 @@ DCRT_API int dcrt_scene_get_material_count(const dcrt_scene* scene, uint32_t* ou
 DCRT_API int dcrt_scene_set_material(dcrt_scene* scene, uint32_t index, int material_type, const float albedo[3],
                                      float roughness, const float ior[3], const float k[3],
                                      int multiscattering, int two_sided);
+/* Material opacity and opacity texture (ImGui.cpp:630-650, SMaterial::m_Opacity /
+ * m_OpacityTextureIndex); texture index -1 = none. Recomputes the instance OPAQUE flags
+ * (Scene.cpp:57-80, 785-800). */
+DCRT_API int dcrt_scene_set_material_opacity(dcrt_scene* scene, uint32_t index, float opacity,
+                                             int32_t opacity_texture_index);
+/* Shader feature toggles of the scene (Scene.h:140-146: m_IsGGXVNDFSamplingEnabled,
+ * m_TraverseBVHFrontToBack, m_IsLightVisible, m_WatertightRayTriangleIntersection,
+ * m_AllowAnyHitShader) as DCRT_FEATURE_* bits; get_frame_params reports them. */
+DCRT_API int dcrt_scene_set_features(dcrt_scene* scene, uint32_t features);
+DCRT_API int dcrt_scene_get_features(const dcrt_scene* scene, uint32_t* out_features);
 /* Flattened buffers; pointers stay valid until the scene is modified or destroyed. */
 DCRT_API int dcrt_scene_get_flat(dcrt_scene* scene, dcrt_flat_scene* out_flat);
 /* The frame constants Render() would upload (WavefrontPathTracer.cpp:372-428). */

@@ -529,17 +529,23 @@ typedef struct hit_info { float t, u, v; uint32_t triangleId, instanceIndex; int
 
 #define O_MAX_STACK 256
 
+static int any_hit_shader(const dcrt_flat_scene* sc, uint32_t tri, uint32_t materialOverride, float u, float v,
+                          float opacitySample);
+
+/* `opacitySample` is used only with DCRT_FEATURE_ALLOW_ANYHIT (BVHAccel.inc.hlsl:95-101, 182-190). */
 static int bvh_intersect(const dcrt_flat_scene* sc, v3 origin, v3 direction, float tMin, float tMaxIn,
-                         int anyHit, uint32_t features, hit_info* hit, uint64_t* nodeVisits, uint64_t* triTests,
-                         uint64_t* blasEntries)
+                         int anyHit, uint32_t features, float opacitySample, hit_info* hit, uint64_t* nodeVisits,
+                         uint64_t* triTests, uint64_t* blasEntries)
 {
     uint32_t stack[O_MAX_STACK];
     int count = 0;
     float tMax = tMaxIn;
     const int watertight = (features & DCRT_FEATURE_WATERTIGHT) != 0;
     const int f2b = (features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
+    const int allowAnyHit = (features & DCRT_FEATURE_ALLOW_ANYHIT) != 0;
     uint32_t nodeIndex = 0, instanceIndex = 0;
-    int isBLAS = 0;
+    uint32_t materialOverride = DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE;
+    int isBLAS = 0, isOpaque = 0;
     v3 lo = origin, ld = direction;
     const uint32_t instanceCount = sc->instance_count;
     for (;;) {
@@ -557,6 +563,8 @@ static int bvh_intersect(const dcrt_flat_scene* sc, v3 origin, v3 direction, flo
                 isBLAS = 1;
                 instanceIndex = primCountOrInstance;
                 nodeIndex = node->right_child_or_prim_index;
+                isOpaque = (sc->instance_flags[primCountOrInstance] & DCRT_INSTANCE_FLAG_OPAQUE) != 0;   /* :136-139 */
+                materialOverride = sc->instance_material_overrides[primCountOrInstance];
                 if (blasEntries) ++*blasEntries;
             } else if (primCountOrInstance == 0) {
                 uint32_t axis = node->misc & 0x3u;
@@ -578,6 +586,8 @@ static int bvh_intersect(const dcrt_flat_scene* sc, v3 origin, v3 direction, flo
                     float t, u, v; int bf;
                     int h = watertight ? tri_watertight(lo, shear, perm, tMin, tMax, v0, v1, v2, &t, &u, &v, &bf)
                                        : tri_moller(lo, ld, tMin, tMax, v0, v1, v2, &t, &u, &v, &bf);
+                    if (h && allowAnyHit && !isOpaque)
+                        h = any_hit_shader(sc, p, materialOverride, u, v, opacitySample);
                     if (h) {
                         if (anyHit) return 1;
                         tMax = t;
@@ -717,6 +727,26 @@ static void sample_texture_wrap(const dcrt_texture* t, float u, float v, float o
         out[i] = top * (1.0f - fy) + bot * fy;
     }
 }
+/* AnyHitShader (HitShader.inc.hlsl:86-113): accept when opacitySample < opacity. */
+static f2 bary2(const float* p0, const float* p1, const float* p2, float u, float v);
+static int any_hit_shader(const dcrt_flat_scene* sc, uint32_t tri, uint32_t materialOverride, float u, float v,
+                          float opacitySample)
+{
+    const uint32_t mid = materialOverride != DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE ? materialOverride : sc->material_ids[tri];
+    const dcrt_material* m = &sc->materials[mid];
+    float opacity = m->opacity;
+    if (m->opacity_texture_index != -1) {
+        f2 tc = bary2(sc->vertices[sc->triangles[tri * 3]].texcoord, sc->vertices[sc->triangles[tri * 3 + 1]].texcoord,
+                      sc->vertices[sc->triangles[tri * 3 + 2]].texcoord, u, v);
+        tc.x = tc.x * m->tex_tiling[0];
+        tc.y = tc.y * m->tex_tiling[1];
+        float rgba[4];
+        sample_texture_wrap(&sc->textures[m->opacity_texture_index], tc.x, tc.y, rgba);
+        opacity = opacity * rgba[0];
+    }
+    return opacitySample < opacity;
+}
+
 /* TextureCube<float3>.SampleLevel(clamp, dir, 0): D3D face selection, bilinear within the face */
 static v3 sample_env_cube(const dcrt_flat_scene* sc, v3 d)
 {
@@ -1520,6 +1550,12 @@ static void trace_path(const dcrt_flat_scene* sc, const dcrt_frame_params* f, in
     generate_ray(filmSample, apertureSample, f, &origin, &direction);
     const uint32_t features = f->features;
     const int lightVisible = (features & DCRT_FEATURE_LIGHT_VISIBLE) != 0;
+    /* ALLOW_ANYHIT_SHADER: one opacity sample per cast ray. Wavefront: NEW_PATH :223-226,
+     * then MATERIAL :422-430 (extension, then shadow, after the BSDF sample). Megakernel:
+     * drawn inside IntersectScene / IsOcculuded (MegakernelPathTracing.hlsl:27-28, 57-58),
+     * i.e. the shadow ray's before the BSDF sample. The first ray's is the same in both. */
+    const int anyHitOn = (features & DCRT_FEATURE_ALLOW_ANYHIT) != 0;
+    float extOpacity = anyHitOn ? next1d(s) : 0.0f, shadowOpacity = 0.0f;
     v3 T = V3(1.0f, 1.0f, 1.0f), Li = V3(0.0f, 0.0f, 0.0f);
     float bsdfPdfPrev = 0.0f;
     int isDeltaPrev = 1;
@@ -1529,7 +1565,7 @@ static void trace_path(const dcrt_flat_scene* sc, const dcrt_frame_params* f, in
         /* EXTENSION_RAY_CAST :84-120 */
         hit_info h; memset(&h, 0, sizeof(h));
         if (cnt) cnt->extension_rays++;
-        int hasHit = bvh_intersect(sc, ro, rd, 0.0f, o_inf(), 0, features, &h,
+        int hasHit = bvh_intersect(sc, ro, rd, 0.0f, o_inf(), 0, features, extOpacity, &h,
                                    cnt ? &cnt->node_visits : NULL, cnt ? &cnt->triangle_tests : NULL, cnt ? &cnt->blas_entries : NULL);
         float hitT = hasHit ? h.t : o_inf();
         /* MATERIAL :302-479 */
@@ -1580,6 +1616,7 @@ static void trace_path(const dcrt_flat_scene* sc, const dcrt_frame_params* f, in
                     so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
                     sdist = ls.distance;
                     hasShadowRay = 1;
+                    if (anyHitOn && mode == ORACLE_MODE_MEGAKERNEL) shadowOpacity = next1d(s);
                 }
             }
             float bsdfPdf = 0.0f; int isDeltaB = 0;
@@ -1604,12 +1641,16 @@ static void trace_path(const dcrt_flat_scene* sc, const dcrt_frame_params* f, in
             }
             bsdfPdfPrev = bsdfPdf;
             isDeltaPrev = isDeltaB;
+            if (anyHitOn) {
+                if (!terminate) extOpacity = next1d(s);
+                if (hasShadowRay && mode != ORACLE_MODE_MEGAKERNEL) shadowOpacity = next1d(s);
+            }
         }
         /* SHADOW_RAY_CAST :141-172 */
         int shadowHit = 0;
         if (hasShadowRay) {
             if (cnt) cnt->shadow_rays++;
-            shadowHit = bvh_intersect(sc, so, sd, 0.0f, sdist, 1, features, &h,
+            shadowHit = bvh_intersect(sc, so, sd, 0.0f, sdist, 1, features, shadowOpacity, &h,
                                       cnt ? &cnt->shadow_node_visits : NULL, cnt ? &cnt->shadow_triangle_tests : NULL,
                                       cnt ? &cnt->shadow_blas_entries : NULL);
         }
@@ -1710,7 +1751,7 @@ void oracle_trace_rays(const dcrt_flat_scene* sc, const dcrt_ray* rays, uint32_t
 {
     for (uint32_t i = 0; i < count; ++i) {
         hit_info h; memset(&h, 0, sizeof(h));
-        int hasHit = bvh_intersect(sc, vload(rays[i].origin), vload(rays[i].direction), 0.0f, o_inf(), 0, features, &h,
+        int hasHit = bvh_intersect(sc, vload(rays[i].origin), vload(rays[i].direction), 0.0f, o_inf(), 0, features & ~DCRT_FEATURE_ALLOW_ANYHIT, 0.0f, &h,
                                    cnt ? &cnt->node_visits : NULL, cnt ? &cnt->triangle_tests : NULL, cnt ? &cnt->blas_entries : NULL);
         if (cnt) cnt->extension_rays++;
         /* WavefrontPathTracing.hlsl:113-117; miss fields are defined as zero here (A.5) */
@@ -1726,7 +1767,7 @@ void oracle_occluded(const dcrt_flat_scene* sc, const dcrt_ray* rays, uint32_t c
 {
     for (uint32_t i = 0; i < count; ++i) {
         hit_info h;
-        occ[i] = (uint32_t)bvh_intersect(sc, vload(rays[i].origin), vload(rays[i].direction), 0.0f, rays[i].t_max, 1, features, &h,
+        occ[i] = (uint32_t)bvh_intersect(sc, vload(rays[i].origin), vload(rays[i].direction), 0.0f, rays[i].t_max, 1, features & ~DCRT_FEATURE_ALLOW_ANYHIT, 0.0f, &h,
                                          cnt ? &cnt->shadow_node_visits : NULL, cnt ? &cnt->shadow_triangle_tests : NULL,
                                          cnt ? &cnt->shadow_blas_entries : NULL);
         if (cnt) cnt->shadow_rays++;

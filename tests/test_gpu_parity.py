@@ -298,3 +298,45 @@ def test_megakernel_matches_oracle_megakernel(native_lib, golden_luts, oracle_mo
             assert bad == 0, f"{scene_name} seed {seed}: {bad} pixels differ"
     finally:
         t.destroy()
+
+
+# ---- ALLOW_ANYHIT_SHADER ------------------------------------------------------------------
+def _anyhit_scenes():
+    from directcomputeraytracing_amd import FEATURE_ALLOW_ANYHIT
+    from test_oracle import anyhit_scene
+    s = anyhit_scene()
+    s.features = s.features | FEATURE_ALLOW_ANYHIT
+    c = cornell(48, 40, 6)
+    c.features = c.features | FEATURE_ALLOW_ANYHIT
+    c.set_material_opacity(3, 0.5, -1)          # short box: per-triangle material ids, no override
+    c.set_material_opacity(4, 0.25, -1)
+    return {"mask_xml": s, "cornell_translucent": c}
+
+
+@pytest.mark.parametrize("name", ["mask_xml", "cornell_translucent"])
+def test_anyhit_wavefront_bit_exact(gpu_tracer, golden_luts, oracle_mod, name):
+    """Opacity samples drawn by NEW_PATH / MATERIAL (:223-226, :422-430), the AnyHitShader
+    with float and bitmap opacity, OBJ material ids and rectangle instance overrides."""
+    s = _anyhit_scenes()[name]
+    list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 5]))
+
+
+@pytest.mark.parametrize("name", ["mask_xml", "cornell_translucent"])
+def test_anyhit_megakernel_bit_exact(native_lib, golden_luts, oracle_mod, name):
+    """MegakernelPathTracing.hlsl draws the opacity samples inside IntersectScene/IsOcculuded."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    s = _anyhit_scenes()[name]
+    t = WavefrontPathTracer(path_pool_size=1 << 15, debug_rng=True)
+    try:
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        t.set_mode("megakernel")
+        t.clear_film()
+        t.render_images(2, 1)
+        pos, val = t.read_samples()
+        p_ref, v_ref, r_ref, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(2), oracle_mod.MEGAKERNEL, rng=True)
+        assert np.array_equal(t.read_rng(), r_ref)
+        assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
+        assert same_bits(val, v_ref).all()
+    finally:
+        t.destroy()

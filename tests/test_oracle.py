@@ -403,3 +403,77 @@ def test_bmp_writer_roundtrip(tmp_path):
     save_bmp(tmp_path / "x.bmp", img)
     back = np.asarray(Image.open(tmp_path / "x.bmp").convert("RGB"))
     assert np.array_equal(back, img[..., :3])
+
+
+# ---- ALLOW_ANYHIT_SHADER (HitShader.inc.hlsl:86-113, BVHAccel.inc.hlsl:182-190) ------------
+def anyhit_scene():
+    from directcomputeraytracing_amd import Scene
+    s = Scene((8, 8))
+    s.load_from_file(GOLDEN / "anyhit" / "anyhit.xml")
+    return s
+
+
+def test_anyhit_fixture_is_reproducible(tmp_path):
+    from directcomputeraytracing_amd import scenes
+    scenes.write_anyhit(tmp_path)
+    for f in (GOLDEN / "anyhit").iterdir():
+        assert (tmp_path / f.name).read_bytes() == f.read_bytes(), f.name
+
+
+def test_anyhit_mask_translation_and_instance_flags():
+    """mask BSDF: float opacity, or a bitmap with opacity bypassed to 1 (SceneXMLLoading.cpp:
+    748-767); instances are OPAQUE iff their material(s) are (Scene.cpp:57-80, 785-800)."""
+    s = anyhit_scene()
+    a = s.arrays()
+    mats = a["materials"]
+    opacity = mats[:, 10].view(np.float32)
+    otex = mats[:, 12].view(np.int32)
+    assert s.flat().texture_count == 2
+    leaf = int(np.flatnonzero(otex == 1)[0])           # the second texture (first is the floor albedo)
+    assert opacity[leaf] == 1.0
+    veil = int(np.flatnonzero(np.isclose(opacity, 0.4))[0])
+    assert otex[veil] == -1
+    flags = a["instance_flags"]
+    assert flags.shape[0] == 5
+    assert int(np.count_nonzero(flags & 1)) == 3       # floor, wall, light opaque; leaf, veil not
+    # editing a material updates the flags
+    s.set_material_opacity(veil, 1.0, -1)
+    assert int(np.count_nonzero(s.arrays()["instance_flags"] & 1)) == 4
+    s.set_material_opacity(leaf, 1.0, -1)
+    assert int(np.count_nonzero(s.arrays()["instance_flags"] & 1)) == 5
+    from directcomputeraytracing_amd import DCRTError
+    with pytest.raises(DCRTError):
+        s.set_material_opacity(leaf, 0.5, 7)
+
+
+def test_scene_feature_toggles():
+    from directcomputeraytracing_amd import FEATURE_ALLOW_ANYHIT, FEATURE_DEFAULT, DCRTError
+    s = anyhit_scene()
+    assert s.features == FEATURE_DEFAULT
+    s.features = FEATURE_DEFAULT | FEATURE_ALLOW_ANYHIT
+    assert s.frame_params(0).features == FEATURE_DEFAULT | FEATURE_ALLOW_ANYHIT
+    with pytest.raises(DCRTError):
+        s.features = 0x100
+
+
+def test_anyhit_oracle_semantics(oracle_mod, golden_luts):
+    """Any-hit on: masked geometry lets rays through (fewer ext hits on it, extra RNG draws);
+    all-opaque materials make the any-hit variant hit exactly what the default variant hits."""
+    from directcomputeraytracing_amd import FEATURE_ALLOW_ANYHIT
+    s = anyhit_scene()
+    fr = s.frame_params(3)
+    off = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rng=True, threads=4)
+    fr.features |= FEATURE_ALLOW_ANYHIT
+    on = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rng=True, threads=4)
+    assert not np.array_equal(off[2], on[2])
+    assert on[3]["triangle_tests"] > off[3]["triangle_tests"]    # rejected hits keep traversing
+    v = np.nan_to_num(on[1][..., :3])
+    assert np.isfinite(v).all() and v.mean() > 0
+    # camera rays: identical pixel samples (the opacity draw comes after the aperture sample)
+    assert np.array_equal(off[0], on[0])
+    # primary visibility through a fully transparent leaf equals the leaf removed from view
+    a = s.arrays()
+    leaf = int(np.flatnonzero(a["materials"][:, 12].view(np.int32) == 1)[0])
+    s.set_material_opacity(leaf, 0.0, -1)
+    gone = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rng=True, threads=4)
+    assert not np.array_equal(gone[1], on[1])
