@@ -5,11 +5,16 @@
 // at the median with MSVC's nth_element (a stable insertion sort for ranges of
 // at most 32 elements), std::partition with the two-ended bidirectional scheme.
 // With maxPrim = 2 (BLAS) / 1 (TLAS) every leaf holds exactly one primitive
-// (SURVEY.md §8 a28).
+// (SURVEY.md §8 a28). Large builds split their top levels across threads and splice
+// the subtrees back in depth-first order: the output is bit-identical to the
+// single-threaded reference build (parity mode).
 #include "bvh_accel.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <exception>
 #include <stack>
+#include <thread>
 
 namespace dcrt {
 namespace bvh {
@@ -73,123 +78,145 @@ PrimInfo* PartitionByBucket(PrimInfo* first, PrimInfo* last, uint32_t split)
     }
 }
 
-// BVHAccel.cpp:120-415 (BuildNodes). `primitives` / `reorderedPrimitives` are the
-// index triples of a BLAS (nullptr for the TLAS).
-void BuildNodes(std::vector<PrimInfo>& infos, const uint32_t* primitives, NodeInfo root, uint32_t maxPrim,
-                uint32_t* reorderedPrimitives, uint32_t* reorderedPrimitiveIndices, uint32_t* leafDepths,
-                BuildResult* out)
+// The build's fixed inputs and outputs, shared by all subtree builders.
+struct BuildContext {
+    std::vector<PrimInfo>& infos;
+    const uint32_t* primitives;            // index triples of a BLAS (nullptr for the TLAS)
+    uint32_t maxPrim;
+    uint32_t* reorderedPrimitives;
+    uint32_t* reorderedPrimitiveIndices;
+    uint32_t* leafDepths;
+};
+
+// A subtree's nodes in depth-first order with subtree-local child indices.
+struct Subtree {
+    std::vector<Node> nodes;
+    uint32_t maxDepth = 0;
+    uint32_t maxStackSize = 0;
+};
+
+// Leaves are emitted left to right over the primitive ranges, so a leaf's first
+// reordered slot is its range begin: subtrees write disjoint slots.
+void EmitLeaf(const BuildContext& c, Node* node, const NodeInfo& info, uint32_t count)
+{
+    for (uint32_t i = 0; i < count; ++i) {
+        const uint32_t prim = c.infos[info.primBegin + i].primIndex;
+        const uint32_t slot = info.primBegin + i;
+        if (c.primitives) {
+            c.reorderedPrimitives[slot * 3 + 0] = c.primitives[prim * 3 + 0];
+            c.reorderedPrimitives[slot * 3 + 1] = c.primitives[prim * 3 + 1];
+            c.reorderedPrimitives[slot * 3 + 2] = c.primitives[prim * 3 + 2];
+        }
+        c.reorderedPrimitiveIndices[slot] = prim;
+    }
+    node->childOrPrimIndex = info.primBegin;
+    node->primCountOrInstance = count;
+    node->isLeaf = true;
+    if (c.leafDepths) c.leafDepths[info.primBegin] = info.depth;
+}
+
+// One node of BVHAccel.cpp:120-415 (BuildNodes): bounds, split axis, SAH or median
+// split, or a leaf. Returns true (and the split point) when the node is interior.
+bool ProcessNode(const BuildContext& c, const NodeInfo& cur, Node* node, uint32_t* primMiddle)
+{
+    std::vector<PrimInfo>& infos = c.infos;
+    node->primCountOrInstance = 0;
+    node->isLeaf = false;
+    node->box = infos[cur.primBegin].box;
+    for (uint32_t i = cur.primBegin + 1; i < cur.primEnd; ++i) node->box = BoxMerged(node->box, infos[i].box);
+
+    const uint32_t count = cur.primEnd - cur.primBegin;
+    *primMiddle = (cur.primBegin + cur.primEnd) / 2;
+    if (count == 1) {
+        EmitLeaf(c, node, cur, 1);
+        return false;
+    }
+    Float3 cmin = infos[cur.primBegin].box.center, cmax = cmin;
+    for (uint32_t i = cur.primBegin + 1; i < cur.primEnd; ++i) {
+        cmax = VMax(cmax, infos[i].box.center);
+        cmin = VMin(cmin, infos[i].box.center);
+    }
+    const BoundingBox centroidBox = BoxFromPoints(cmin, cmax);
+    int axis = 0;
+    {
+        float mx = centroidBox.extents.x;
+        if (centroidBox.extents.y > mx) { mx = centroidBox.extents.y; axis = 1; }
+        if (centroidBox.extents.z > mx) axis = 2;
+    }
+    node->splitAxis = (uint8_t)axis;
+    const float nodeArea = SurfaceArea(node->box);
+    if (nodeArea == 0.0f || centroidBox.extents[axis] == 0.0f) {
+        if (count < c.maxPrim) {
+            EmitLeaf(c, node, cur, count);
+            return false;
+        }
+        return true;   // split at the middle without sorting (BVHAccel.cpp:264-273)
+    }
+    if (count <= 4) {
+        InsertionSortByCenter(&infos[cur.primBegin], &infos[cur.primBegin] + count, axis);
+        return true;
+    }
+    constexpr uint32_t kBuckets = 12;
+    struct Bucket { uint32_t count = 0; BoundingBox box{ { 0, 0, 0 }, { 0, 0, 0 } }; };
+    Bucket buckets[kBuckets];
+    for (uint32_t i = cur.primBegin; i < cur.primEnd; ++i) {
+        const float mn = centroidBox.center[axis] - centroidBox.extents[axis];
+        const float size = centroidBox.extents[axis] * 2.0f;
+        const float f = (float)kBuckets * (infos[i].box.center[axis] - mn) / size;
+        uint32_t n = f > 0.0f ? (uint32_t)f : 0u;
+        if (n >= kBuckets) n = kBuckets - 1;
+        infos[i].bucketIndex = n;
+        if (buckets[n].count == 0) buckets[n].box = infos[i].box;
+        else buckets[n].box = BoxMerged(buckets[n].box, infos[i].box);
+        buckets[n].count++;
+    }
+    float cost[kBuckets - 1];
+    for (uint32_t i = 0; i < kBuckets - 1; ++i) {
+        uint32_t c0 = 0, c1 = 0;
+        BoundingBox b0, b1;
+        bool init0 = false, init1 = false;
+        for (uint32_t j = 0; j <= i; ++j) {
+            if (!buckets[j].count) continue;
+            b0 = init0 ? BoxMerged(b0, buckets[j].box) : buckets[j].box;
+            init0 = true;
+            c0 += buckets[j].count;
+        }
+        for (uint32_t j = i + 1; j < kBuckets; ++j) {
+            if (!buckets[j].count) continue;
+            b1 = init1 ? BoxMerged(b1, buckets[j].box) : buckets[j].box;
+            init1 = true;
+            c1 += buckets[j].count;
+        }
+        cost[i] = 0.125f + ((float)c0 * SurfaceArea(b0) + (float)c1 * SurfaceArea(b1)) / nodeArea;
+    }
+    uint32_t minIndex = 0;
+    for (uint32_t i = 1; i < kBuckets - 1; ++i)
+        if (cost[i] < cost[minIndex]) minIndex = i;
+    const float minCost = cost[minIndex];
+    if (count > c.maxPrim || minCost < (float)count) {
+        PrimInfo* base = infos.data();
+        PrimInfo* p = PartitionByBucket(base + cur.primBegin, base + cur.primEnd, minIndex);
+        *primMiddle = (uint32_t)(p - base);
+        return true;
+    }
+    EmitLeaf(c, node, cur, count);
+    return false;
+}
+
+// The reference's iterative depth-first loop over one subtree. `pending` = entries
+// the reference's traversal-order stack already holds when it reaches this subtree's
+// root (right siblings of left-side ancestors), so maxStackSize comes out the same.
+void BuildSequential(const BuildContext& c, NodeInfo cur, uint32_t pending, Subtree* out)
 {
     std::vector<Node>& nodes = out->nodes;
     std::stack<NodeInfo> stack;
-    uint32_t reorderedCount = 0;
-
-    auto emitLeaf = [&](Node& node, const NodeInfo& info, uint32_t count) {
-        for (uint32_t i = 0; i < count; ++i) {
-            const uint32_t prim = infos[info.primBegin + i].primIndex;
-            if (primitives) {
-                reorderedPrimitives[(reorderedCount + i) * 3 + 0] = primitives[prim * 3 + 0];
-                reorderedPrimitives[(reorderedCount + i) * 3 + 1] = primitives[prim * 3 + 1];
-                reorderedPrimitives[(reorderedCount + i) * 3 + 2] = primitives[prim * 3 + 2];
-            }
-            reorderedPrimitiveIndices[reorderedCount + i] = prim;
-        }
-        node.childOrPrimIndex = reorderedCount;
-        node.primCountOrInstance = count;
-        node.isLeaf = true;
-        reorderedCount += count;
-        if (leafDepths) leafDepths[node.childOrPrimIndex] = info.depth;
-    };
-
-    NodeInfo cur = root;
+    cur.parentIndex = -1;
     for (;;) {
         const uint32_t nodeIndex = (uint32_t)nodes.size();
         if (cur.parentIndex != -1) nodes[(size_t)cur.parentIndex].childOrPrimIndex = nodeIndex;
         nodes.emplace_back();
-        Node* node = &nodes.back();
-        node->primCountOrInstance = 0;
-        node->isLeaf = false;
-
-        node->box = infos[cur.primBegin].box;
-        for (uint32_t i = cur.primBegin + 1; i < cur.primEnd; ++i) node->box = BoxMerged(node->box, infos[i].box);
-
-        const uint32_t count = cur.primEnd - cur.primBegin;
-        bool descend = true;
-        uint32_t primMiddle = (cur.primBegin + cur.primEnd) / 2;
-        if (count == 1) {
-            emitLeaf(*node, cur, 1);
-            descend = false;
-        } else {
-            Float3 cmin = infos[cur.primBegin].box.center, cmax = cmin;
-            for (uint32_t i = cur.primBegin + 1; i < cur.primEnd; ++i) {
-                cmax = VMax(cmax, infos[i].box.center);
-                cmin = VMin(cmin, infos[i].box.center);
-            }
-            const BoundingBox centroidBox = BoxFromPoints(cmin, cmax);
-            int axis = 0;
-            {
-                float mx = centroidBox.extents.x;
-                if (centroidBox.extents.y > mx) { mx = centroidBox.extents.y; axis = 1; }
-                if (centroidBox.extents.z > mx) axis = 2;
-            }
-            node->splitAxis = (uint8_t)axis;
-            const float nodeArea = SurfaceArea(node->box);
-            if (nodeArea == 0.0f || centroidBox.extents[axis] == 0.0f) {
-                if (count < maxPrim) {
-                    emitLeaf(*node, cur, count);
-                    descend = false;
-                }
-                // else: split at the middle without sorting (BVHAccel.cpp:264-273)
-            } else if (count <= 4) {
-                InsertionSortByCenter(&infos[cur.primBegin], &infos[cur.primBegin] + count, axis);
-            } else {
-                constexpr uint32_t kBuckets = 12;
-                struct Bucket { uint32_t count = 0; BoundingBox box{ { 0, 0, 0 }, { 0, 0, 0 } }; };
-                Bucket buckets[kBuckets];
-                for (uint32_t i = cur.primBegin; i < cur.primEnd; ++i) {
-                    const float mn = centroidBox.center[axis] - centroidBox.extents[axis];
-                    const float size = centroidBox.extents[axis] * 2.0f;
-                    const float f = (float)kBuckets * (infos[i].box.center[axis] - mn) / size;
-                    uint32_t n = f > 0.0f ? (uint32_t)f : 0u;
-                    if (n >= kBuckets) n = kBuckets - 1;
-                    infos[i].bucketIndex = n;
-                    if (buckets[n].count == 0) buckets[n].box = infos[i].box;
-                    else buckets[n].box = BoxMerged(buckets[n].box, infos[i].box);
-                    buckets[n].count++;
-                }
-                float cost[kBuckets - 1];
-                for (uint32_t i = 0; i < kBuckets - 1; ++i) {
-                    uint32_t c0 = 0, c1 = 0;
-                    BoundingBox b0, b1;
-                    bool init0 = false, init1 = false;
-                    for (uint32_t j = 0; j <= i; ++j) {
-                        if (!buckets[j].count) continue;
-                        b0 = init0 ? BoxMerged(b0, buckets[j].box) : buckets[j].box;
-                        init0 = true;
-                        c0 += buckets[j].count;
-                    }
-                    for (uint32_t j = i + 1; j < kBuckets; ++j) {
-                        if (!buckets[j].count) continue;
-                        b1 = init1 ? BoxMerged(b1, buckets[j].box) : buckets[j].box;
-                        init1 = true;
-                        c1 += buckets[j].count;
-                    }
-                    cost[i] = 0.125f + ((float)c0 * SurfaceArea(b0) + (float)c1 * SurfaceArea(b1)) / nodeArea;
-                }
-                uint32_t minIndex = 0;
-                for (uint32_t i = 1; i < kBuckets - 1; ++i)
-                    if (cost[i] < cost[minIndex]) minIndex = i;
-                const float minCost = cost[minIndex];
-                if (count > maxPrim || minCost < (float)count) {
-                    PrimInfo* base = infos.data();
-                    PrimInfo* p = PartitionByBucket(base + cur.primBegin, base + cur.primEnd, minIndex);
-                    primMiddle = (uint32_t)(p - base);
-                } else {
-                    emitLeaf(*node, cur, count);
-                    descend = false;
-                }
-            }
-        }
-        if (!descend) {
+        uint32_t primMiddle = 0;
+        if (!ProcessNode(c, cur, &nodes.back(), &primMiddle)) {
             if (stack.empty()) break;
             cur = stack.top();
             stack.pop();
@@ -200,8 +227,82 @@ void BuildNodes(std::vector<PrimInfo>& infos, const uint32_t* primitives, NodeIn
         cur.parentIndex = -1;
         cur.primEnd = primMiddle;
         out->maxDepth = std::max(out->maxDepth, cur.depth);
-        out->maxStackSize = std::max(out->maxStackSize, (uint32_t)stack.size());
+        out->maxStackSize = std::max(out->maxStackSize, pending + (uint32_t)stack.size());
     }
+}
+
+// Parallel parity build: the top `budget` levels split on the calling thread and
+// hand the right subtree to a new thread; subtrees are spliced in depth-first order
+// (node, left subtree, right subtree), which is exactly the sequential node order.
+// Every node's own arithmetic stays sequential, so the result is bit-identical.
+constexpr uint32_t kParallelMinPrims = 8192;
+
+void BuildParallel(const BuildContext& c, NodeInfo cur, uint32_t pending, int budget, Subtree* out)
+{
+    if (budget <= 0 || cur.primEnd - cur.primBegin < kParallelMinPrims) {
+        BuildSequential(c, cur, pending, out);
+        return;
+    }
+    Node node;
+    uint32_t primMiddle = 0;
+    if (!ProcessNode(c, cur, &node, &primMiddle)) {
+        out->nodes.push_back(node);
+        return;
+    }
+    const uint32_t depth = cur.depth + 1;
+    Subtree left, right;
+    std::exception_ptr error;
+    std::thread worker([&] {
+        try {
+            BuildParallel(c, { -1, primMiddle, cur.primEnd, depth }, pending, budget - 1, &right);
+        } catch (...) {
+            error = std::current_exception();
+        }
+    });
+    try {
+        BuildParallel(c, { -1, cur.primBegin, primMiddle, depth }, pending + 1, budget - 1, &left);
+    } catch (...) {
+        worker.join();
+        throw;
+    }
+    worker.join();
+    if (error) std::rethrow_exception(error);
+    out->maxDepth = std::max({ depth, left.maxDepth, right.maxDepth });
+    out->maxStackSize = std::max({ pending + 1, left.maxStackSize, right.maxStackSize });
+    const uint32_t leftCount = (uint32_t)left.nodes.size();
+    node.childOrPrimIndex = 1 + leftCount;
+    out->nodes.reserve(1 + left.nodes.size() + right.nodes.size());
+    out->nodes.push_back(node);
+    for (Node n : left.nodes) {
+        if (!n.isLeaf) n.childOrPrimIndex += 1;
+        out->nodes.push_back(n);
+    }
+    for (Node n : right.nodes) {
+        if (!n.isLeaf) n.childOrPrimIndex += 1 + leftCount;
+        out->nodes.push_back(n);
+    }
+}
+
+int BuildThreadBudget()
+{
+    unsigned threads = std::thread::hardware_concurrency();
+    if (const char* e = std::getenv("DCRT_BUILD_THREADS")) threads = (unsigned)std::max(1, std::atoi(e));
+    threads = std::min(threads ? threads : 1u, 16u);
+    int budget = 0;
+    while ((1u << budget) < threads) ++budget;
+    return budget;
+}
+
+void BuildNodes(std::vector<PrimInfo>& infos, const uint32_t* primitives, NodeInfo root, uint32_t maxPrim,
+                uint32_t* reorderedPrimitives, uint32_t* reorderedPrimitiveIndices, uint32_t* leafDepths,
+                BuildResult* out)
+{
+    const BuildContext c{ infos, primitives, maxPrim, reorderedPrimitives, reorderedPrimitiveIndices, leafDepths };
+    Subtree tree;
+    BuildParallel(c, root, 0, BuildThreadBudget(), &tree);
+    out->nodes = std::move(tree.nodes);
+    out->maxDepth = tree.maxDepth;
+    out->maxStackSize = tree.maxStackSize;
 }
 
 }  // namespace

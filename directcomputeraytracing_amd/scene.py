@@ -166,3 +166,30 @@ class Scene:
             "tlas_node_count": f.tlas_node_count,
             "stack_size": f.bvh_traversal_stack_size,
         }
+
+
+def build_blas(vertices: np.ndarray, indices: np.ndarray) -> dict:
+    """BVHAccel::BuildBLAS + PackBVH (BVHAccel.cpp:376-447) over one triangle mesh.
+
+    ``vertices`` is an (N, 11) float32 array in the ``dcrt_vertex`` layout (or (N, 3)
+    positions), ``indices`` (T, 3) uint32. Returns the packed nodes, the BVH-ordered
+    index triples and the new->old triangle map, with the tree's depth and stack size."""
+    lib = _abi.load_library()
+    v = np.ascontiguousarray(vertices, np.float32)
+    if v.ndim == 2 and v.shape[1] == 3:
+        full = np.zeros((v.shape[0], 11), np.float32)
+        full[:, :3] = v
+        v = full
+    idx = np.ascontiguousarray(indices, np.uint32).reshape(-1)
+    n = idx.size // 3
+    nodes = np.zeros((max(1, 2 * n), 8), np.uint32)
+    reordered = np.zeros(idx.size, np.uint32)
+    tri_map = np.zeros(n, np.uint32)
+    count, depth, stack = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    check(lib.dcrt_bvh_build_blas(v.ctypes.data_as(C.POINTER(_abi.Vertex)), idx.ctypes.data_as(C.POINTER(C.c_uint32)), n,
+                                  nodes.ctypes.data_as(C.POINTER(_abi.BVHNode)), C.byref(count),
+                                  reordered.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                  tri_map.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(depth), C.byref(stack)),
+          "BuildBLAS")
+    return {"nodes": nodes[:count.value], "indices": reordered.reshape(-1, 3), "triangles": tri_map,
+            "max_depth": depth.value, "max_stack_size": stack.value}

@@ -477,3 +477,53 @@ def test_anyhit_oracle_semantics(oracle_mod, golden_luts):
     s.set_material_opacity(leaf, 0.0, -1)
     gone = oracle_mod.render(s.flat(), golden_luts, fr, oracle_mod.WAVEFRONT, rng=True, threads=4)
     assert not np.array_equal(gone[1], on[1])
+
+
+# ---- BVH build (BVHAccel.cpp:76-447): parallel parity build == single-threaded ----------------
+def _random_mesh(n, seed=1):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-10, 10, (n, 1, 3))
+    p = (c + rng.normal(0, 0.05, (n, 3, 3))).reshape(-1, 3).astype(np.float32)
+    return p, np.arange(3 * n, dtype=np.uint32).reshape(-1, 3)
+
+
+def _bvh_digest(r):
+    import hashlib
+    return hashlib.sha1(r["nodes"].tobytes() + r["indices"].tobytes() + r["triangles"].tobytes()).hexdigest()[:16]
+
+
+def test_bvh_parallel_build_is_bit_identical(monkeypatch):
+    """f4: the threaded build splices subtrees in depth-first order; node order, boxes,
+    leaf ranges, depth and stack size equal the single-threaded reference order. The digest
+    pins the single-threaded output recorded before the threaded builder existed."""
+    from directcomputeraytracing_amd.scene import build_blas
+    p, idx = _random_mesh(100_000)
+    out = {}
+    for threads in ("1", "3", "8", "16"):
+        monkeypatch.setenv("DCRT_BUILD_THREADS", threads)
+        r = build_blas(p, idx)
+        out[threads] = (_bvh_digest(r), r["max_depth"], r["max_stack_size"], r["nodes"].shape[0])
+    assert len(set(out.values())) == 1, out
+    assert out["1"] == ("1d747587bfd760c9", 20, 17, 199_999)
+
+
+def test_bvh_structure_invariants():
+    from directcomputeraytracing_amd.scene import build_blas
+    p, idx = _random_mesh(20_000, seed=3)
+    r = build_blas(p, idx)
+    nodes = r["nodes"]
+    bmin = nodes[:, 0:3].view(np.float32)
+    bmax = nodes[:, 3:6].view(np.float32)
+    right, misc = nodes[:, 6], nodes[:, 7]
+    count = (misc >> 3) & 0x1FFFFFFF
+    leaf = count > 0
+    assert np.array_equal(np.sort(r["triangles"]), np.arange(20_000))       # every triangle once
+    assert np.all(count[leaf] == 1)                                          # maxPrim 2 -> single-triangle leaves
+    assert np.array_equal(np.sort(right[leaf]), np.arange(20_000))
+    inner = np.flatnonzero(~leaf)
+    for child in (inner + 1, right[inner]):                                 # children inside parents
+        assert np.all(bmin[child] >= bmin[inner] - 1e-5) and np.all(bmax[child] <= bmax[inner] + 1e-5)
+    tri = p[r["indices"].reshape(-1)].reshape(-1, 3, 3)
+    lf = np.flatnonzero(leaf)
+    t = tri[right[lf]]
+    assert np.all(t.min(1) >= bmin[lf] - 1e-5) and np.all(t.max(1) <= bmax[lf] + 1e-5)
