@@ -147,7 +147,8 @@ struct HitRecord {
 // lanes (persistent "while-while" with per-lane dynamic ray fetch), so a wave64
 // does not idle until its slowest ray is done.
 // The per-lane stack lives in LDS: column `lane` of a [stackSize][blockDim] array
-// (consecutive lanes on consecutive banks).
+// (consecutive lanes on consecutive banks); blockDim is a power of two and entry i of
+// a lane sits at lds[i << shift], shift = log2(blockDim) (a shift, not a 32-bit multiply).
 struct TraversalStats {
     uint32_t nodes;   // iterationCounter (BVHAccel.inc.hlsl:121)
     uint32_t tris;    // triangle tests
@@ -210,11 +211,11 @@ DEV bool any_hit_shader(const DeviceScene& sc, uint32_t tri, uint32_t ov, float 
 }
 
 // Pop the next node (BVHAccel.inc.hlsl stack pop); true when the stack is empty.
-DEV bool trav_pop(const DeviceScene& sc, TravState& s, const uint32_t* lds, uint32_t stride)
+DEV bool trav_pop(const DeviceScene& sc, TravState& s, const uint32_t* lds, uint32_t shift)
 {
     if (s.count == 0) return true;
     --s.count;
-    const uint32_t packed = s.count < sc.stackSize ? lds[s.count * stride] : 0u;
+    const uint32_t packed = s.count < sc.stackSize ? lds[s.count << shift] : 0u;
     const bool wasBlas = s.inBlas;
     s.node = packed & 0x7FFFFFFFu;
     s.inBlas = (packed & 0x80000000u) != 0;
@@ -236,7 +237,7 @@ DEV bool trav_pop(const DeviceScene& sc, TravState& s, const uint32_t* lds, uint
 // spare slot `stackSize` past the end, which nothing reads), the pop always loads
 // the top, and selects pick the outcome; the lanes of a wave stay convergent.
 template <bool INSTR>
-DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds, uint32_t stride, TraversalStats& st)
+DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
     const float4 a = sc.nodes[s.node * 2];
@@ -254,8 +255,8 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds
     const bool neg = f2b && ((axis == 0u && nx) | (axis == 1u && ny) | (axis == 2u && nz));
     const uint32_t nearChild = neg ? right : s.node + 1;
     const uint32_t farChild = neg ? s.node + 1 : right;
-    const uint32_t top = lds[(s.count > 0u ? min(s.count - 1u, sc.stackSize) : sc.stackSize) * stride];
-    lds[min(s.count, sc.stackSize) * stride] = (farChild & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
+    const uint32_t top = lds[(s.count > 0u ? min(s.count - 1u, sc.stackSize) : sc.stackSize) << shift];
+    lds[min(s.count, sc.stackSize) << shift] = (farChild & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
     const bool pop = !hit && s.count > 0u;
     const bool done = !hit && s.count == 0u;
     const bool popBlas = (top & 0x80000000u) != 0u;
@@ -276,7 +277,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds
 // Phase B: the parked leaf's work. TLAS leaf: move the ray into the instance and
 // continue at its BLAS root. BLAS leaf: test triangles [ref, ref + count), then pop.
 template <bool ANY_HIT, bool INSTR, bool OPACITY = false>
-DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t stride, TraversalStats& st)
+DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     s.parked = false;
     const uint32_t primOrInst = (s.leafMisc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
@@ -325,7 +326,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
             s.hit.inst = s.inst;
         }
     }
-    return trav_pop(sc, s, lds, stride);
+    return trav_pop(sc, s, lds, shift);
 }
 
 // ---- texture emulation ----------------------------------------------------------

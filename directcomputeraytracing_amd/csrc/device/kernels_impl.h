@@ -278,9 +278,18 @@ __global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScen
 // the next items of the wave's range (ballot + mbcnt, no atomics), so all 64
 // lanes keep traversing until the range is drained.
 
+// log2(blockDim.x): traversal kernels run power-of-two workgroups (tracer.hip)
+__device__ __forceinline__ uint32_t block_shift() { return 31u - (uint32_t)__clz((int)blockDim.x); }
+
+#ifndef DCRT_VISITS_PER_CHECK
+#define DCRT_VISITS_PER_CHECK 3
+#endif
+// node visits between two wave-level checks of the phase-A exit condition
+constexpr int kVisitsPerCheck = DCRT_VISITS_PER_CHECK;
+
 template <bool ANY_HIT, bool INSTR, bool OPACITY, typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
-                                                 uint32_t kParkLanes, uint32_t* lds, uint32_t stride, Fetch fetch, Emit emit,
+                                                 uint32_t kParkLanes, uint32_t* lds, uint32_t shift, Fetch fetch, Emit emit,
                                                  TraversalStats& st)
 {
     const bool watertight = (features & DCRT_FEATURE_WATERTIGHT) != 0;
@@ -310,9 +319,12 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         // phase A: node visits only, until enough lanes are parked at leaves (or
         // enough are idle to refill, or none can advance)
         for (;;) {
-            if (active && !s.parked && trav_visit<INSTR>(sc, s, f2b, lds, stride, st)) {
-                emit(item, s);
-                active = false;
+#pragma unroll
+            for (int k = 0; k < kVisitsPerCheck; ++k) {
+                if (active && !s.parked && trav_visit<INSTR>(sc, s, f2b, lds, shift, st)) {
+                    emit(item, s);
+                    active = false;
+                }
             }
             const unsigned long long runnable = __ballot(active && !s.parked);
             const uint32_t parked = (uint32_t)__popcll(__ballot(active && s.parked));
@@ -320,7 +332,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             if (runnable == 0ull || parked >= kParkLanes || (idle >= kRefillLanes && cursor < end)) break;
         }
         // phase B: the parked lanes' leaf work, shared by many lanes at once
-        if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY>(sc, s, watertight, lds, stride, st)) {
+        if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY>(sc, s, watertight, lds, shift, st)) {
             emit(item, s);
             active = false;
         }
@@ -344,7 +356,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
     qmap(cnt, kQExt, &qm);
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<false, INSTR, OPACITY>(
-        sc, qm.prefix[kShards], fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, blockDim.x,
+        sc, qm.prefix[kShards], fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const uint32_t path = qentry(pool.extQueue, pool.size, qm, i);
             const float4 o = pool.rayO[path], d = pool.rayD[path];
@@ -371,7 +383,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
     const uint32_t n = qm.prefix[kShards];
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<true, INSTR, OPACITY>(
-        sc, n, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, blockDim.x,
+        sc, n, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const uint32_t path = qentry(pool.shadowQueue, pool.size, qm, i);
             const float4 o = pool.shadowO[path], d = pool.shadowD[path];
@@ -406,15 +418,15 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
 // emission, exactly like the reference's two tracers.
 template <bool ANY_HIT, bool OPACITY>
 __device__ __forceinline__ bool trace_full(const DeviceScene& sc, V3 o, V3 d, float tMax, bool watertight, bool f2b,
-                                           float opacitySample, uint32_t* lds, uint32_t stride, HitRecord* hit)
+                                           float opacitySample, uint32_t* lds, uint32_t shift, HitRecord* hit)
 {
     TravState s;
     trav_init(s, o, d, 0.0f, tMax);
     s.opacitySample = opacitySample;
     TraversalStats st = {0u, 0u, 0u};
     for (;;) {
-        if (trav_visit<false>(sc, s, f2b, lds, stride, st)) break;
-        if (s.parked && trav_leaf<ANY_HIT, false, OPACITY>(sc, s, watertight, lds, stride, st)) break;
+        if (trav_visit<false>(sc, s, f2b, lds, shift, st)) break;
+        if (s.parked && trav_leaf<ANY_HIT, false, OPACITY>(sc, s, watertight, lds, shift, st)) break;
     }
     *hit = s.hit;
     return s.found;
@@ -435,7 +447,7 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
     const bool vndf = (fc.features & DCRT_FEATURE_GGX_SAMPLE_VNDF) != 0;
     const bool lightVisible = (fc.features & DCRT_FEATURE_LIGHT_VISIBLE) != 0;
     uint32_t* lds = stackMem + threadIdx.x;
-    const uint32_t stride = blockDim.x;
+    const uint32_t shift = block_shift();
     unsigned long long extRays = 0, shadowRays = 0;
     for (;;) {
         // every wave of the block claims one block per round (one atomic per workgroup)
@@ -467,7 +479,7 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
             ++extRays;
             // IntersectScene draws the ray's opacity sample (MegakernelPathTracing.hlsl:27-28)
             const float extOpacity = OPACITY ? next1(rng) : 0.0f;
-            const bool hasHit = trace_full<false, OPACITY>(sc, ro, rd, inf(), watertight, f2b, extOpacity, lds, stride, &hit);
+            const bool hasHit = trace_full<false, OPACITY>(sc, ro, rd, inf(), watertight, f2b, extOpacity, lds, shift, &hit);
             const float hitT = hasHit ? hit.t : inf();
             Intersection it;
             it.lightIndex = DCRT_LIGHT_INDEX_INVALID; it.triangleIndex = 0;
@@ -538,7 +550,7 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
             if (hasShadow) {
                 ++shadowRays;
                 HitRecord sh;
-                const bool occluded = trace_full<true, OPACITY>(sc, so, sd, sdist, watertight, f2b, shadowOpacity, lds, stride, &sh);
+                const bool occluded = trace_full<true, OPACITY>(sc, so, sd, sdist, watertight, f2b, shadowOpacity, lds, shift, &sh);
                 if (!occluded) L = L + lsr;
             }
             if (terminate) break;
@@ -560,7 +572,7 @@ __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const 
     extern __shared__ uint32_t stackMem[];
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<ANY, true, false>(
-        sc, n, features, 16u, 32u, stackMem + threadIdx.x, blockDim.x,
+        sc, n, features, 16u, 32u, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
             const dcrt_ray r = rays[i];
             trav_init(s, ld3(r.origin), ld3(r.direction), 0.0f, ANY ? r.t_max : inf());

@@ -1,8 +1,8 @@
 #!/bin/bash
-# A/B: bench each experimental library variant (experiments/*.so) on the GPU box.
+# A/B: bench each experimental library variant (gpu_ab/*.so) on the GPU box.
 set -u
 mkdir -p gpurun_out
-for lib in experiments/*.so; do
+for lib in gpu_ab/*.so; do
   n=$(basename $lib .so)
   DCRT_LIB=$lib timeout -k 10 200 python bench.py --steps 24 --warmup 2 --no-cpu-baseline --roofline-images 1 > gpurun_out/ab_$n.log 2>&1 || exit $?
   echo "$n $(python -c "import json;d=json.load(open('gpurun_out/ab_$n.log'));print(d['ms_per_spp'], d['roofline']['avg_launch_us'])")"
