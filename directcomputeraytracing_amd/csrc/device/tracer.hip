@@ -45,6 +45,14 @@ constexpr uint32_t kDefaultIterations = 8;
 constexpr uint32_t kControlBlock = 256;
 constexpr uint32_t kMaterialBlock = 256;
 constexpr uint32_t kMaxPersistentBlocks = 256 * 8;   // CUs x resident workgroups
+#ifndef DCRT_CONTROL_MAX_BLOCKS
+#define DCRT_CONTROL_MAX_BLOCKS 0xFFFFFFFFu
+#endif
+#ifndef DCRT_MATERIAL_MAX_BLOCKS
+#define DCRT_MATERIAL_MAX_BLOCKS 0xFFFFFFFFu
+#endif
+constexpr uint32_t kControlMaxBlocks = DCRT_CONTROL_MAX_BLOCKS;
+constexpr uint32_t kMaterialMaxBlocks = DCRT_MATERIAL_MAX_BLOCKS;
 
 template <typename T>
 int DeviceAlloc(T** p, size_t count, std::vector<void*>* owner)
@@ -544,8 +552,11 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
 {
     Counters* cnt = dCounters + par;
     Counters* next = dCounters + (par ^ 1u);
-    const uint32_t controlGrid = std::min<uint32_t>(poolSize / kControlBlock, kMaxPersistentBlocks);
-    const uint32_t materialGrid = std::min<uint32_t>((poolSize + kMaterialBlock - 1) / kMaterialBlock, kMaxPersistentBlocks);
+    // CONTROL and MATERIAL get one workgroup per 256 slots (their grid-stride loops then run
+    // once): the hardware dispatcher balances them, where a capped grid leaves a partial
+    // second round of workgroups (occupancy 7 and 3 waves/SIMD, not 8) as a tail.
+    const uint32_t controlGrid = std::min<uint32_t>(poolSize / kControlBlock, kControlMaxBlocks);
+    const uint32_t materialGrid = std::min<uint32_t>((poolSize + kMaterialBlock - 1) / kMaterialBlock, kMaterialMaxBlocks);
     const bool opacity = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) != 0;
     const uint32_t castGrid = CastGrid(castBlock, opacity);
     hipLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, pool, film, (const FrameConstants*)dFrame, cnt,
