@@ -184,9 +184,14 @@ def main():
     tracer.set_instrumentation(False, False)
     ext_bytes = (EXT_RAY_BYTES * cr["extension_rays"] + NODE_BYTES * st["ext_node_visits"]
                  + TRI_BYTES * st["ext_triangle_tests"] + BLAS_BYTES * st["ext_blas_entries"])
+    shadow_bytes = (SHADOW_RAY_BYTES * cr["shadow_rays"] + NODE_BYTES * st["shadow_node_visits"]
+                    + TRI_BYTES * st["shadow_triangle_tests"] + BLAS_BYTES * st["shadow_blas_entries"])
+    # the timed launch is the merged EXTENSION+SHADOW cast kernel unless DCRT_SPLIT_CASTS=1
+    merged = os.environ.get("DCRT_SPLIT_CASTS", "0") in ("", "0")
+    cast_bytes = ext_bytes + shadow_bytes if merged else ext_bytes
     launches = max(1, tm["ext_launches"])
     avg_ms = tm["ext_kernel_ms"] / launches
-    bytes_per_launch = ext_bytes / launches
+    bytes_per_launch = cast_bytes / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     traffic = None
     cands = sorted((ROOT / "profiles").glob("r*_pmc_traffic.json"))
@@ -216,14 +221,19 @@ def main():
                    "resolution": [args.width, args.height], "spp": images, "max_bounce": args.bounces,
                    "path_pool": args.pool, "parallelism": f"film stripes x{world}" if world > 1 else "single GPU",
                    "rays": int(rays)},
-        "roofline": {"bound": "hbm", "kernel": "extension_kernel (EXTENSION_RAY_CAST)",
+        "roofline": {"bound": "hbm",
+                     "kernel": "cast_kernel (EXTENSION_RAY_CAST + SHADOW_RAY_CAST, one launch)" if merged
+                               else "extension_kernel (EXTENSION_RAY_CAST)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 2),
                      "launches": int(launches),
-                     "per_ray": {"nodes": st["ext_node_visits"] / max(1, cr["extension_rays"]),
-                                 "tris": st["ext_triangle_tests"] / max(1, cr["extension_rays"]),
-                                 "blas": st["ext_blas_entries"] / max(1, cr["extension_rays"])}},
+                     "per_ext_ray": {"nodes": st["ext_node_visits"] / max(1, cr["extension_rays"]),
+                                     "tris": st["ext_triangle_tests"] / max(1, cr["extension_rays"]),
+                                     "blas": st["ext_blas_entries"] / max(1, cr["extension_rays"])},
+                     "per_shadow_ray": {"nodes": st["shadow_node_visits"] / max(1, cr["shadow_rays"]),
+                                        "tris": st["shadow_triangle_tests"] / max(1, cr["shadow_rays"]),
+                                        "blas": st["shadow_blas_entries"] / max(1, cr["shadow_rays"])}},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -162,6 +162,7 @@ struct TravState {
     uint32_t node, count, inst;
     uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked)
     bool inBlas, shearValid, found, parked, noZero;   // noZero: no component of o, d is +-0
+    bool anyHit;          // merged cast kernel: this lane's ray is a shadow ray (first hit ends it)
     Shear sh;
     HitRecord hit;
     // ALLOW_ANYHIT_SHADER only (dead, and removed by the compiler, otherwise)
@@ -177,7 +178,7 @@ DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax)
     s.tMin = tMin; s.tMax = tMax;
     s.node = 0; s.count = 0; s.inst = 0;
     s.leafRef = 0; s.leafMisc = 0;
-    s.inBlas = false; s.shearValid = false; s.found = false; s.parked = false;
+    s.inBlas = false; s.shearValid = false; s.found = false; s.parked = false; s.anyHit = false;
     s.noZero = o.x != 0.0f && o.y != 0.0f && o.z != 0.0f && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
     s.hit.t = 0.0f; s.hit.u = 0.0f; s.hit.v = 0.0f; s.hit.tri = 0u; s.hit.inst = 0u;
     s.opacitySample = 0.0f; s.matOverride = DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE; s.opaque = false;
@@ -276,7 +277,8 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds
 
 // Phase B: the parked leaf's work. TLAS leaf: move the ray into the instance and
 // continue at its BLAS root. BLAS leaf: test triangles [ref, ref + count), then pop.
-template <bool ANY_HIT, bool INSTR, bool OPACITY = false>
+// LANE_ANY: any-hit is a per-lane choice (s.anyHit), for the merged ray-cast kernel
+template <bool ANY_HIT, bool INSTR, bool OPACITY = false, bool LANE_ANY = false>
 DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     s.parked = false;
@@ -319,7 +321,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         if (OPACITY && h && !s.opaque) h = any_hit_shader(sc, p, s.matOverride, u, v, s.opacitySample);
         if (h) {
             s.found = true;
-            if (ANY_HIT) return true;
+            if (ANY_HIT || (LANE_ANY && s.anyHit)) return true;
             s.tMax = t;
             s.hit.t = t; s.hit.u = u; s.hit.v = v;
             s.hit.tri = (p & 0x7FFFFFFFu) | (bf ? 0x80000000u : 0u);

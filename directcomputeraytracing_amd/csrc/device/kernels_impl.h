@@ -286,30 +286,56 @@ __device__ __forceinline__ uint32_t block_shift() { return 31u - (uint32_t)__clz
 #endif
 // node visits between two wave-level checks of the phase-A exit condition
 constexpr int kVisitsPerCheck = DCRT_VISITS_PER_CHECK;
+#ifndef DCRT_INTERLEAVE
+#define DCRT_INTERLEAVE 64
+#endif
+// queue items per round-robin group of the cast kernels' static work split (power of two)
+constexpr uint32_t kInterleave = DCRT_INTERLEAVE;
 
-template <bool ANY_HIT, bool INSTR, bool OPACITY, typename Fetch, typename Emit>
+#ifdef DCRT_WAVE_TIMELINE
+// Diagnostic build only (tools/wave_timeline.py): per-wave start/end realtime stamps
+// and item counts of the cast kernels, 16 iteration slots x 8192 waves x 2 kernels.
+__device__ unsigned long long g_waveLog[2][16][8192][2];
+__device__ uint32_t g_waveItems[2][16][8192];
+#define DCRT_WAVE_TAG(g) ((int)((g)->iterations & 15ull))
+#else
+#define DCRT_WAVE_TAG(g) (-1)
+#endif
+
+template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
                                                  uint32_t kParkLanes, uint32_t* lds, uint32_t shift, Fetch fetch, Emit emit,
-                                                 TraversalStats& st)
+                                                 TraversalStats& st, int waveTag = -1)
 {
     const bool watertight = (features & DCRT_FEATURE_WATERTIGHT) != 0;
     const bool f2b = (features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
     const uint32_t wavesPerBlock = blockDim.x >> 6;
     const uint32_t waves = gridDim.x * wavesPerBlock;
     const uint32_t waveId = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
-    const uint32_t chunk = (n + waves - 1) / waves;
-    uint32_t cursor = min(waveId * chunk, n);
-    const uint32_t end = min(cursor + chunk, n);
+    // Work split: the queue is cut into groups of kInterleave consecutive items (one
+    // region of the image / one producer workgroup each) dealt round-robin to the
+    // waves, so every wave samples the whole queue and per-wave costs even out
+    // (contiguous ranges follow the image's cost structure and leave the slowest
+    // waves alone at the end). `cursor` and `end` count in the wave's own sequence.
+    const uint32_t groups = (n + kInterleave - 1) / kInterleave;
+    const uint32_t myGroups = groups > waveId ? (groups - waveId + waves - 1) / waves : 0u;
+    uint32_t cursor = 0;
+    const uint32_t end = myGroups * kInterleave;
+    const uint32_t chunk = end;   // (diagnostics)
     TravState s;
     bool active = false;
     uint32_t item = 0;
+#ifdef DCRT_WAVE_TIMELINE
+    const unsigned long long tStart = wall_clock64();
+#endif
     for (;;) {
         // refill only when at least kRefillLanes lanes are idle: the fetch (queue
         // read, ray loads, three IEEE divisions) is then shared by many lanes
         const unsigned long long need = __ballot(!active);
         if ((uint32_t)__popcll(need) >= kRefillLanes && cursor < end) {
-            const uint32_t idx = cursor + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-            if (!active && idx < end) {
+            const uint32_t k = cursor + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            const uint32_t idx = (waveId + (k / kInterleave) * waves) * kInterleave + k % kInterleave;
+            if (!active && k < end && idx < n) {
                 item = fetch(idx, s);
                 active = true;
             }
@@ -332,11 +358,18 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             if (runnable == 0ull || parked >= kParkLanes || (idle >= kRefillLanes && cursor < end)) break;
         }
         // phase B: the parked lanes' leaf work, shared by many lanes at once
-        if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY>(sc, s, watertight, lds, shift, st)) {
+        if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY>(sc, s, watertight, lds, shift, st)) {
             emit(item, s);
             active = false;
         }
     }
+#ifdef DCRT_WAVE_TIMELINE
+    if (waveTag >= 0 && n > 0 && (threadIdx.x & 63u) == 0 && waveId < 8192) {
+        g_waveLog[ANY_HIT ? 1 : 0][waveTag & 15][waveId][0] = tStart;
+        g_waveLog[ANY_HIT ? 1 : 0][waveTag & 15][waveId][1] = wall_clock64();
+        g_waveItems[ANY_HIT ? 1 : 0][waveTag & 15][waveId] = chunk;
+    }
+#endif
 }
 
 __device__ __forceinline__ void flush_stats(const TraversalStats& st, unsigned long long* dst)
@@ -368,9 +401,25 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
             pool.hit[path] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
             pool.hitInst[path] = s.found ? s.hit.inst : 0u;
         },
-        st);
+        st, DCRT_WAVE_TAG(g));
     if (INSTR) flush_stats(st, instr);
     (void)g;
+}
+
+// End of an iteration (after both casts): account it and clear the other parity's counters.
+__device__ __forceinline__ void end_iteration(const Counters* cnt, Counters* nextCnt, Globals* g, uint32_t shadowRays)
+{
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            const uint32_t ext = qtotal(cnt, kQExt), material = qtotal(cnt, kQMaterial);
+            g->extRays += ext;
+            g->shadowRays += shadowRays;
+            g->iterations += 1ull;
+            // IsImageComplete (WavefrontPathTracer.cpp:508-523), exact and on the device
+            g->imageComplete = (material == 0u && ext == 0u && !g->stopped) ? 1u : 0u;
+        }
+        if (threadIdx.x < kQueues * kShards) nextCnt->w[threadIdx.x * kShardStride] = 0u;
+    }
 }
 
 template <bool INSTR, bool OPACITY>
@@ -395,20 +444,57 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
             const uint32_t f = pool.flags[path];
             pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (f & 0xBFFFFFFFu);
         },
-        st);
+        st, DCRT_WAVE_TAG(g));
     if (INSTR) flush_stats(st, instr + 3);
-    // End of the iteration: account and clear the other parity's counters.
-    if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) {
-            const uint32_t ext = qtotal(cnt, kQExt), material = qtotal(cnt, kQMaterial);
-            g->extRays += ext;
-            g->shadowRays += n;
-            g->iterations += 1ull;
-            // IsImageComplete (WavefrontPathTracer.cpp:508-523), exact and on the device
-            g->imageComplete = (material == 0u && ext == 0u && !g->stopped) ? 1u : 0u;
-        }
-        if (threadIdx.x < kQueues * kShards) nextCnt->w[threadIdx.x * kShardStride] = 0u;
-    }
+    end_iteration(cnt, nextCnt, g, n);
+}
+
+// EXTENSION_RAY_CAST + SHADOW_RAY_CAST in one persistent launch. The two queues are
+// independent (MATERIAL filled both), so their items form one sequence (extension
+// rays first) dealt to the waves like a single queue: one ramp and one drain per
+// iteration instead of two, and a shadow ray can fill a lane an extension ray left
+// idle. Per lane the ray keeps its own semantics (closest hit vs first hit), so the
+// results are those of the two separate kernels.
+template <bool INSTR, bool OPACITY>
+__global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void cast_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
+                                                                     Counters* nextCnt, Globals* g, unsigned long long* instr)
+{
+    extern __shared__ uint32_t stackMem[];
+    QueueMap qe, qs;
+    qmap(cnt, kQExt, &qe);
+    qmap(cnt, kQShadow, &qs);
+    const uint32_t nExt = qe.prefix[kShards], nShadow = qs.prefix[kShards];
+    TraversalStats st = {0u, 0u, 0u};
+    TraversalStats stExt = {0u, 0u, 0u}, stShadow = {0u, 0u, 0u};
+    persistent_trace<false, INSTR, OPACITY, true>(
+        sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
+        [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
+            const bool shadow = i >= nExt;
+            const uint32_t path = shadow ? qentry(pool.shadowQueue, pool.size, qs, i - nExt) : qentry(pool.extQueue, pool.size, qe, i);
+            const float4 o = shadow ? pool.shadowO[path] : pool.rayO[path];
+            const float4 d = shadow ? pool.shadowD[path] : pool.rayD[path];
+            trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, shadow ? o.w : inf());
+            s.anyHit = shadow;
+            if (OPACITY) s.opacitySample = shadow ? pool.shadowOpacity[path] : pool.extOpacity[path];
+            if (INSTR) { st.nodes = 0u; st.tris = 0u; st.blas = 0u; }
+            return path;
+        },
+        [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
+            if (s.anyHit) {
+                const uint32_t f = pool.flags[path];
+                pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (f & 0xBFFFFFFFu);
+            } else {
+                pool.hit[path] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
+                pool.hitInst[path] = s.found ? s.hit.inst : 0u;
+            }
+            if (INSTR) {
+                TraversalStats& dst = s.anyHit ? stShadow : stExt;
+                dst.nodes += st.nodes; dst.tris += st.tris; dst.blas += st.blas;
+            }
+        },
+        st, DCRT_WAVE_TAG(g));
+    if (INSTR) { flush_stats(stExt, instr); flush_stats(stShadow, instr + 3); }
+    end_iteration(cnt, nextCnt, g, nShadow);
 }
 
 // ---- GPU megakernel (MegakernelPathTracing.hlsl:65-208) -------------------------------------
@@ -886,6 +972,10 @@ template __global__ void shadow_kernel<false, false>(PathPool, DeviceScene, cons
 template __global__ void shadow_kernel<false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void shadow_kernel<true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void shadow_kernel<true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void megakernel<false>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void megakernel<true>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void batch_trace_kernel<false>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);

@@ -107,6 +107,7 @@ struct dcrt_tracer {
     bool hasScene = false;
     uint32_t castBlock = 256;
     size_t castLds = 0;
+    bool mergedCasts = true;           // one cast_kernel per iteration (DCRT_SPLIT_CASTS=1: EXT then SHADOW)
 
     dcrt_bxdf_luts* dLuts = nullptr;
     Film film{};
@@ -218,6 +219,7 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     poolSize = (poolSize + 255u) & ~255u;   // whole 256-thread workgroups of whole waves
     iterationsPerRender = cfg.iterations_per_render ? cfg.iterations_per_render : kDefaultIterations;
     debugRng = cfg.debug_rng != 0;
+    if (const char* split = std::getenv("DCRT_SPLIT_CASTS")) mergedCasts = std::atoi(split) == 0;
     if (const char* tune = std::getenv("DCRT_TRAVERSAL_TUNE")) {
         unsigned r = 0, p = 0;
         if (std::sscanf(tune, "%u,%u", &r, &p) == 2 && r >= 1 && r <= 64 && p >= 1 && p <= 64) {
@@ -402,14 +404,16 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         hipDeviceProp_t prop;
         HIPCHECK(hipGetDeviceProperties(&prop, device));
         int perCU = 0;
-        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false, false>, (int)castBlock, castLds));
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, cast_kernel<false, false>, (int)castBlock, castLds));
+        else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false, false>, (int)castBlock, castLds));
         if (const char* b = std::getenv("DCRT_CAST_BLOCKS_PER_CU")) {   // tuning experiments
             const int v = std::atoi(b);
             if (v >= 1 && v < perCU) perCU = v;
         }
         castResident = (uint32_t)std::max(1, perCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int opacityPerCU = 0;
-        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLds));
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, cast_kernel<false, true>, (int)castBlock, castLds));
+        else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLds));
         castResidentOpacity = (uint32_t)std::max(1, std::min(opacityPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int megaPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel<false>, (int)castBlock, castLds));
@@ -575,14 +579,21 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     // Timed launches take their start/stop timestamps from the dispatch itself
     // (hipExtLaunchKernelGGL), so the duration is the kernel's, as rocprofv3 reports it.
     // kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER
-    auto ext = instrCounters ? (opacity ? extension_kernel<true, true> : extension_kernel<true, false>)
-                             : (opacity ? extension_kernel<false, true> : extension_kernel<false, false>);
-    auto shadow = instrCounters ? (opacity ? shadow_kernel<true, true> : shadow_kernel<true, false>)
-                                : (opacity ? shadow_kernel<false, true> : shadow_kernel<false, false>);
-    hipExtLaunchKernelGGL(ext, dim3(castGrid), dim3(castBlock), castLds, stream, e0, e1, 0, pool, scene,
-                          (const FrameConstants*)dFrame, (const Counters*)cnt, dGlobals, dInstr);
-    hipLaunchKernelGGL(shadow, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
-                       next, dGlobals, dInstr);
+    if (mergedCasts) {
+        auto cast = instrCounters ? (opacity ? cast_kernel<true, true> : cast_kernel<true, false>)
+                                  : (opacity ? cast_kernel<false, true> : cast_kernel<false, false>);
+        hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), castLds, stream, e0, e1, 0, pool, scene,
+                              (const FrameConstants*)dFrame, cnt, next, dGlobals, dInstr);
+    } else {
+        auto ext = instrCounters ? (opacity ? extension_kernel<true, true> : extension_kernel<true, false>)
+                                 : (opacity ? extension_kernel<false, true> : extension_kernel<false, false>);
+        auto shadow = instrCounters ? (opacity ? shadow_kernel<true, true> : shadow_kernel<true, false>)
+                                    : (opacity ? shadow_kernel<false, true> : shadow_kernel<false, false>);
+        hipExtLaunchKernelGGL(ext, dim3(castGrid), dim3(castBlock), castLds, stream, e0, e1, 0, pool, scene,
+                              (const FrameConstants*)dFrame, (const Counters*)cnt, dGlobals, dInstr);
+        hipLaunchKernelGGL(shadow, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
+                           next, dGlobals, dInstr);
+    }
     if (sequenced) {
         hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, partition.world_size,
                            partition.rank, std::max<uint32_t>(partition.stripe_height, 1), (const Globals*)dGlobals);
@@ -1131,3 +1142,15 @@ DCRT_API int dcrt_device_math_eval(dcrt_tracer* t, int function, const float* x,
 }
 
 }  // extern "C"
+
+#ifdef DCRT_WAVE_TIMELINE
+// Diagnostic build only: copy the per-wave cast timeline (see kernels_impl.h).
+extern "C" DCRT_API int dcrt_debug_wave_timeline(dcrt_tracer* t, unsigned long long* stamps, uint32_t* items)
+{
+    TRACER_GUARD(t);
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    HIPCHECK(hipMemcpyFromSymbol(stamps, HIP_SYMBOL(g_waveLog), sizeof(g_waveLog)));
+    HIPCHECK(hipMemcpyFromSymbol(items, HIP_SYMBOL(g_waveItems), sizeof(g_waveItems)));
+    return DCRT_OK;
+}
+#endif

@@ -50,7 +50,9 @@ def main(src, dst_prefix):
             d["hbm_bytes_per_launch"] = d["hbm_read_bytes_per_launch"] + d["hbm_write_bytes_per_launch"]
         if "FETCH_SIZE_avg" in d and "TCC_EA0_RDREQ_sum_avg" in d and d["TCC_EA0_RDREQ_sum_avg"]:
             d["fetch_kib_per_rdreq"] = d["FETCH_SIZE_avg"] / d["TCC_EA0_RDREQ_sum_avg"]
-    ext = next((v for k, v in out["kernels"].items() if k.startswith("dcrt::dev::extension_kernel<false")), {})
+    # the timed ray-cast launch: the merged cast_kernel, else (DCRT_SPLIT_CASTS=1) the EXT kernel
+    ext = next((v for k, v in out["kernels"].items() if k.startswith("dcrt::dev::cast_kernel<false")), None) or \
+        next((v for k, v in out["kernels"].items() if k.startswith("dcrt::dev::extension_kernel<false")), {})
     out["ext_hbm_bytes_per_launch"] = ext.get("hbm_bytes_per_launch")
     Path(dst_prefix + "_pmc_traffic.json").write_text(json.dumps(out, indent=1, sort_keys=True))
     print(json.dumps({"ext_hbm_bytes_per_launch": out["ext_hbm_bytes_per_launch"]}))

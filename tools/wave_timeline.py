@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-wave timeline of the EXT / SHADOW cast kernels (1 image, 1080p Cornell).
+
+Needs a library built with -DDCRT_WAVE_TIMELINE (gpu_ab/timeline.so, DCRT_LIB=...).
+For each iteration slot prints: waves, items, kernel span (first start .. last end),
+mean wave lifetime / span (= average residency), and the end-time percentiles that
+show how long the last waves keep the kernel alive.
+"""
+import ctypes as C
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
+    scene = Scene((1920, 1080))
+    scenes.setup_cornell(scene, 1920, 1080, 8)
+    tr = WavefrontPathTracer(path_pool_size=1 << 21, iterations_per_render=16)
+    tr.on_scene_loaded(scene)
+    filt = scene.filter_params()
+    tr.clear_film()
+    tr.render_images(100, 1, filt)
+    tr.render_images(0, 1, filt)
+    tr.synchronize()
+    fn = tr._lib.dcrt_debug_wave_timeline
+    fn.restype = C.c_int
+    stamps = np.zeros((2, 16, 8192, 2), np.uint64)
+    items = np.zeros((2, 16, 8192), np.uint32)
+    rc = fn(tr._h, stamps.ctypes.data_as(C.c_void_p), items.ctypes.data_as(C.c_void_p))
+    assert rc == 0, rc
+    for k, name in enumerate(("EXT", "SHADOW")):
+        for it in range(16):
+            st = stamps[k, it]
+            valid = st[:, 1] > 0
+            if not valid.any():
+                continue
+            s0, s1 = st[valid, 0].astype(np.int64), st[valid, 1].astype(np.int64)
+            t0 = s0.min()
+            span = (s1.max() - t0) / 100.0    # wall_clock64: 100 MHz -> us
+            life = (s1 - s0) / 100.0
+            ends = np.percentile((s1 - t0) / 100.0, [50, 90, 99, 100])
+            starts = np.percentile((s0 - t0) / 100.0, [50, 99, 100])
+            print(f"{name:6s} it{it:2d} waves {valid.sum():5d} items {int(items[k, it][valid].sum()):8d} span {span:7.1f}us "
+                  f"residency {life.mean() / span:5.2f} start p50/p99/max {starts[0]:5.1f}/{starts[1]:5.1f}/{starts[2]:5.1f} "
+                  f"end p50/p90/p99/max {ends[0]:6.1f}/{ends[1]:6.1f}/{ends[2]:6.1f}/{ends[3]:6.1f}")
+    tr.destroy()
+
+
+if __name__ == "__main__":
+    main()
