@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--pool", type=int, default=1 << 21, help="path pool slots")
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
+    ap.add_argument("--image-batch", type=int, default=0, help="images per wavefront batch (0 = automatic)")
     ap.add_argument("--roofline-images", type=int, default=4)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (CPU reduce, for tests)")
     ap.add_argument("--save-film", default=None, help="rank 0 writes the reduced RGBA32F film (.npy)")
@@ -114,9 +115,11 @@ def main():
     tracer = WavefrontPathTracer(path_pool_size=args.pool, iterations_per_render=args.iterations, device=device)
     tracer.on_scene_loaded(scene)
     tracer.set_mode(args.mode)
-    if world > 1:
-        tracer.set_film_partition(world, rank, args.stripe)
+    tracer.set_image_batch(args.image_batch)
     filt = scene.filter_params()
+    if world > 1:
+        from directcomputeraytracing_amd.partition import halo_for_radius
+        tracer.set_film_partition(world, rank, args.stripe, max(1, halo_for_radius(filt.radius)))
 
     def barrier_sync():
         tracer.synchronize()

@@ -170,6 +170,7 @@ SIGNATURES = [
     ("dcrt_tracer_render", _I, [_P, _U]),
     ("dcrt_tracer_render_images", _I, [_P, _U, _U, C.POINTER(FilterParams)]),
     ("dcrt_tracer_set_mode", _I, [_P, _I]),
+    ("dcrt_tracer_set_image_batch", _I, [_P, C.c_uint32]),
     ("dcrt_tracer_reset_image", _I, [_P]),
     ("dcrt_tracer_is_image_complete", _I, [_P, C.POINTER(C.c_int)]),
     ("dcrt_tracer_acquire_film_clear_trigger", _I, [_P, C.POINTER(C.c_int)]),

@@ -36,7 +36,9 @@ struct Globals {
     // device-side image sequencing (RenderImages): no host round trip between images
     uint32_t imageComplete;   // SHADOW: this iteration's CONTROL found every path idle and nothing to claim
     uint32_t stopped;         // all requested images are done: CONTROL claims nothing more
-    uint32_t imagesDone, imageTarget, seedBase, pad1;
+    uint32_t imagesDone, imageTarget, seedBase;
+    uint32_t batchImages;     // images path-traced together in the current batch (image index in [0, batchImages))
+    uint32_t batchCap;        // RenderImages' batch size
     unsigned long long extRays, shadowRays, newPaths, iterations;
 };
 
@@ -81,7 +83,8 @@ struct FrameConstants {
     float apertureBaseAngle;
     uint32_t frameSeed;
     uint32_t maxBounce, lightCount, envLightIndex, features;
-    uint32_t blocksX, bandCount;     // blocks per row, number of 8-row bands
+    uint32_t blocksX, bandCount;     // blocks per row, number of 8-row groups of the rendered rows
+    uint32_t blocksPerImage;         // blocksX * bandCount
     uint32_t refillLanes, parkLanes; // persistent traversal thresholds (lanes of a wave64)
 };
 
@@ -126,7 +129,7 @@ struct PathPool {
     uint32_t* hitInst;
     float4* shadowO;
     float4* shadowD;
-    uint32_t* pixel;     // x | y << 16
+    uint32_t* pixel;     // sample index: image * W*H + y * W + x
     float2* pixelSample;
     uint4* rng;
     float4* lsr;         // light sampling result
@@ -141,14 +144,32 @@ struct PathPool {
     uint32_t size;
 };
 
+// Sample textures (m_SamplePositionTexture / m_SampleValueTexture) for every image of a
+// batch: image b's sample of pixel (x, y) sits at b * W*H + y * W + x.
 struct Film {
-    float2* samplePosition;   // W*H
-    float4* sampleValue;      // W*H
-    uint4* debugRng;          // W*H or nullptr
+    float2* samplePosition;   // batch x W*H
+    float4* sampleValue;      // batch x W*H
+    uint4* debugRng;          // batch x W*H or nullptr
     float4* accum;            // W*H RGBA32F (sum w*L, sum w)
-    const uint32_t* bandY;    // first row of each 8-row band this tracer renders
-    uint32_t width, height;
+    const uint32_t* rowY;     // the rows this tracer path-traces (8 per block row), ascending
+    const uint32_t* rowOwned; // per film row: 1 if this tracer convolves it (nullptr: all rows)
+    uint32_t width, height, rowCount;
 };
+
+// Pixel of lane `lane` in claimed block `block` of the batch: image, then 8-row group,
+// then 8-column block. False for lanes outside the film or past the last rendered row.
+DEV bool block_pixel(const FrameConstants& fc, const Film& film, uint32_t block, uint32_t lane, uint32_t* px, uint32_t* py,
+                     uint32_t* image)
+{
+    *image = block / fc.blocksPerImage;
+    const uint32_t local = block - *image * fc.blocksPerImage;
+    const uint32_t band = local / fc.blocksX, bx = local - band * fc.blocksX;
+    const uint32_t ri = band * kBlockH + lane / kBlockW;
+    *px = bx * kBlockW + (lane % kBlockW);
+    if (*px >= fc.resolution[0] || ri >= film.rowCount) return false;
+    *py = film.rowY[ri];
+    return *py < fc.resolution[1];
+}
 
 }  // namespace dev
 }  // namespace dcrt

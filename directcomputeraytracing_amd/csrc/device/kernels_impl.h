@@ -53,6 +53,8 @@ __global__ void set_idle_kernel(PathPool pool, Counters* counters, Globals* g, u
     if (tid < kShards) g->nextBlock[tid * kShardStride] = 0u;
     if (tid == 0) {
         g->totalBlocks = totalBlocks;
+        g->batchImages = 1u;
+        g->batchCap = 1u;
         g->imageComplete = 0u;
         g->stopped = 0u;
         g->imagesDone = 0u;
@@ -100,8 +102,7 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
         li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
         li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
         if (terminate) {
-            const uint32_t pp = pool.pixel[tid];
-            const size_t p = (size_t)(pp >> 16) * film.width + (pp & 0xFFFFu);
+            const size_t p = pool.pixel[tid];
             film.samplePosition[p] = pool.pixelSample[tid];
             film.sampleValue[p] = make_float4(li.x, li.y, li.z, 0.0f);
             if (debugRng) film.debugRng[p] = pool.rng[tid];
@@ -123,13 +124,10 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
     const uint32_t block = shard + claimed * kShards;
     bool newPath = false;
     if (got) {
-        const uint32_t band = block / fc->blocksX, bx = block % fc->blocksX;
-        const uint32_t px = bx * kBlockW + (lane % kBlockW);
-        const uint32_t py = film.bandY[band] + lane / kBlockW;
-        const bool clipped = px >= fc->resolution[0] || py >= fc->resolution[1];
-        if (!clipped) {
-            // NEW_PATH :211-237
-            Rng rng = rng_init(px, py, fc->frameSeed);
+        uint32_t px = 0, py = 0, image = 0;
+        if (block_pixel(*fc, film, block, lane, &px, &py, &image)) {
+            // NEW_PATH :211-237 (image `image` of the batch has frame seed frameSeed + image)
+            Rng rng = rng_init(px, py, fc->frameSeed + image);
             const float psx = next1(rng), psy = next1(rng);
             const float fsx = (psx + (float)px) / (float)fc->resolution[0];
             const float fsy = (psy + (float)py) / (float)fc->resolution[1];
@@ -137,7 +135,7 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
             V3 o, d;
             generate_ray(*fc, fsx, fsy, a0, a1, a2, &o, &d);
             if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) pool.extOpacity[tid] = next1(rng);   // :223-226
-            pool.pixel[tid] = px | (py << 16);
+            pool.pixel[tid] = image * (film.width * film.height) + py * film.width + px;
             pool.pixelSample[tid] = make_float2(psx, psy);
             pool.lsr[tid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             pool.rng[tid] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
@@ -157,7 +155,12 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
 }
 
 // ---- MATERIAL -----------------------------------------------------------------------
-__global__ __launch_bounds__(256) void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt)
+#ifdef DCRT_MATERIAL_WAVES_PER_EU
+#define DCRT_MATERIAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(DCRT_MATERIAL_WAVES_PER_EU, 8)))
+#else
+#define DCRT_MATERIAL_OCCUPANCY
+#endif
+__global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt)
 {
     __shared__ uint32_t sm[64];
     QueueMap qm;
@@ -545,11 +548,9 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
         if (__syncthreads_or(got ? 1 : 0) == 0) break;
         if (!got) continue;
         const uint32_t block = shard + claimed * kShards;
-        const uint32_t band = block / fc.blocksX, bx = block % fc.blocksX;
-        const uint32_t px = bx * kBlockW + (lane % kBlockW);
-        const uint32_t py = film.bandY[band] + lane / kBlockW;
-        if (px >= fc.resolution[0] || py >= fc.resolution[1]) continue;
-        Rng rng = rng_init(px, py, fc.frameSeed);
+        uint32_t px = 0, py = 0, image = 0;
+        if (!block_pixel(fc, film, block, lane, &px, &py, &image)) continue;
+        Rng rng = rng_init(px, py, fc.frameSeed + image);
         const float psx = next1(rng), psy = next1(rng);
         const float fsx = (psx + (float)px) / (float)fc.resolution[0];
         const float fsy = (psy + (float)py) / (float)fc.resolution[1];
@@ -641,7 +642,7 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
             }
             if (terminate) break;
         }
-        const size_t p = (size_t)py * film.width + px;
+        const size_t p = (size_t)image * film.width * film.height + (size_t)py * film.width + px;
         film.samplePosition[p] = make_float2(psx, psy);
         film.sampleValue[p] = make_float4(L.x, L.y, L.z, 0.0f);
         if (debugRng) film.debugRng[p] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
@@ -730,59 +731,71 @@ __device__ __forceinline__ float evaluate_filter(const FilterConsts& c, float px
 
 // SampleConvolution (SampleConvolution.hlsl:67-106), grid-stride over pixels. With
 // `guard` set it runs only in the iteration that completed an image (RenderImages).
-__global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t worldSize, uint32_t rank,
-                                                   uint32_t stripeHeight, const Globals* guard)
+__global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t images, const Globals* guard)
 {
     if (guard && !guard->imageComplete) return;
+    // the images of a completed batch, in order: per pixel the same additions as one
+    // film pass per image
+    const uint32_t count = guard ? guard->batchImages : images;
     const FilterConsts c = *fcon;
     const uint32_t W = film.width, H = film.height;
     const uint32_t total = W * H;
     for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
         const uint32_t py = p / W, px = p - py * W;
-        if (worldSize > 1 && (py / stripeHeight) % worldSize != rank) continue;
+        if (film.rowOwned && !film.rowOwned[py]) continue;
         const float r = c.radius;
         const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
         int xs = (int)floorf(cx - r); xs = xs < 0 ? 0 : xs;
         int xe = (int)floorf(cx + r); xe = xe > (int)W - 1 ? (int)W - 1 : xe;
         int ys = (int)floorf(cy - r); ys = ys < 0 ? 0 : ys;
         int ye = (int)floorf(cy + r); ye = ye > (int)H - 1 ? (int)H - 1 : ye;
-        float wsum = 0.0f;
-        V3 sum = mk(0.0f, 0.0f, 0.0f);
-        for (int y = ys; y <= ye; ++y)
-            for (int x = xs; x <= xe; ++x) {
-                const size_t q = (size_t)y * W + x;
-                const float2 sp = film.samplePosition[q];
-                const float4 sv = film.sampleValue[q];
-                const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
-                sum = sum + mk(sv.x, sv.y, sv.z) * w;
-                wsum = wsum + w;
-            }
         float4 v = film.accum[p];
-        v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
+        for (uint32_t b = 0; b < count; ++b) {
+            const float2* sPos = film.samplePosition + (size_t)b * total;
+            const float4* sVal = film.sampleValue + (size_t)b * total;
+            float wsum = 0.0f;
+            V3 sum = mk(0.0f, 0.0f, 0.0f);
+            for (int y = ys; y <= ye; ++y)
+                for (int x = xs; x <= xe; ++x) {
+                    const size_t q = (size_t)y * W + x;
+                    const float2 sp = sPos[q];
+                    const float4 sv = sVal[q];
+                    const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
+                    sum = sum + mk(sv.x, sv.y, sv.z) * w;
+                    wsum = wsum + w;
+                }
+            v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
+        }
         film.accum[p] = v;
     }
 }
 
-// After the film pass of a completed image: next frame seed, rewind the block cursors.
+// After the film pass of a completed batch: the next batch's first frame seed and
+// size, rewind the block cursors.
 __global__ void advance_image_kernel(FrameConstants* fc, Globals* g)
 {
     if (threadIdx.x != 0 || !g->imageComplete) return;
     g->imageComplete = 0u;
-    g->imagesDone += 1u;
+    g->imagesDone += g->batchImages;
     if (g->imagesDone < g->imageTarget) {
         fc->frameSeed = g->seedBase + g->imagesDone;
+        g->batchImages = min(g->batchCap, g->imageTarget - g->imagesDone);
+        g->totalBlocks = fc->blocksPerImage * g->batchImages;
         for (uint32_t s = 0; s < kShards; ++s) g->nextBlock[s * kShardStride] = 0u;
     } else {
         g->stopped = 1u;
     }
 }
 
-__global__ void begin_images_kernel(Globals* g, uint32_t count, uint32_t firstSeed)
+__global__ void begin_images_kernel(Globals* g, const FrameConstants* fc, uint32_t count, uint32_t firstSeed, uint32_t batchCap)
 {
     if (threadIdx.x != 0) return;
     g->imagesDone = 0u;
     g->imageTarget = count;
     g->seedBase = firstSeed;
+    g->batchCap = batchCap;
+    g->batchImages = min(batchCap, count);
+    g->totalBlocks = fc->blocksPerImage * g->batchImages;
     g->stopped = count == 0u ? 1u : 0u;
     g->imageComplete = 0u;
 }

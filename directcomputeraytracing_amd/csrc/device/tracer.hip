@@ -101,7 +101,7 @@ struct dcrt_tracer {
     bool debugRng = false;
     uint32_t refillLanes = 16, parkLanes = 32;   // DCRT_TRAVERSAL_TUNE="refill,park" overrides
 
-    std::vector<void*> poolAllocs, sceneAllocs, filmAllocs;
+    std::vector<void*> poolAllocs, sceneAllocs, filmAllocs, sampleAllocs, rowAllocs;
     PathPool pool{};
     DeviceScene scene{};
     bool hasScene = false;
@@ -112,8 +112,11 @@ struct dcrt_tracer {
     dcrt_bxdf_luts* dLuts = nullptr;
     Film film{};
     uint32_t filmW = 0, filmH = 0;
-    uint32_t* dBands = nullptr;
-    uint32_t bandCount = 0;
+    uint32_t rowCount = 0;             // rows this tracer path-traces (film.rowY)
+    uint32_t bandCount = 0;            // ceil(rowCount / 8): block rows of an image
+    uint32_t sampleImages = 0;         // images the sample textures hold (batch capacity)
+    uint32_t batchImages = 0;          // RenderImages batch size (0: automatic)
+    uint32_t lastSlot = 0;             // sample slot of the last completed image
     dcrt_film_partition partition{ 1, 0, 64, 0 };
 
     dcrt_frame_params frame{};
@@ -154,7 +157,9 @@ struct dcrt_tracer {
     int SetFrame(const dcrt_frame_params& p);
     int SetPartition(const dcrt_film_partition& p);
     int EnsureFilm(uint32_t w, uint32_t h);
-    int BuildBands();
+    int BuildRows();
+    int EnsureSamples(uint32_t images);
+    uint32_t AutoBatch(uint32_t count) const;
     int BeginImage();
     int LaunchIteration(uint32_t par, bool timed, bool sequenced);
     int LaunchGraph(bool sequenced, uint32_t iters);
@@ -195,6 +200,8 @@ dcrt_tracer::~dcrt_tracer()
     FreeAll(&poolAllocs);
     FreeAll(&sceneAllocs);
     FreeAll(&filmAllocs);
+    FreeAll(&sampleAllocs);
+    FreeAll(&rowAllocs);
     if (hCounters) (void)hipHostFree(hCounters);
     if (ownsStream && stream) (void)hipStreamDestroy(stream);
 }
@@ -432,52 +439,94 @@ int dcrt_tracer::EnsureFilm(uint32_t w, uint32_t h)
     HIPCHECK(hipStreamSynchronize(stream));
     InvalidateGraph();
     FreeAll(&filmAllocs);
+    FreeAll(&sampleAllocs);
+    sampleImages = 0;
     const size_t n = (size_t)w * h;
-    CHECKED(DeviceAlloc(&film.samplePosition, n, &filmAllocs));
-    CHECKED(DeviceAlloc(&film.sampleValue, n, &filmAllocs));
     CHECKED(DeviceAlloc(&film.accum, n, &filmAllocs));
-    film.debugRng = nullptr;
-    if (debugRng) CHECKED(DeviceAlloc(&film.debugRng, n, &filmAllocs));
-    HIPCHECK(hipMemsetAsync(film.samplePosition, 0, n * sizeof(float2), stream));
-    HIPCHECK(hipMemsetAsync(film.sampleValue, 0, n * sizeof(float4), stream));
     HIPCHECK(hipMemsetAsync(film.accum, 0, n * sizeof(float4), stream));
-    if (film.debugRng) HIPCHECK(hipMemsetAsync(film.debugRng, 0, n * sizeof(uint4), stream));
     filmW = w; filmH = h;
     film.width = w; film.height = h;
-    return BuildBands();
+    CHECKED(EnsureSamples(1));
+    return BuildRows();
 }
 
-// 8-row bands this tracer renders: its stripes plus `halo` rows either side
-// (a band may be shorter than 8 rows at a halo edge; its missing rows are clipped).
-int dcrt_tracer::BuildBands()
+// Sample textures for `images` images (a RenderImages batch); grows only.
+int dcrt_tracer::EnsureSamples(uint32_t images)
 {
-    std::vector<uint32_t> bands;
-    const uint32_t H = filmH;
-    if (partition.world_size <= 1) {
-        for (uint32_t y = 0; y < H; y += kBlockH) bands.push_back(y);
-    } else {
-        const uint32_t S = partition.stripe_height, halo = partition.halo_rows ? partition.halo_rows : 2u;
-        std::vector<uint8_t> need(H, 0);
-        for (uint32_t y = 0; y < H; ++y) {
-            if ((y / S) % partition.world_size != partition.rank) continue;
-            const uint32_t lo = y >= halo ? y - halo : 0, hi = std::min(H - 1, y + halo);
-            for (uint32_t k = lo; k <= hi; ++k) need[k] = 1;
-        }
-        // one band per aligned 8-row group that contains a needed row
-        for (uint32_t y = 0; y < H; y += kBlockH) {
-            bool any = false;
-            for (uint32_t k = y; k < std::min(H, y + kBlockH); ++k) any = any || need[k];
-            if (any) bands.push_back(y);
-        }
-    }
-    if (bands.empty()) bands.push_back(0);
-    bandCount = (uint32_t)bands.size();
-    uint32_t* p = nullptr;
-    CHECKED(DeviceAlloc(&p, bands.size(), &filmAllocs));
-    HIPCHECK(hipMemcpyAsync(p, bands.data(), bands.size() * 4, hipMemcpyHostToDevice, stream));
+    if (images <= sampleImages) return DCRT_OK;
     HIPCHECK(hipStreamSynchronize(stream));
-    dBands = p;
-    film.bandY = p;
+    InvalidateGraph();
+    FreeAll(&sampleAllocs);
+    const size_t n = (size_t)filmW * filmH * images;
+    CHECKED(DeviceAlloc(&film.samplePosition, n, &sampleAllocs));
+    CHECKED(DeviceAlloc(&film.sampleValue, n, &sampleAllocs));
+    film.debugRng = nullptr;
+    if (debugRng) CHECKED(DeviceAlloc(&film.debugRng, n, &sampleAllocs));
+    HIPCHECK(hipMemsetAsync(film.samplePosition, 0, n * sizeof(float2), stream));
+    HIPCHECK(hipMemsetAsync(film.sampleValue, 0, n * sizeof(float4), stream));
+    if (film.debugRng) HIPCHECK(hipMemsetAsync(film.debugRng, 0, n * sizeof(uint4), stream));
+    sampleImages = images;
+    return DCRT_OK;
+}
+
+// Images per RenderImages batch: as many as the path pool holds at once, so that a rank
+// of a partitioned film (a fraction of every image) still runs full wavefronts. A batch
+// that overflows the pool by a little is avoided: its last pixel blocks would start only
+// when the first paths end and stretch the batch by a whole path length.
+uint32_t dcrt_tracer::AutoBatch(uint32_t count) const
+{
+    uint32_t b = batchImages;
+    if (b == 0) {
+        const uint64_t pixels = std::max<uint64_t>(1, (uint64_t)rowCount * filmW);
+        b = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, poolSize / pixels));
+    }
+    return std::max<uint32_t>(1, std::min(b, count));
+}
+
+// Rows this tracer renders. One tracer: every row. Partitioned film: the
+// film is cut into K = N * k stripes of floor/ceil(H / K) rows, k = round(H / (N * S))
+// for the target stripe height S, stripe j belongs to rank j mod N (every rank gets k
+// stripes, equal row counts to one row); a rank renders its rows plus `halo` rows on
+// either side of each stripe and convolves only its own rows. The rows are packed 8 per
+// block row in ascending order (directcomputeraytracing_amd/partition.py mirrors this).
+int dcrt_tracer::BuildRows()
+{
+    const uint32_t H = filmH;
+    std::vector<uint32_t> rows;
+    std::vector<uint32_t> owned;
+    if (partition.world_size <= 1) {
+        for (uint32_t y = 0; y < H; ++y) rows.push_back(y);
+    } else {
+        const uint32_t N = partition.world_size, halo = partition.halo_rows ? partition.halo_rows : 2u;
+        const uint32_t k = std::max<uint32_t>(1, (uint32_t)((H + (N * partition.stripe_height) / 2) / (N * partition.stripe_height)));
+        const uint64_t K = std::min<uint64_t>((uint64_t)N * k, H);
+        owned.assign(H, 0);
+        std::vector<uint8_t> need(H, 0);
+        for (uint64_t j = partition.rank; j < K; j += N) {
+            const uint32_t y0 = (uint32_t)(j * H / K), y1 = (uint32_t)((j + 1) * H / K);
+            for (uint32_t y = y0; y < y1; ++y) owned[y] = 1;
+            const uint32_t lo = y0 >= halo ? y0 - halo : 0, hi = std::min(H, y1 + halo);
+            for (uint32_t y = lo; y < hi; ++y) need[y] = 1;
+        }
+        for (uint32_t y = 0; y < H; ++y) if (need[y]) rows.push_back(y);
+    }
+    if (rows.empty()) rows.push_back(0);
+    HIPCHECK(hipStreamSynchronize(stream));
+    FreeAll(&rowAllocs);
+    rowCount = (uint32_t)rows.size();
+    bandCount = (rowCount + kBlockH - 1) / kBlockH;
+    uint32_t* dRows = nullptr;
+    CHECKED(DeviceAlloc(&dRows, rows.size(), &rowAllocs));
+    HIPCHECK(hipMemcpyAsync(dRows, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, stream));
+    uint32_t* dOwned = nullptr;
+    if (!owned.empty()) {
+        CHECKED(DeviceAlloc(&dOwned, owned.size(), &rowAllocs));
+        HIPCHECK(hipMemcpyAsync(dOwned, owned.data(), owned.size() * 4, hipMemcpyHostToDevice, stream));
+    }
+    HIPCHECK(hipStreamSynchronize(stream));
+    film.rowY = dRows;
+    film.rowOwned = dOwned;
+    film.rowCount = rowCount;
     return DCRT_OK;
 }
 
@@ -499,7 +548,7 @@ int dcrt_tracer::SetFrame(const dcrt_frame_params& p)
 
 int dcrt_tracer::SetPartition(const dcrt_film_partition& p)
 {
-    if (p.world_size == 0 || p.rank >= p.world_size || (p.world_size > 1 && (p.stripe_height == 0 || p.stripe_height % kBlockH))) {
+    if (p.world_size == 0 || p.rank >= p.world_size || (p.world_size > 1 && p.stripe_height == 0)) {
         SetLastError("invalid film partition");
         return DCRT_E_INVALID_ARG;
     }
@@ -507,7 +556,7 @@ int dcrt_tracer::SetPartition(const dcrt_film_partition& p)
     if (filmW) {
         HIPCHECK(hipStreamSynchronize(stream));
         InvalidateGraph();
-        CHECKED(BuildBands());
+        CHECKED(BuildRows());
     }
     newImage = true;
     return DCRT_OK;
@@ -534,10 +583,11 @@ int dcrt_tracer::BeginImage()
     fc.features = frame.features;
     fc.blocksX = (frame.resolution[0] + kBlockW - 1) / kBlockW;
     fc.bandCount = bandCount;
+    fc.blocksPerImage = fc.blocksX * bandCount;
     fc.refillLanes = refillLanes;
     fc.parkLanes = parkLanes;
     hipLaunchKernelGGL(set_frame_kernel, dim3(1), dim3(1), 0, stream, dFrame, fc);
-    const uint32_t total = fc.blocksX * bandCount;
+    const uint32_t total = fc.blocksPerImage;
     const uint32_t idleThreads = std::max<uint32_t>(poolSize, 2u * (uint32_t)(sizeof(Counters) / 4));
     hipLaunchKernelGGL(set_idle_kernel, dim3((idleThreads + 255) / 256), dim3(256), 0, stream, pool, dCounters, dGlobals, total);
     HIPCHECK(hipGetLastError());
@@ -595,8 +645,8 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
                            next, dGlobals, dInstr);
     }
     if (sequenced) {
-        hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, partition.world_size,
-                           partition.rank, std::max<uint32_t>(partition.stripe_height, 1), (const Globals*)dGlobals);
+        hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
+                           (const Globals*)dGlobals);
         hipLaunchKernelGGL(advance_image_kernel, dim3(1), dim3(64), 0, stream, dFrame, dGlobals);
     }
     HIPCHECK(hipGetLastError());
@@ -663,6 +713,7 @@ int dcrt_tracer::Render(uint32_t maxIterations)
     if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
     if (newImage) CHECKED(BeginImage());
+    lastSlot = 0;
     CHECKED(RunIterations(maxIterations ? maxIterations : iterationsPerRender));
     bool complete = false;
     CHECKED(ReadCompletion(&complete));
@@ -683,8 +734,8 @@ int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
 {
     if (!film.accum) { SetLastError("no film"); return DCRT_E_INVALID_ARG; }
     CHECKED(UploadFilter(f));
-    hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, partition.world_size,
-                       partition.rank, std::max<uint32_t>(partition.stripe_height, 1), (const Globals*)nullptr);
+    hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
+                       (const Globals*)nullptr);
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
 }
@@ -697,6 +748,15 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
     if (count == 0) return DCRT_OK;
+    if (partition.world_size > 1) {
+        // a partitioned film's convolution reads floor(r + 0.5) rows beyond its stripes
+        const uint32_t halo = partition.halo_rows ? partition.halo_rows : 2u;
+        if (!(filter.radius >= 0.0f) || (double)std::floor(filter.radius + 0.5f) > (double)halo) {
+            SetLastError("filter radius needs more halo rows than the film partition renders");
+            return DCRT_E_INVALID_ARG;
+        }
+    }
+    lastSlot = 0;
     if (mode == 1) {   // MegakernelPathTracer::Render: one persistent launch + SampleConvolution per image
         CHECKED(UploadFilter(filter));
         for (uint32_t img = 0; img < count; ++img) {
@@ -715,8 +775,8 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
             auto mk = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) ? megakernel<true> : megakernel<false>;
             hipExtLaunchKernelGGL(mk, dim3(megaResident), dim3(castBlock), castLds, stream, e0, e1, 0, scene,
                                   (const FrameConstants*)dFrame, film, dGlobals, (uint32_t)(film.debugRng != nullptr));
-            hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, partition.world_size,
-                               partition.rank, std::max<uint32_t>(partition.stripe_height, 1), (const Globals*)nullptr);
+            hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
+                               (const Globals*)nullptr);
             HIPCHECK(hipGetLastError());
         }
         HIPCHECK(hipStreamSynchronize(stream));
@@ -724,10 +784,12 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
         newImage = true;
         return DCRT_OK;
     }
+    const uint32_t batch = AutoBatch(count);
+    CHECKED(EnsureSamples(batch));
     frame.frame_seed = firstSeed;
     CHECKED(UploadFilter(filter));
     CHECKED(BeginImage());
-    hipLaunchKernelGGL(begin_images_kernel, dim3(1), dim3(64), 0, stream, dGlobals, count, firstSeed);
+    hipLaunchKernelGGL(begin_images_kernel, dim3(1), dim3(64), 0, stream, dGlobals, (const FrameConstants*)dFrame, count, firstSeed, batch);
     HIPCHECK(hipGetLastError());
     // a path needs maxBounce + 3 iterations; cap the total so a broken scene cannot spin forever
     const uint64_t maxIterations = ((uint64_t)count + 2) * (frame.max_bounce_count + 8) * (1 + (filmW * (uint64_t)filmH) / poolSize) + 64;
@@ -771,6 +833,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     }
     imageComplete = true;
     newImage = true;
+    lastSlot = (count - 1) % batch;
     return DCRT_OK;
 }
 
@@ -896,9 +959,9 @@ DCRT_API int dcrt_tracer_read_samples(dcrt_tracer* t, float* pos, float* val)
 {
     TRACER_GUARD(t);
     if (!t->film.sampleValue) return DCRT_E_INVALID_ARG;
-    const size_t n = (size_t)t->filmW * t->filmH;
-    if (pos) HIPCHECK(hipMemcpyAsync(pos, t->film.samplePosition, n * sizeof(float2), hipMemcpyDeviceToHost, t->stream));
-    if (val) HIPCHECK(hipMemcpyAsync(val, t->film.sampleValue, n * sizeof(float4), hipMemcpyDeviceToHost, t->stream));
+    const size_t n = (size_t)t->filmW * t->filmH, o = n * t->lastSlot;   // the last image's samples
+    if (pos) HIPCHECK(hipMemcpyAsync(pos, t->film.samplePosition + o, n * sizeof(float2), hipMemcpyDeviceToHost, t->stream));
+    if (val) HIPCHECK(hipMemcpyAsync(val, t->film.sampleValue + o, n * sizeof(float4), hipMemcpyDeviceToHost, t->stream));
     HIPCHECK(hipStreamSynchronize(t->stream));
     return DCRT_OK;
 }
@@ -907,7 +970,8 @@ DCRT_API int dcrt_tracer_read_rng(dcrt_tracer* t, uint32_t* out)
 {
     TRACER_GUARD(t);
     if (!out || !t->film.debugRng) { SetLastError("tracer was created without debug_rng"); return DCRT_E_INVALID_ARG; }
-    HIPCHECK(hipMemcpyAsync(out, t->film.debugRng, (size_t)t->filmW * t->filmH * sizeof(uint4), hipMemcpyDeviceToHost, t->stream));
+    const size_t n = (size_t)t->filmW * t->filmH;
+    HIPCHECK(hipMemcpyAsync(out, t->film.debugRng + n * t->lastSlot, n * sizeof(uint4), hipMemcpyDeviceToHost, t->stream));
     HIPCHECK(hipStreamSynchronize(t->stream));
     return DCRT_OK;
 }
@@ -1073,6 +1137,14 @@ DCRT_API int dcrt_tracer_trace_rays_device(dcrt_tracer* t, const void* d_rays, u
 {
     TRACER_GUARD(t);
     return TraceBatch(t, (const dcrt_ray*)d_rays, n, (dcrt_ray_hit*)d_hits, nullptr, false, features);
+}
+
+DCRT_API int dcrt_tracer_set_image_batch(dcrt_tracer* t, uint32_t images)
+{
+    TRACER_GUARD(t);
+    if (images > 64) { SetLastError("image batch too large (max 64)"); return DCRT_E_INVALID_ARG; }
+    t->batchImages = images;
+    return DCRT_OK;
 }
 
 DCRT_API int dcrt_tracer_set_mode(dcrt_tracer* t, int mode)

@@ -1,12 +1,18 @@
 """Film partitioning across ranks.
 
-Stripes of ``stripe_height`` rows go round-robin to ranks (stripe k -> rank
-k mod N). A rank renders the 8-row pixel bands (the 8x8 wave block height)
-that touch its stripes or their ``halo`` rows, and convolves only the rows it
-owns, so the sum of all ranks' films equals the one-GPU film bit for bit.
-This mirrors ``dcrt_tracer::BuildBands`` / ``film_kernel`` in csrc/device.
+The H film rows are cut into K = N * k stripes of floor/ceil(H / K) rows, with
+k = round(H / (N * stripe_height)) (at least 1): stripe j covers rows
+[j*H/K, (j+1)*H/K) and belongs to rank j mod N, so every rank owns k stripes and
+the same number of rows to within one per stripe. A rank path-traces its rows
+plus ``halo`` rows beyond each stripe edge (the filter's support, floor(r + 0.5)
+rows) and convolves only the rows it owns, so the sum of all ranks' films equals
+the one-GPU film bit for bit. The rendered rows are packed 8 per block row in
+ascending order. This mirrors ``dcrt_tracer::BuildRows`` / ``film_kernel`` in
+csrc/device.
 """
 from __future__ import annotations
+
+import math
 
 import numpy as np
 
@@ -14,34 +20,48 @@ BLOCK_H = 8
 DEFAULT_HALO = 2
 
 
+def stripe_count(height: int, world_size: int, stripe_height: int) -> int:
+    k = max(1, (height + (world_size * stripe_height) // 2) // (world_size * stripe_height))
+    return min(world_size * k, height)
+
+
 def owned_rows(height: int, world_size: int, rank: int, stripe_height: int) -> np.ndarray:
-    y = np.arange(height)
     if world_size <= 1:
         return np.ones(height, bool)
-    return (y // stripe_height) % world_size == rank
+    K = stripe_count(height, world_size, stripe_height)
+    own = np.zeros(height, bool)
+    for j in range(rank, K, world_size):
+        own[j * height // K:(j + 1) * height // K] = True
+    return own
 
 
-def render_bands(height: int, world_size: int, rank: int, stripe_height: int, halo: int = DEFAULT_HALO) -> list:
-    """First rows of the 8-row bands this rank path-traces."""
+def render_rows(height: int, world_size: int, rank: int, stripe_height: int, halo: int = DEFAULT_HALO) -> list:
+    """Rows this rank path-traces, ascending (8 of them per block row)."""
     if world_size <= 1:
-        return list(range(0, height, BLOCK_H))
-    own = owned_rows(height, world_size, rank, stripe_height)
+        return list(range(height))
+    K = stripe_count(height, world_size, stripe_height)
     need = np.zeros(height, bool)
-    for y in np.nonzero(own)[0]:
-        need[max(0, y - halo):min(height - 1, y + halo) + 1] = True
-    return [y for y in range(0, height, BLOCK_H) if need[y:y + BLOCK_H].any()]
+    for j in range(rank, K, world_size):
+        y0, y1 = j * height // K, (j + 1) * height // K
+        need[max(0, y0 - halo):min(height, y1 + halo)] = True
+    return [int(y) for y in np.nonzero(need)[0]]
+
+
+def halo_for_radius(radius: float) -> int:
+    """Rows of support beyond a pixel row that SampleConvolution gathers (SampleConvolution.hlsl:77-81)."""
+    return int(math.floor(radius + 0.5))
+
+
+def row_runs(rows) -> list:
+    """Contiguous (y0, y1) runs of an ascending row list."""
+    out = []
+    for y in rows:
+        if out and out[-1][1] == y:
+            out[-1][1] = y + 1
+        else:
+            out.append([y, y + 1])
+    return [tuple(r) for r in out]
 
 
 def owned_row_ranges(height: int, world_size: int, rank: int, stripe_height: int) -> list:
-    own = owned_rows(height, world_size, rank, stripe_height)
-    out, y = [], 0
-    while y < height:
-        if own[y]:
-            y1 = y
-            while y1 < height and own[y1]:
-                y1 += 1
-            out.append((y, y1))
-            y = y1
-        else:
-            y += 1
-    return out
+    return row_runs(np.nonzero(owned_rows(height, world_size, rank, stripe_height))[0])

@@ -83,6 +83,10 @@ class WavefrontPathTracer:
         f = filter_params or self.filter
         check(self._lib.dcrt_tracer_render_images(self._h, int(first_seed), int(count), C.byref(f)), "RenderImages")
 
+    def set_image_batch(self, images: int = 0) -> None:
+        """Images per render_images batch (0 = automatic)."""
+        check(self._lib.dcrt_tracer_set_image_batch(self._h, int(images)), "SetImageBatch")
+
     def set_mode(self, mode: str) -> None:
         """"wavefront" (CWavefrontPathTracer) or "megakernel" (CMegakernelPathTracer) for render_images."""
         check(self._lib.dcrt_tracer_set_mode(self._h, {"wavefront": 0, "megakernel": 1}[mode]), "SetMode")

@@ -244,12 +244,15 @@ typedef struct dcrt_ray_stats {
 } dcrt_ray_stats;
 
 /* Rows of the film a tracer renders and convolves (multi-GPU film tiling).
- * Stripes of `stripe_height` rows; stripe k belongs to rank k % world_size. */
+ * The H rows are cut into K = N * k stripes of floor/ceil(H / K) rows, k = round(H / (N *
+ * stripe_height)) (at least 1); stripe j = rows [j*H/K, (j+1)*H/K) belongs to rank j % N.
+ * A rank path-traces its rows plus halo_rows rows beyond each stripe edge and convolves
+ * only its own rows, so the SUM of all ranks' films is the one-tracer film bit for bit. */
 typedef struct dcrt_film_partition {
-    uint32_t world_size;          /* 1 = whole film                                   */
+    uint32_t world_size;          /* N; 1 = whole film                                */
     uint32_t rank;
-    uint32_t stripe_height;       /* multiple of 8                                    */
-    uint32_t halo_rows;           /* rows rendered beyond each stripe edge (filter support); 0 = 2 */
+    uint32_t stripe_height;       /* target stripe height in rows                     */
+    uint32_t halo_rows;           /* >= floor(filter radius + 0.5); 0 = 2             */
 } dcrt_film_partition;
 
 /* Traversal work counters of the extension / shadow casts
@@ -332,10 +335,15 @@ DCRT_API int dcrt_tracer_set_frame_params(dcrt_tracer* tracer, const dcrt_frame_
 DCRT_API int dcrt_tracer_set_film_partition(dcrt_tracer* tracer, const dcrt_film_partition* partition);
 /* Render(): run up to max_iterations wavefront iterations (0 = config value). */
 DCRT_API int dcrt_tracer_render(dcrt_tracer* tracer, uint32_t max_iterations);
-/* Render whole images: image s uses frame seed first_seed + s; each completed image is
- * convolved into the film (SampleConvolution) before the next starts. */
+/* Render whole images: image s uses frame seed first_seed + s. Images are path-traced in
+ * batches that share the path pool (new paths of the next image start as soon as slots
+ * are idle); a completed batch is convolved into the film (SampleConvolution) image by
+ * image, in order, so the film is the same as with one image at a time. */
 DCRT_API int dcrt_tracer_render_images(dcrt_tracer* tracer, uint32_t first_seed, uint32_t image_count,
                                        const dcrt_filter_params* filter);
+/* Images per render_images batch (0 = automatic: about twice the path pool's worth of
+ * pixels, at most 16). */
+DCRT_API int dcrt_tracer_set_image_batch(dcrt_tracer* tracer, uint32_t images);
 /* 0 = wavefront (CWavefrontPathTracer, default), 1 = megakernel (CMegakernelPathTracer,
  * MegakernelPathTracing.hlsl) for dcrt_tracer_render_images. */
 DCRT_API int dcrt_tracer_set_mode(dcrt_tracer* tracer, int mode);

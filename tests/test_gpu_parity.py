@@ -167,6 +167,46 @@ def test_film_partition_sums_to_single_gpu(native_lib, golden_luts):
     assert same_bits(total, films[0]).all()
 
 
+def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
+    """render_images in batches (images sharing the path pool) == one image at a time:
+    same film bits, and read_samples returns the last image's samples."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    s = cornell(96, 64, 4)
+    films, samples = [], []
+    for batch in (1, 2, 0):
+        t = WavefrontPathTracer(path_pool_size=1 << 12, debug_rng=True)
+        try:
+            t.set_luts(golden_luts)
+            t.on_scene_loaded(s)
+            t.set_image_batch(batch)
+            t.clear_film()
+            t.render_images(5, 3)
+            films.append(t.read_film())
+            samples.append(t.read_samples())
+        finally:
+            t.destroy()
+    for f in films[1:]:
+        assert same_bits(f, films[0]).all()
+    p_ref, v_ref, _, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(7), oracle_mod.WAVEFRONT)
+    for pos, val in samples:
+        assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
+
+
+def test_partition_rejects_filter_wider_than_halo(native_lib, golden_luts):
+    from directcomputeraytracing_amd import DCRTError, FILTER_BOX, FilterParams, WavefrontPathTracer
+    s = cornell(64, 48, 2)
+    t = WavefrontPathTracer(path_pool_size=1 << 12)
+    try:
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        t.set_film_partition(2, 0, 16, 1)
+        with pytest.raises(DCRTError):
+            t.render_images(0, 1, FilterParams(FILTER_BOX, 2.0, 1.5, 1 / 3, 1 / 3, 3))
+        t.render_images(0, 1, FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3))
+    finally:
+        t.destroy()
+
+
 def test_traversal_counters_match_oracle(native_lib, golden_luts, oracle_mod):
     """Instrumented casts count the same AABB/triangle/BLAS work as the oracle (bytes/ray basis)."""
     from directcomputeraytracing_amd import WavefrontPathTracer

@@ -1,7 +1,7 @@
 """Film partitioning across ranks on CPU with gloo, world size 2.
 
-Each rank path-traces only the 8-row bands of its round-robin stripes plus
-halo (directcomputeraytracing_amd.partition, mirroring dcrt_tracer::BuildBands),
+Each rank path-traces only the rows of its round-robin stripes plus a 1-row
+halo (directcomputeraytracing_amd.partition, mirroring dcrt_tracer::BuildRows),
 convolves only the rows it owns, and one reduce(SUM) of the RGBA32F film
 yields the single-rank film bit for bit. The per-rank rendering here is the
 oracle (no GPU in this container); the GPU path is covered by
@@ -17,22 +17,25 @@ from conftest import GOLDEN, ROOT
 
 
 def test_partition_rows_cover_film():
-    from directcomputeraytracing_amd.partition import owned_rows, render_bands
+    from directcomputeraytracing_amd.partition import owned_rows, render_rows
     H, S = 1080, 64
     for world in (1, 2, 3, 4, 8):
         owners = np.stack([owned_rows(H, world, r, S) for r in range(world)])
         assert np.all(owners.sum(0) == 1)                      # every row owned exactly once
-        for r in range(world):
-            bands = render_bands(H, world, r, S)
-            covered = np.zeros(H, bool)
-            for y in bands:
-                covered[y:y + 8] = True
-            own = np.nonzero(owners[r])[0]
-            for y in own:                                      # owned rows +- 2-row halo rendered
-                assert covered[max(0, y - 2):min(H, y + 3)].all()
-        if world > 1:
-            extra = sum(len(render_bands(H, world, r, S)) for r in range(world)) * 8 / H - 1
-            assert extra < 0.3                                 # halo overhead at S = 64
+        counts = owners.sum(1)
+        assert counts.max() - counts.min() <= max(1, H // (world * S))   # balanced to a row per stripe
+        for halo in (1, 2):
+            total = 0
+            for r in range(world):
+                rows = render_rows(H, world, r, S, halo)
+                assert rows == sorted(set(rows))
+                covered = np.zeros(H, bool)
+                covered[rows] = True
+                for y in np.nonzero(owners[r])[0]:             # owned rows +- halo rendered
+                    assert covered[max(0, y - halo):min(H, y + halo + 1)].all()
+                total += len(rows)
+            if world > 1:
+                assert total / H - 1 < 0.035 * halo            # halo overhead (16 stripes at S = 64)
 
 
 def _free_port():
@@ -52,7 +55,7 @@ def _worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import oracle
     from directcomputeraytracing_amd import FILTER_BOX, FilterParams, Scene, scenes
-    from directcomputeraytracing_amd.partition import owned_row_ranges, render_bands
+    from directcomputeraytracing_amd.partition import owned_row_ranges, render_rows, row_runs
     W, H, S = 96, 80, 16
     s = Scene((W, H))
     scenes.setup_cornell(s, W, H, 3)
@@ -63,10 +66,9 @@ def _worker(rank, world, port, out_dir):
         fr = s.frame_params(seed)
         pos = np.zeros((H, W, 2), np.float32)
         val = np.zeros((H, W, 4), np.float32)
-        for y in render_bands(H, world, rank, S):
-            h = min(8, H - y)
-            p, v, _, _ = oracle.render(s.flat(), luts, fr, oracle.WAVEFRONT, rect=(0, y, W, h), threads=1)
-            pos[y:y + h], val[y:y + h] = p[y:y + h], v[y:y + h]
+        for (y0, y1) in row_runs(render_rows(H, world, rank, S, 1)):
+            p, v, _, _ = oracle.render(s.flat(), luts, fr, oracle.WAVEFRONT, rect=(0, y0, W, y1 - y0), threads=1)
+            pos[y0:y1], val[y0:y1] = p[y0:y1], v[y0:y1]
         for (r0, r1) in owned_row_ranges(H, world, rank, S):
             oracle.sample_convolution(filt, pos, val, film, rows=(r0, r1))
     t = torch.from_numpy(film)

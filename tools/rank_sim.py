@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Weak-scaling rehearsal on one GPU: the per-rank work of bench.py --gpus N, one rank at a time.
+
+At N GPUs a bench step is N images, each rank path-tracing its stripes (+halo) of all N.
+Ranks run independently until the final film reduce, so the N-GPU step time is about the
+slowest rank's time; this times every rank's share on this one GPU and prints, per N, the
+max / mean rank time per step and the implied weak-scaling efficiency vs N = 1.
+
+  python tools/rank_sim.py [--gpus 1,2,4,8] [--steps 8] [--image-batch 0]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--image-batch", type=int, default=0)
+    ap.add_argument("--stripe", type=int, default=64)
+    ap.add_argument("--pool", type=int, default=1 << 21)
+    ap.add_argument("--rank0-only", action="store_true", help="time rank 0's share only (sweeps)")
+    args = ap.parse_args()
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
+    from directcomputeraytracing_amd.partition import halo_for_radius
+    scene = Scene((1920, 1080))
+    scenes.setup_cornell(scene, 1920, 1080, 8)
+    filt = scene.filter_params()
+    base = None
+    for n in [int(x) for x in args.gpus.split(",")]:
+        times = []
+        for r in range(1 if args.rank0_only else n):
+            t = WavefrontPathTracer(path_pool_size=args.pool, iterations_per_render=16)
+            try:
+                t.on_scene_loaded(scene)
+                t.set_image_batch(args.image_batch)
+                if n > 1:
+                    t.set_film_partition(n, r, args.stripe, max(1, halo_for_radius(filt.radius)))
+                t.clear_film()
+                t.render_images(10_000, n, filt)
+                t.synchronize()
+                t0 = time.perf_counter()
+                t.render_images(0, args.steps * n, filt)
+                t.synchronize()
+                times.append((time.perf_counter() - t0) * 1e3 / args.steps)
+            finally:
+                t.destroy()
+        mx, mean = max(times), sum(times) / len(times)
+        base = base or mx
+        print(json.dumps({"n_gpus": n, "ms_per_step_max_rank": round(mx, 3), "ms_per_step_mean_rank": round(mean, 3),
+                          "weak_efficiency": round(base / mx, 3), "image_batch": args.image_batch, "pool": args.pool}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
