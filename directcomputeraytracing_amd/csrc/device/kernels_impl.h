@@ -347,18 +347,22 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         if (__ballot(active) == 0ull) break;
         // phase A: node visits only, until enough lanes are parked at leaves (or
         // enough are idle to refill, or none can advance)
+        // (a lane whose ray ends here only flags it: the result is written once, after
+        // the loop, which keeps the stores out of the unrolled visit steps)
+        bool done = false;
         for (;;) {
 #pragma unroll
             for (int k = 0; k < kVisitsPerCheck; ++k) {
-                if (active && !s.parked && trav_visit<INSTR>(sc, s, f2b, lds, shift, st)) {
-                    emit(item, s);
-                    active = false;
-                }
+                if (active && !done && !s.parked && trav_visit<INSTR>(sc, s, f2b, lds, shift, st)) done = true;
             }
-            const unsigned long long runnable = __ballot(active && !s.parked);
-            const uint32_t parked = (uint32_t)__popcll(__ballot(active && s.parked));
-            const uint32_t idle = (uint32_t)__popcll(__ballot(!active));
+            const unsigned long long runnable = __ballot(active && !done && !s.parked);
+            const uint32_t parked = (uint32_t)__popcll(__ballot(active && !done && s.parked));
+            const uint32_t idle = (uint32_t)__popcll(__ballot(!active || done));
             if (runnable == 0ull || parked >= kParkLanes || (idle >= kRefillLanes && cursor < end)) break;
+        }
+        if (done) {
+            emit(item, s);
+            active = false;
         }
         // phase B: the parked lanes' leaf work, shared by many lanes at once
         if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY>(sc, s, watertight, lds, shift, st)) {
