@@ -44,7 +44,28 @@ struct DeviceScene {
     uint32_t triangleCount;
     uint32_t envCubeSize;
     uint32_t stackSize;           // per-lane traversal stack entries
+    uint32_t cachedNodes;         // nodes [0, cachedNodes) are mirrored in LDS (scene_cache_load)
+    uint32_t cachedTris;          // triVerts of triangles [0, cachedTris) likewise, after the nodes
 };
+
+// LDS scene cache of the traversal kernels: after the per-lane stacks ([stackSize + 1]
+// x blockDim words) the block holds a copy of the first cachedNodes BVH nodes and the
+// first cachedTris pre-gathered triangles (the whole BVH and mesh of a small scene, the
+// TLAS and the first BLAS nodes of a large one), so most node and triangle fetches are
+// ds_read_b128 instead of vector-memory gathers through the texture path.
+DEV float4* scene_cache(const DeviceScene& sc, uint32_t* stackMem, uint32_t shift)
+{
+    return (float4*)(stackMem + ((sc.stackSize + 1u) << shift));
+}
+// Every thread of the block: fill the cache, then a barrier.
+DEV void scene_cache_load(const DeviceScene& sc, uint32_t* stackMem, uint32_t shift)
+{
+    float4* c = scene_cache(sc, stackMem, shift);
+    const uint32_t nn = sc.cachedNodes * 2u, nt = sc.cachedTris * 3u;
+    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) c[i] = sc.nodes[i];
+    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) c[nn + i] = sc.triVerts[i];
+    __syncthreads();
+}
 
 // ---- ray / primitive tests ----------------------------------------------------
 DEV bool ray_aabb(V3 o, V3 inv, float tMin, float tMax, float4 a, float4 b)
@@ -241,8 +262,15 @@ template <bool INSTR>
 DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
-    const float4 a = sc.nodes[s.node * 2];
-    const float4 b = sc.nodes[s.node * 2 + 1];
+    float4 a, b;
+    if (s.node < sc.cachedNodes) {
+        const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
+        a = c[s.node * 2];
+        b = c[s.node * 2 + 1];
+    } else {
+        a = sc.nodes[s.node * 2];
+        b = sc.nodes[s.node * 2 + 1];
+    }
     const bool hit = ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a, b);
     const uint32_t misc = asu(b.w);
     const uint32_t right = asu(b.z);
@@ -311,9 +339,15 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
     const uint32_t end = begin + primOrInst;
     for (uint32_t p = begin; p < end; ++p) {
         if (INSTR) ++st.tris;
-        const float4 q0 = sc.triVerts[(size_t)p * 3];
-        const float4 q1 = sc.triVerts[(size_t)p * 3 + 1];
-        const float4 q2 = sc.triVerts[(size_t)p * 3 + 2];
+        float4 q0, q1, q2;
+        if (p < sc.cachedTris) {
+            const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u;
+            q0 = c[p * 3]; q1 = c[p * 3 + 1]; q2 = c[p * 3 + 2];
+        } else {
+            q0 = sc.triVerts[(size_t)p * 3];
+            q1 = sc.triVerts[(size_t)p * 3 + 1];
+            q2 = sc.triVerts[(size_t)p * 3 + 2];
+        }
         const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
         float t, u, v; bool bf;
         bool h = watertight ? tri_watertight(s.lo, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)

@@ -392,6 +392,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
                                                          Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
+    scene_cache_load(sc, stackMem, block_shift());
     QueueMap qm;
     qmap(cnt, kQExt, &qm);
     TraversalStats st = {0u, 0u, 0u};
@@ -434,6 +435,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
                                                       Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
+    scene_cache_load(sc, stackMem, block_shift());
     QueueMap qm;
     qmap(cnt, kQShadow, &qm);
     const uint32_t n = qm.prefix[kShards];
@@ -467,6 +469,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void cast_kernel(PathPool 
                                                                      Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
+    scene_cache_load(sc, stackMem, block_shift());
     QueueMap qe, qs;
     qmap(cnt, kQExt, &qe);
     qmap(cnt, kQShadow, &qs);
@@ -529,6 +532,7 @@ template <bool OPACITY>
 __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameConstants* fcp, Film film, Globals* g, uint32_t debugRng)
 {
     extern __shared__ uint32_t stackMem[];
+    scene_cache_load(sc, stackMem, block_shift());
     __shared__ uint32_t sm[64];
     const FrameConstants& fc = *fcp;
     const uint32_t lane = threadIdx.x & 63u;
@@ -661,6 +665,7 @@ __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const 
                                                            dcrt_ray_hit* hits, uint32_t* occluded, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
+    scene_cache_load(sc, stackMem, block_shift());
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<ANY, true, false>(
         sc, n, features, 16u, 32u, stackMem + threadIdx.x, block_shift(),

@@ -407,6 +407,18 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     castLds = (size_t)(d.stackSize + 1) * castBlock * 4;
     if (castLds > 65536) { SetLastError("BVH traversal stack too deep for LDS"); return DCRT_E_LIMIT; }
     {
+        // LDS scene cache in what is left of the 32 KiB (5 workgroups per CU, the cast kernels'
+        // register-limited occupancy): BVH nodes first, then pre-gathered triangles
+        const size_t budget = castLds < 32768 ? 32768 - castLds : 0;
+        d.cachedNodes = (uint32_t)std::min<size_t>(s.bvh_node_count, budget / 32);
+        d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
+        if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {   // A/B experiments
+            if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
+        }
+        castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * 48;
+        scene = d;
+    }
+    {
         // The persistent traversal kernels run exactly one resident wave of workgroups.
         hipDeviceProp_t prop;
         HIPCHECK(hipGetDeviceProperties(&prop, device));
