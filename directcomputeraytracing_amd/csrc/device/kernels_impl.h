@@ -267,9 +267,13 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
     }
 }
 
-// Occupancy experiments only (tools/ab_libs.sh): forcing more waves spills the
-// traversal state and measured slower, so by default the compiler chooses.
-#ifdef DCRT_CAST_WAVES_PER_EU
+// Cast-kernel occupancy: 6 waves per SIMD (<= 80 VGPRs; the compiler alone takes ~99,
+// i.e. 4 waves). Measured on the 1080p Cornell bench: 4 waves 5.51, 5 waves 5.46,
+// 6 waves 5.37, 7 waves 5.77 (spills), 8 waves 7.19 ms/spp (tools/ab_libs.sh).
+#ifndef DCRT_CAST_WAVES_PER_EU
+#define DCRT_CAST_WAVES_PER_EU 6
+#endif
+#if DCRT_CAST_WAVES_PER_EU > 0
 #define DCRT_CAST_OCCUPANCY __attribute__((amdgpu_waves_per_eu(DCRT_CAST_WAVES_PER_EU, 8)))
 #else
 #define DCRT_CAST_OCCUPANCY

@@ -407,9 +407,13 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     castLds = (size_t)(d.stackSize + 1) * castBlock * 4;
     if (castLds > 65536) { SetLastError("BVH traversal stack too deep for LDS"); return DCRT_E_LIMIT; }
     {
-        // LDS scene cache in what is left of the 32 KiB (5 workgroups per CU, the cast kernels'
-        // register-limited occupancy): BVH nodes first, then pre-gathered triangles
-        const size_t budget = castLds < 32768 ? 32768 - castLds : 0;
+        // LDS scene cache in what the cast kernel's register-limited occupancy leaves of the
+        // CU's 160 KiB per workgroup: BVH nodes first, then pre-gathered triangles
+        int regPerCU = 0;
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false>, (int)castBlock, castLds));
+        else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, extension_kernel<false, false>, (int)castBlock, castLds));
+        const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
+        const size_t budget = castLds < perBlock ? perBlock - castLds : 0;
         d.cachedNodes = (uint32_t)std::min<size_t>(s.bvh_node_count, budget / 32);
         d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
         if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {   // A/B experiments
