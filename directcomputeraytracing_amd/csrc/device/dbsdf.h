@@ -283,14 +283,51 @@ DEV DielectricMs dielectric_ms(const DeviceScene& s, float cosThetaO, float alph
     return d;
 }
 
-DEV V3 evaluate_bsdf(const DeviceScene& s, bool vndf, V3 wiW, V3 woW, const Intersection& it)
+// Per-hit BSDF frame shared by EvaluateBSDF, EvaluateBSDFPdf and SampleBSDF of one
+// MATERIAL step (same intersection, same wo): the shading basis, wo in it, and the
+// LUT terms that depend only on (cos(theta_o), alpha, ior). Each is the value the
+// three functions computed on their own, so sharing them changes no bit; it saves the
+// repeated basis transform and, above all, the repeated dependent LUT fetches.
+struct BsdfFrame {
+    V3 b, wo;            // bitangent; wo in (tangent, b, normal), z made >= 0
+    bool inv;            // wo was below the shading surface
+    bool any;            // !inv || two-sided
+    float E, Eavg;       // lut_brdf / lut_brdf_avg (multiscattering plastic / conductor)
+    float diel;          // lut_brdf_dielectric (plastic)
+    V3 isf;              // isf_factor (plastic)
+    DielectricMs dms;    // dielectric_ms (multiscattering rough dielectric)
+};
+DEV BsdfFrame bsdf_frame(const DeviceScene& s, V3 woW, const Intersection& it)
 {
-    const V3 b = cross(it.normal, it.tangent);
-    V3 wo = to_tbn(woW, it.tangent, b, it.normal);
-    V3 wi = to_tbn(wiW, it.tangent, b, it.normal);
-    const bool inv = wo.z < 0.0f;
-    if (inv) { wo.z = -wo.z; wi.z = -wi.z; }
-    const float cosO = wo.z;
+    BsdfFrame f;
+    f.b = cross(it.normal, it.tangent);
+    f.wo = to_tbn(woW, it.tangent, f.b, it.normal);
+    f.inv = f.wo.z < 0.0f;
+    if (f.inv) f.wo.z = -f.wo.z;
+    f.any = !f.inv || it.isTwoSided;
+    const float cosO = f.wo.z;
+    const uint32_t type = it.materialType;
+    f.E = 0.0f; f.Eavg = 0.0f; f.diel = 0.0f; f.isf = mk(1.0f, 1.0f, 1.0f);
+    f.dms.E = 0.0f; f.dms.Eavg = 0.0f; f.dms.EinvAvg = 0.0f; f.dms.ratio = 0.0f;
+    if (it.multiscattering && (type == DCRT_MATERIAL_TYPE_PLASTIC || type == DCRT_MATERIAL_TYPE_CONDUCTOR) && f.any) {
+        f.E = lut_brdf(s, cosO, it.alpha);
+        f.Eavg = lut_brdf_avg(s, it.alpha);
+    }
+    if (type == DCRT_MATERIAL_TYPE_PLASTIC && f.any) {
+        f.diel = lut_brdf_dielectric(s, cosO, it.alpha, it.ior.x, false);
+        f.isf = isf_factor(s, it.alpha, it.albedo, it.ior.x, it.internalScatteringMode);
+    }
+    if (type == DCRT_MATERIAL_TYPE_DIELECTRIC && it.multiscattering && !(it.alpha < kAlphaThreshold))
+        f.dms = dielectric_ms(s, cosO, it.alpha, it.ior.x, f.inv);
+    return f;
+}
+
+DEV V3 evaluate_bsdf(const DeviceScene& s, bool vndf, V3 wiW, const BsdfFrame& f, const Intersection& it)
+{
+    const V3 wo = f.wo;
+    V3 wi = to_tbn(wiW, it.tangent, f.b, it.normal);
+    const bool inv = f.inv;
+    if (inv) wi.z = -wi.z;
     LCtx c;
     calc_h(wo, wi, c);
     const bool smooth = it.alpha < kAlphaThreshold;
@@ -298,24 +335,21 @@ DEV V3 evaluate_bsdf(const DeviceScene& s, bool vndf, V3 wiW, V3 woW, const Inte
     const uint32_t type = it.materialType;
     if (type != DCRT_MATERIAL_TYPE_DIELECTRIC && type != DCRT_MATERIAL_TYPE_THIN_DIELECTRIC) {
         bool hasL = false, hasCT = false, hasMS = false, dielF = false;
-        float ratioL = 0.0f, E = 0.0f, Eavg = 0.0f;
+        float ratioL = 0.0f;
+        const float E = f.E, Eavg = f.Eavg;
         V3 Fms = mk(0.0f, 0.0f, 0.0f), isf = mk(1.0f, 1.0f, 1.0f);
-        const bool any = !inv || it.isTwoSided;
-        if (it.multiscattering && (type == DCRT_MATERIAL_TYPE_PLASTIC || type == DCRT_MATERIAL_TYPE_CONDUCTOR) && any && !smooth) {
-            E = lut_brdf(s, cosO, it.alpha);
-            Eavg = lut_brdf_avg(s, it.alpha);
-        }
+        const bool any = f.any;
         if (type == DCRT_MATERIAL_TYPE_DIFFUSE && any) {
             hasL = true; ratioL = 1.0f;
         } else if (type == DCRT_MATERIAL_TYPE_PLASTIC && any) {
             hasL = true; hasCT = !smooth; hasMS = it.multiscattering && !smooth; dielF = true;
-            ratioL = 1.0f - lut_brdf_dielectric(s, cosO, it.alpha, it.ior.x, false);
+            ratioL = 1.0f - f.diel;
             if (hasMS) {
-                const float f = ms_fresnel(Eavg, favg_dielectric(it.ior.x));
-                Fms = splat(f);
+                const float fm = ms_fresnel(Eavg, favg_dielectric(it.ior.x));
+                Fms = splat(fm);
                 ratioL = fmaxf(ratioL - Fms.x * (1.0f - E), 0.0f);
             }
-            isf = isf_factor(s, it.alpha, it.albedo, it.ior.x, it.internalScatteringMode);
+            isf = f.isf;
         } else if (type == DCRT_MATERIAL_TYPE_CONDUCTOR && any && !smooth) {
             hasCT = true; hasMS = it.multiscattering;
             if (hasMS) {
@@ -335,21 +369,19 @@ DEV V3 evaluate_bsdf(const DeviceScene& s, bool vndf, V3 wiW, V3 woW, const Inte
         const float etaO = inv ? it.ior.x : 1.0f, etaI = inv ? 1.0f : it.ior.x;
         value = value + splat(ct_bsdf<false>(wi, wo, it.alpha, etaO, etaI));
         if (it.multiscattering) {
-            const DielectricMs d = dielectric_ms(s, cosO, it.alpha, it.ior.x, inv);
+            const DielectricMs& d = f.dms;
             value = value + splat(ct_ms_bsdf(s, wi, it.alpha, d.ratio, it.ior.x, d.E, d.Eavg, d.EinvAvg, inv));
         }
     }
     return value;
 }
 
-DEV float evaluate_bsdf_pdf(const DeviceScene& s, bool vndf, V3 wiW, V3 woW, const Intersection& it)
+DEV float evaluate_bsdf_pdf(const DeviceScene& s, bool vndf, V3 wiW, const BsdfFrame& f, const Intersection& it)
 {
-    const V3 b = cross(it.normal, it.tangent);
-    V3 wo = to_tbn(woW, it.tangent, b, it.normal);
-    V3 wi = to_tbn(wiW, it.tangent, b, it.normal);
-    const bool inv = wo.z < 0.0f;
-    if (inv) { wo.z = -wo.z; wi.z = -wi.z; }
-    const float cosO = wo.z;
+    const V3 wo = f.wo;
+    V3 wi = to_tbn(wiW, it.tangent, f.b, it.normal);
+    const bool inv = f.inv;
+    if (inv) wi.z = -wi.z;
     LCtx c;
     calc_h(wo, wi, c);
     const bool smooth = it.alpha < kAlphaThreshold;
@@ -358,16 +390,16 @@ DEV float evaluate_bsdf_pdf(const DeviceScene& s, bool vndf, V3 wiW, V3 woW, con
     if (type != DCRT_MATERIAL_TYPE_DIELECTRIC && type != DCRT_MATERIAL_TYPE_THIN_DIELECTRIC) {
         bool hasL = false, hasCT = false, hasMS = false;
         float wl = 0.0f, wct = 0.0f, wms = 0.0f;
-        const bool any = !inv || it.isTwoSided;
+        const bool any = f.any;
         if (type == DCRT_MATERIAL_TYPE_DIFFUSE && any) {
             hasL = true; wl = 1.0f;
         } else if (type == DCRT_MATERIAL_TYPE_PLASTIC && any) {
             hasL = true; hasCT = !smooth; hasMS = it.multiscattering && !smooth;
-            wct = lut_brdf_dielectric(s, cosO, it.alpha, it.ior.x, false);
+            wct = f.diel;
             wl = 1.0f - wct;
             if (hasMS) {
-                const float E = lut_brdf(s, cosO, it.alpha);
-                const float Eavg = lut_brdf_avg(s, it.alpha);
+                const float E = f.E;
+                const float Eavg = f.Eavg;
                 const float Fms = ms_fresnel(Eavg, favg_dielectric(it.ior.x));
                 wms = Fms * (1.0f - E);
                 wl = fmaxf(wl - wms, 0.0f);
@@ -384,7 +416,7 @@ DEV float evaluate_bsdf_pdf(const DeviceScene& s, bool vndf, V3 wiW, V3 woW, con
         float wb = 1.0f, wms = 0.0f, ratio = 0.0f;
         const float etaO = inv ? it.ior.x : 1.0f, etaI = inv ? 1.0f : it.ior.x;
         if (it.multiscattering) {
-            const DielectricMs d = dielectric_ms(s, cosO, it.alpha, it.ior.x, inv);
+            const DielectricMs& d = f.dms;
             ratio = d.ratio;
             wb = d.E; wms = 1.0f - d.E;
         }
@@ -394,43 +426,38 @@ DEV float evaluate_bsdf_pdf(const DeviceScene& s, bool vndf, V3 wiW, V3 woW, con
     return pdf;
 }
 
-DEV void sample_bsdf(const DeviceScene& s, bool vndf, V3 woW, float sx, float sy, float sel, const Intersection& it,
+DEV void sample_bsdf(const DeviceScene& s, bool vndf, const BsdfFrame& f, float sx, float sy, float sel, const Intersection& it,
                      V3* wiOut, V3* valueOut, float* pdfOut, bool* isDelta)
 {
     V3 wi = mk(0.0f, 0.0f, 0.0f), value = mk(0.0f, 0.0f, 0.0f);
     float pdf = 0.0f;
     *isDelta = false;
-    const V3 b = cross(it.normal, it.tangent);
-    V3 wo = to_tbn(woW, it.tangent, b, it.normal);
-    const bool inv = wo.z < 0.0f;
-    if (inv) wo.z = -wo.z;
-    const float cosO = wo.z;
+    const V3 b = f.b;
+    const V3 wo = f.wo;
+    const bool inv = f.inv;
     LCtx c;
     c.H = mk(0.0f, 0.0f, 0.0f); c.WOdotH = 0.0f;
     const bool smooth = it.alpha < kAlphaThreshold;
     const uint32_t type = it.materialType;
     if (type != DCRT_MATERIAL_TYPE_DIELECTRIC && type != DCRT_MATERIAL_TYPE_THIN_DIELECTRIC) {
         bool hasL = false, hasCT = false, hasMS = false, dielF = false;
-        float wl = 0.0f, wct = 0.0f, wms = 0.0f, E = 0.0f, Eavg = 0.0f;
+        float wl = 0.0f, wct = 0.0f, wms = 0.0f;
+        const float E = f.E, Eavg = f.Eavg;
         V3 Fms = mk(0.0f, 0.0f, 0.0f), isf = mk(1.0f, 1.0f, 1.0f);
-        const bool any = !inv || it.isTwoSided;
-        if (it.multiscattering && (type == DCRT_MATERIAL_TYPE_PLASTIC || type == DCRT_MATERIAL_TYPE_CONDUCTOR) && any) {
-            E = lut_brdf(s, cosO, it.alpha);
-            Eavg = lut_brdf_avg(s, it.alpha);
-        }
+        const bool any = f.any;
         if (type == DCRT_MATERIAL_TYPE_DIFFUSE && any) {
             hasL = true; wl = 1.0f;
         } else if (type == DCRT_MATERIAL_TYPE_PLASTIC && any) {
             hasL = true; hasCT = true; hasMS = it.multiscattering && !smooth; dielF = true;
-            wct = lut_brdf_dielectric(s, cosO, it.alpha, it.ior.x, false);
+            wct = f.diel;
             wl = 1.0f - wct;
             if (hasMS) {
-                const float f = ms_fresnel(Eavg, favg_dielectric(it.ior.x));
-                Fms = splat(f);
+                const float fm = ms_fresnel(Eavg, favg_dielectric(it.ior.x));
+                Fms = splat(fm);
                 wms = Fms.x * (1.0f - E);
                 wl = fmaxf(wl - wms, 0.0f);
             }
-            isf = isf_factor(s, it.alpha, it.albedo, it.ior.x, it.internalScatteringMode);
+            isf = f.isf;
         } else if (type == DCRT_MATERIAL_TYPE_CONDUCTOR && any) {
             hasCT = true; hasMS = it.multiscattering && !smooth;
             wct = 1.0f;
@@ -486,10 +513,9 @@ DEV void sample_bsdf(const DeviceScene& s, bool vndf, V3 woW, float sx, float sy
         *isDelta = true;
     } else {
         float wb = 1.0f, wms = 0.0f;
-        DielectricMs d; d.E = 0.0f; d.Eavg = 0.0f; d.EinvAvg = 0.0f; d.ratio = 0.0f;
+        const DielectricMs& d = f.dms;
         const float etaO = inv ? it.ior.x : 1.0f, etaI = inv ? 1.0f : it.ior.x;
         if (it.multiscattering) {
-            d = dielectric_ms(s, cosO, it.alpha, it.ior.x, inv);
             wb = d.E; wms = 1.0f - d.E;
         }
         if (sel < wb) {

@@ -213,12 +213,13 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             terminate = true;
         } else {
             const V3 wo = -dir;
+            const BsdfFrame bf = bsdf_frame(sc, wo, it);
             if (fc->lightCount != 0) {
                 const LightSample ls = sample_light(sc, it.position, fc->lightCount, rng);
                 if (any_pos(ls.radiance) && ls.pdf > 0.0f) {
-                    const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, wo, it);
+                    const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, bf, it);
                     const float NdotWI = fabsf(dot(it.normal, ls.wi));
-                    const float bsdfPdf = evaluate_bsdf_pdf(sc, vndf, ls.wi, wo, it);
+                    const float bsdfPdf = evaluate_bsdf_pdf(sc, vndf, ls.wi, bf, it);
                     const float weight = ls.isDelta ? 1.0f : power_heuristic(ls.pdf, bsdfPdf);
                     lsr = T * ls.radiance * bsdf * NdotWI * weight / ls.pdf;
                     const V3 so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                 const float sel = next1(rng);
                 const float sx = next1(rng), sy = next1(rng);
                 V3 wi, bsdf;
-                sample_bsdf(sc, vndf, wo, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
+                sample_bsdf(sc, vndf, bf, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
                 if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
                     const float NdotWI = fabsf(dot(it.normal, wi));
                     T = T * bsdf * NdotWI / bsdfPdf;
@@ -606,6 +607,7 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
             }
             if (bounce > fc.maxBounce || !hasHit) break;
             const V3 wo = -rd;
+            const BsdfFrame bf = bsdf_frame(sc, wo, it);
             V3 lsr = mk(0.0f, 0.0f, 0.0f);
             bool hasShadow = false;
             V3 so = mk(0.0f, 0.0f, 0.0f), sd = so;
@@ -613,9 +615,9 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
             if (fc.lightCount != 0) {
                 const LightSample ls = sample_light(sc, it.position, fc.lightCount, rng);
                 if (any_pos(ls.radiance) && ls.pdf > 0.0f) {
-                    const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, wo, it);
+                    const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, bf, it);
                     const float NdotWI = fabsf(dot(it.normal, ls.wi));
-                    const float bsdfPdf = evaluate_bsdf_pdf(sc, vndf, ls.wi, wo, it);
+                    const float bsdfPdf = evaluate_bsdf_pdf(sc, vndf, ls.wi, bf, it);
                     const float weight = ls.isDelta ? 1.0f : power_heuristic(ls.pdf, bsdfPdf);
                     lsr = T * ls.radiance * bsdf * NdotWI * weight / ls.pdf;
                     so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
@@ -633,7 +635,7 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
                 V3 wi, bsdf;
                 float bsdfPdf = 0.0f;
                 bool isDelta = false;
-                sample_bsdf(sc, vndf, wo, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
+                sample_bsdf(sc, vndf, bf, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
                 if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
                     const float NdotWI = fabsf(dot(it.normal, wi));
                     T = T * bsdf * NdotWI / bsdfPdf;
