@@ -95,22 +95,22 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
     const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
     const bool terminate = (flags & kFlagTerminate) != 0;
     uint32_t bounce = flags & 0xFFu;
-    if (!idle) {
+    // Li += light sampling result unless the shadow ray hit (:520-528). For a live path
+    // MATERIAL does this addition as its first step (same operands, same bits), so the
+    // path's Li is read and written once per iteration; the shadow-hit bit is carried.
+    if (!idle && terminate) {
         float4 li = pool.li[tid];
         const float4 lsr = pool.lsr[tid];
         li.x = li.x + (!shadowHit ? lsr.x : 0.0f);
         li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
         li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
-        if (terminate) {
-            const size_t p = pool.pixel[tid];
-            film.samplePosition[p] = pool.pixelSample[tid];
-            film.sampleValue[p] = make_float4(li.x, li.y, li.z, 0.0f);
-            if (debugRng) film.debugRng[p] = pool.rng[tid];
-            idle = true;
-        } else {
-            pool.li[tid] = li;
-        }
+        const size_t p = pool.pixel[tid];
+        film.samplePosition[p] = pool.pixelSample[tid];
+        film.sampleValue[p] = make_float4(li.x, li.y, li.z, 0.0f);
+        if (debugRng) film.debugRng[p] = pool.rng[tid];
+        idle = true;
     }
+    const bool carryShadowHit = !idle && shadowHit;
     const uint32_t mslot = block_append(!idle, qctr(cnt, kQMaterial, shard), sm);
     if (!idle) pool.materialQueue[(size_t)shard * pool.size + mslot] = tid;
 
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, 
     }
     const uint32_t eslot = block_append(newPath, qctr(cnt, kQExt, shard), sm);
     if (newPath) pool.extQueue[(size_t)shard * pool.size + eslot] = tid;
-    pool.flags[tid] = (idle ? kFlagIdle : 0u) | (bounce & 0xFFu);
+    pool.flags[tid] = (idle ? kFlagIdle : 0u) | (carryShadowHit ? kFlagShadowRayHit : 0u) | (bounce & 0xFFu);
     }
 }
 
@@ -184,6 +184,14 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         float4 thr = pool.throughput[path];
         float4 li = pool.li[path];
         uint32_t flags = pool.flags[path];
+        {
+            // CONTROL's Li += light sampling result (:520-528), done here for live paths
+            const float4 lsr0 = pool.lsr[path];
+            const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
+            li.x = li.x + (!shadowHit ? lsr0.x : 0.0f);
+            li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
+            li.z = li.z + (!shadowHit ? lsr0.z : 0.0f);
+        }
         const uint32_t bounce = flags & 0xFFu;
         const uint32_t features = fc->features;
         const bool vndf = (features & DCRT_FEATURE_GGX_SAMPLE_VNDF) != 0;
