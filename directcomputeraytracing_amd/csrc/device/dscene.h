@@ -293,10 +293,14 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds
     s.node = descend ? nearChild : (pop ? (top & 0x7FFFFFFFu) : s.node);
     s.count = descend ? s.count + 1u : (pop ? s.count - 1u : s.count);
     s.inBlas = pop ? popBlas : s.inBlas;
-    s.lo = mk(restore ? s.o.x : s.lo.x, restore ? s.o.y : s.lo.y, restore ? s.o.z : s.lo.z);
-    s.ld = mk(restore ? s.d.x : s.ld.x, restore ? s.d.y : s.ld.y, restore ? s.d.z : s.ld.z);
-    s.inv = mk(restore ? s.invW.x : s.inv.x, restore ? s.invW.y : s.inv.y, restore ? s.invW.z : s.inv.z);
-    s.shearValid = s.shearValid && !restore;
+    // rare (about once per ray): a branch the wave skips when no lane restores; as
+    // selects it cost nine v_cndmask per visit (measured 2.5 % of the cast kernel)
+    if (__builtin_expect(restore, 0)) {
+        s.lo = mk(s.o.x, s.o.y, s.o.z);
+        s.ld = mk(s.d.x, s.d.y, s.d.z);
+        s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+        s.shearValid = false;
+    }
     s.parked = hit && leaf;
     s.leafRef = right;
     s.leafMisc = misc;
