@@ -45,6 +45,12 @@ def main():
             life = (s1 - s0) / 100.0
             ends = np.percentile((s1 - t0) / 100.0, [50, 90, 99, 100])
             starts = np.percentile((s0 - t0) / 100.0, [50, 99, 100])
+            # per-XCD view: workgroup b runs on XCD b % 8 (4 waves per workgroup)
+            wid = np.nonzero(valid)[0]
+            xcd = (wid // 4) % 8
+            endx = [(s1[xcd == x] - t0).mean() / 100.0 for x in range(8)]
+            life_x = [((s1 - s0)[xcd == x]).mean() / 100.0 for x in range(8)]
+            print("        mean end per XCD", " ".join(f"{e:6.1f}" for e in endx), "| mean life", " ".join(f"{e:6.1f}" for e in life_x))
             print(f"{name:6s} it{it:2d} waves {valid.sum():5d} items {int(items[k, it][valid].sum()):8d} span {span:7.1f}us "
                   f"residency {life.mean() / span:5.2f} start p50/p99/max {starts[0]:5.1f}/{starts[1]:5.1f}/{starts[2]:5.1f} "
                   f"end p50/p90/p99/max {ends[0]:6.1f}/{ends[1]:6.1f}/{ends[2]:6.1f}/{ends[3]:6.1f}")
