@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=8)
-    ap.add_argument("--pool", type=int, default=1 << 21, help="path pool slots")
+    ap.add_argument("--pool", type=int, default=1 << 24,
+                    help="path pool slots (2^24 = 8 images of 1080p in flight: one drain per batch, not per image)")
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
     ap.add_argument("--image-batch", type=int, default=0, help="images per wavefront batch (0 = automatic)")

@@ -42,6 +42,7 @@ namespace {
 
 constexpr uint32_t kDefaultPoolSize = 1u << 20;      // 2^20 slots: 16 waves x 256 CUs x 256 (MI355X)
 constexpr uint32_t kDefaultIterations = 8;
+constexpr uint32_t kMaxImageBatch = 64;               // images in flight per RenderImages batch (sample textures: 24 B/px each)
 constexpr uint32_t kControlBlock = 256;
 constexpr uint32_t kMaterialBlock = 256;
 constexpr uint32_t kMaxPersistentBlocks = 256 * 8;   // CUs x resident workgroups
@@ -488,13 +489,16 @@ int dcrt_tracer::EnsureSamples(uint32_t images)
 // Images per RenderImages batch: as many as the path pool holds at once, so that a rank
 // of a partitioned film (a fraction of every image) still runs full wavefronts. A batch
 // that overflows the pool by a little is avoided: its last pixel blocks would start only
-// when the first paths end and stretch the batch by a whole path length.
+// when the first paths end and stretch the batch by a whole path length. Every batch ends
+// in a drain (iterations with a shrinking path population), so large pools and batches of
+// many images amortise it: a rank of an N-GPU film renders 1/N of each image, and gets N
+// times as many images per batch.
 uint32_t dcrt_tracer::AutoBatch(uint32_t count) const
 {
     uint32_t b = batchImages;
     if (b == 0) {
         const uint64_t pixels = std::max<uint64_t>(1, (uint64_t)rowCount * filmW);
-        b = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, poolSize / pixels));
+        b = (uint32_t)std::min<uint64_t>(kMaxImageBatch, std::max<uint64_t>(1, poolSize / pixels));
     }
     return std::max<uint32_t>(1, std::min(b, count));
 }
@@ -1158,7 +1162,7 @@ DCRT_API int dcrt_tracer_trace_rays_device(dcrt_tracer* t, const void* d_rays, u
 DCRT_API int dcrt_tracer_set_image_batch(dcrt_tracer* t, uint32_t images)
 {
     TRACER_GUARD(t);
-    if (images > 64) { SetLastError("image batch too large (max 64)"); return DCRT_E_INVALID_ARG; }
+    if (images > kMaxImageBatch) { SetLastError("image batch too large (max 64)"); return DCRT_E_INVALID_ARG; }
     t->batchImages = images;
     return DCRT_OK;
 }

@@ -49,7 +49,8 @@ def run(name, args):
     scene, desc = setup(name, Path(args.scene_dir), args.small)
     load_s = time.perf_counter() - t0
     W, H = scene.resolution
-    pool = 1 << 21 if W * H <= (1 << 21) else 1 << 23
+    # several images in flight (an image batch), so each batch drains once: 8 images at 1080p, 8 at 4K
+    pool = args.pool or (1 << 24 if W * H <= (1 << 21) else 1 << 26)
     tr = WavefrontPathTracer(path_pool_size=pool, iterations_per_render=16)
     try:
         tr.on_scene_loaded(scene)
@@ -77,17 +78,22 @@ def run(name, args):
         tr.set_instrumentation(False, False)
         ext_bytes = (56 * cr["extension_rays"] + 32 * st["ext_node_visits"] + 48 * st["ext_triangle_tests"]
                      + 56 * st["ext_blas_entries"])
-        achieved = ext_bytes / (tm["ext_kernel_ms"] * 1e-3) / 1e9
+        shadow_bytes = (44 * cr["shadow_rays"] + 32 * st["shadow_node_visits"] + 48 * st["shadow_triangle_tests"]
+                        + 56 * st["shadow_blas_entries"])
+        # the timed launch is the merged EXTENSION+SHADOW cast kernel (as in bench.py)
+        achieved = (ext_bytes + shadow_bytes) / (tm["ext_kernel_ms"] * 1e-3) / 1e9
         info = scene.bvh_info()
-        return {"config": name, "workload": desc, "resolution": [W, H], "spp": args.spp,
+        return {"config": name, "workload": desc, "resolution": [W, H], "spp": args.spp, "path_pool": pool,
                 "value": round(rays / el / 1e6, 1), "unit": "Mrays/s", "ms_per_spp": round(el * 1e3 / args.spp, 2),
                 "rays_per_spp": int(rays / args.spp), "triangles_bvh_nodes": info["total_nodes"],
                 "scene_load_s": round(load_s, 2),
-                "roofline": {"kernel": "extension_kernel", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "roofline": {"kernel": "cast_kernel (EXTENSION_RAY_CAST + SHADOW_RAY_CAST)", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                              "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                              "avg_launch_us": round(tm["ext_kernel_ms"] * 1e3 / max(1, tm["ext_launches"]), 1),
                              "nodes_per_ray": round(st["ext_node_visits"] / max(1, cr["extension_rays"]), 2),
-                             "tris_per_ray": round(st["ext_triangle_tests"] / max(1, cr["extension_rays"]), 2)}}
+                             "tris_per_ray": round(st["ext_triangle_tests"] / max(1, cr["extension_rays"]), 2),
+                             "blas_per_ray": round(st["ext_blas_entries"] / max(1, cr["extension_rays"]), 2),
+                             "shadow_nodes_per_ray": round(st["shadow_node_visits"] / max(1, cr["shadow_rays"]), 2)}}
     finally:
         tr.destroy()
 
@@ -98,6 +104,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--configs", default="cornell,coffee,spaceship,lamp")
     ap.add_argument("--scene-dir", default="/tmp/dcrt_scenes")
+    ap.add_argument("--pool", type=int, default=0, help="path pool slots (0: 2^24 at 1080p, 2^26 at 4K)")
     ap.add_argument("--small", action="store_true", help="small meshes (CI smoke)")
     args = ap.parse_args()
     for name in args.configs.split(","):
