@@ -44,7 +44,8 @@ def parse():
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
     ap.add_argument("--image-batch", type=int, default=0, help="images per wavefront batch (0 = automatic)")
-    ap.add_argument("--roofline-images", type=int, default=4)
+    ap.add_argument("--roofline-images", type=int, default=0,
+                    help="images of the roofline leg (0 = the timed images, so its launches are the timed region's)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) or gloo (CPU reduce, for tests)")
     ap.add_argument("--save-film", default=None, help="rank 0 writes the reduced RGBA32F film (.npy)")
     ap.add_argument("--mode", choices=["wavefront", "megakernel"], default="wavefront",
@@ -175,7 +176,7 @@ def main():
         np.save(args.save_film, film.reshape(args.height, args.width, 4))
 
     # ---- roofline leg: same workload (seeds 0..R-1), counters then HIP-event timing
-    R = max(1, args.roofline_images)
+    R = max(1, args.roofline_images or images)
     tracer.set_instrumentation(True, False)
     tracer.reset_stats()
     tracer.render_images(0, R, filt)

@@ -7,14 +7,16 @@ OUT="$ROOTDIR/gpurun_out/prof"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS="--steps ${PROF_STEPS:-16} --warmup 1 --roofline-images 2 --no-cpu-baseline ${PROF_ARGS:-}"
+# no warmup: every cast launch of the run is then one of the 64-image workload the bench's
+# roofline leg times, so the kernel-stats average is comparable with roofline.avg_launch_us
+ARGS="--steps ${PROF_STEPS:-64} --warmup 0 --no-cpu-baseline ${PROF_ARGS:-}"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$OUT" -o trace -- \
     python3 "$ROOTDIR/bench.py" $ARGS > "$OUT/trace_bench.log" 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 if [ -n "${PMC:-}" ]; then
   for ctr in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum; do
     timeout -k 10 400 rocprofv3 --pmc $ctr --kernel-trace -f csv -d "$OUT" -o pmc_$ctr -- \
-        python3 "$ROOTDIR/bench.py" --steps 2 --warmup 1 --roofline-images 1 --no-cpu-baseline ${PROF_ARGS:-} \
+        python3 "$ROOTDIR/bench.py" $ARGS \
         > "$OUT/pmc_${ctr}.log" 2>&1
     rc=$?; echo "pmc $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
