@@ -499,6 +499,10 @@ uint32_t dcrt_tracer::AutoBatch(uint32_t count) const
     if (b == 0) {
         const uint64_t pixels = std::max<uint64_t>(1, (uint64_t)rowCount * filmW);
         b = (uint32_t)std::min<uint64_t>(kMaxImageBatch, std::max<uint64_t>(1, poolSize / pixels));
+        // equal batches: as many batches as the cap needs, each as large as the others (a
+        // small last batch would pay a whole drain for a sparse wavefront)
+        const uint32_t batches = (count + b - 1) / b;
+        b = (count + batches - 1) / batches;
     }
     return std::max<uint32_t>(1, std::min(b, count));
 }

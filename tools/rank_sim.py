@@ -34,7 +34,7 @@ def main():
     filt = scene.filter_params()
     base = None
     for n in [int(x) for x in args.gpus.split(",")]:
-        times = []
+        times, rays, iters = [], [], []
         for r in range(1 if args.rank0_only else n):
             t = WavefrontPathTracer(path_pool_size=args.pool, iterations_per_render=16)
             try:
@@ -45,16 +45,23 @@ def main():
                 t.clear_film()
                 t.render_images(10_000, n, filt)
                 t.synchronize()
+                t.reset_stats()
                 t0 = time.perf_counter()
                 t.render_images(0, args.steps * n, filt)
                 t.synchronize()
                 times.append((time.perf_counter() - t0) * 1e3 / args.steps)
+                c = t.counters()
+                rays.append((c["extension_rays"] + c["shadow_rays"]) / args.steps)
+                iters.append(c.get("iterations", 0) / args.steps)
             finally:
                 t.destroy()
         mx, mean = max(times), sum(times) / len(times)
         base = base or mx
         print(json.dumps({"n_gpus": n, "ms_per_step_max_rank": round(mx, 3), "ms_per_step_mean_rank": round(mean, 3),
-                          "weak_efficiency": round(base / mx, 3), "image_batch": args.image_batch, "pool": args.pool}), flush=True)
+                          "weak_efficiency": round(base / mx, 3), "image_batch": args.image_batch, "pool": args.pool,
+                          "mrays_per_step_mean_rank": round(sum(rays) / len(rays) / 1e6, 3),
+                          "ns_per_ray_mean_rank": round(mean * 1e6 / (sum(rays) / len(rays)), 4),
+                          "iterations_per_step_mean_rank": round(sum(iters) / len(iters), 2)}), flush=True)
 
 
 if __name__ == "__main__":
