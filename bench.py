@@ -19,6 +19,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -43,6 +44,8 @@ def parse():
                     help="path pool slots (2^24 = 8 images of 1080p in flight: one drain per batch, not per image)")
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="concurrent wavefront pipelines per GPU (film partitions on their own streams)")
     ap.add_argument("--image-batch", type=int, default=0, help="images per wavefront batch (0 = automatic)")
     ap.add_argument("--roofline-images", type=int, default=0,
                     help="images of the roofline leg (0 = the timed images, so its launches are the timed region's)")
@@ -114,21 +117,52 @@ def main():
 
     scene = Scene((args.width, args.height))
     scenes.setup_cornell(scene, args.width, args.height, args.bounces)
-    tracer = WavefrontPathTracer(path_pool_size=args.pool, iterations_per_render=args.iterations, device=device)
-    tracer.on_scene_loaded(scene)
-    tracer.set_mode(args.mode)
-    tracer.set_image_batch(args.image_batch)
     filt = scene.filter_params()
-    if world > 1:
-        from directcomputeraytracing_amd.partition import halo_for_radius
-        tracer.set_film_partition(world, rank, args.stripe, max(1, halo_for_radius(filt.radius)))
+    from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
+    halo = max(1, halo_for_radius(filt.radius))
+
+    def make_tracer(pool, part):
+        t = WavefrontPathTracer(path_pool_size=pool, iterations_per_render=args.iterations, device=device)
+        t.on_scene_loaded(scene)
+        t.set_mode(args.mode)
+        t.set_image_batch(args.image_batch)
+        if part is not None:
+            t.set_film_partition(*part, halo)
+        return t
+
+    # K concurrent pipelines per GPU (--streams): tracer s renders the rank's stripes dealt
+    # to it (partition.stream_partition), on its own stream, from its own host thread; the
+    # K films have disjoint supports and are summed on the device (add_film_device).
+    K = max(1, args.streams)
+    tracers = []
+    for s_ in range(K):
+        part = stream_partition(args.height, world, rank, K, s_, args.stripe) if (K > 1 or world > 1) else None
+        tracers.append(make_tracer(args.pool // K, part))
+    tracer = tracers[0]
+
+    def render_all(first, count):
+        if K == 1:
+            tracer.render_images(first, count, filt)
+            return
+        th = [threading.Thread(target=t.render_images, args=(first, count, filt)) for t in tracers]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
 
     def barrier_sync():
-        tracer.synchronize()
+        for t in tracers:
+            t.synchronize()
         if dist is not None:
             import torch
             torch.cuda.synchronize()
             dist.barrier()
+
+    def combine_films():
+        # the K pipelines' films into tracer 0's (disjoint supports: bit-exact sum)
+        for t in tracers[1:]:
+            t.synchronize()
+            tracer.add_film_device(t.film_device_ptr())
 
     film_buf = None
     on_device = args.dist_backend == "nccl"
@@ -146,28 +180,33 @@ def main():
         dist.reduce(film_buf, dst=0, op=dist.ReduceOp.SUM)
 
     # warmup (also builds the graphs)
-    tracer.clear_film()
+    for t in tracers:
+        t.clear_film()
     if args.warmup:
-        tracer.render_images(10_000, args.warmup, filt)
-    tracer.clear_film()
-    tracer.reset_stats()
+        render_all(10_000, args.warmup)
+    for t in tracers:
+        t.clear_film()
+        t.reset_stats()
     barrier_sync()
     t0 = time.perf_counter()
     images = args.steps * world            # weak scaling: each step is one image per GPU-equivalent
-    tracer.render_images(0, images, filt)
+    render_all(0, images)
+    combine_films()
     if dist is not None:
         reduce_film()
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    c = tracer.counters()
-    rays = c["extension_rays"] + c["shadow_rays"]
+    rays = 0
+    for t in tracers:
+        c = t.counters()
+        rays += c["extension_rays"] + c["shadow_rays"]
 
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda" if on_device else "cpu")
-        tmax = t[:1].clone()
+        tt = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda" if on_device else "cpu")
+        tmax = tt[:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t[1:].clone()
+        tsum = tt[1:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed, rays = float(tmax.item()), float(tsum.item())
 
@@ -175,8 +214,14 @@ def main():
         film = film_buf.cpu().numpy() if dist is not None else tracer.read_film()
         np.save(args.save_film, film.reshape(args.height, args.width, 4))
 
-    # ---- roofline leg: same workload (seeds 0..R-1), counters then HIP-event timing
+    # ---- roofline leg: same workload (seeds 0..R-1), counters then HIP-event timing, on
+    # ONE pipeline (the rank's whole partition, as with --streams 1): a kernel's duration
+    # is only its own when no other pipeline's kernels share the GPU
     R = max(1, args.roofline_images or images)
+    if K > 1:
+        for t in tracers:
+            t.destroy()
+        tracer = make_tracer(args.pool, (world, rank, args.stripe) if world > 1 else None)
     tracer.set_instrumentation(True, False)
     tracer.reset_stats()
     tracer.render_images(0, R, filt)
@@ -224,7 +269,9 @@ def main():
         "config": {"workload": f"cornell_box_obj {args.width}x{args.height}, {images} spp ({world} spp/step, film "
                                f"stripes across {world} GPU(s)), {args.bounces} bounces, wavefront, point light",
                    "resolution": [args.width, args.height], "spp": images, "max_bounce": args.bounces,
-                   "path_pool": args.pool, "parallelism": f"film stripes x{world}" if world > 1 else "single GPU",
+                   "path_pool": args.pool, "streams_per_gpu": K,
+                   "parallelism": (f"film stripes x{world}" if world > 1 else "single GPU")
+                                  + (f", {K} concurrent pipelines per GPU" if K > 1 else ""),
                    "rays": int(rays)},
         "roofline": {"bound": "hbm",
                      "kernel": "cast_kernel (EXTENSION_RAY_CAST + SHADOW_RAY_CAST, one launch)" if merged

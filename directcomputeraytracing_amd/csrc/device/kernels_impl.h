@@ -793,6 +793,15 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
     }
 }
 
+// film += src (dcrt_tracer_add_film_device): the films of disjoint film partitions
+__global__ void add_film_kernel(float4* film, const float4* src, uint32_t n)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 a = film[i], b = src[i];
+        film[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
+}
+
 // After the film pass of a completed batch: the next batch's first frame seed and
 // size, rewind the block cursors.
 __global__ void advance_image_kernel(FrameConstants* fc, Globals* g)

@@ -1018,6 +1018,18 @@ DCRT_API int dcrt_tracer_copy_film_device(dcrt_tracer* t, void* d_dst)
     return DCRT_OK;
 }
 
+DCRT_API int dcrt_tracer_add_film_device(dcrt_tracer* t, const void* d_src)
+{
+    TRACER_GUARD(t);
+    if (!d_src || !t->film.accum) return DCRT_E_INVALID_ARG;
+    const uint32_t n = t->filmW * t->filmH;
+    hipLaunchKernelGGL(add_film_kernel, dim3(std::min<uint32_t>((n + 255) / 256, kMaxPersistentBlocks)), dim3(256), 0, t->stream,
+                       t->film.accum, (const float4*)d_src, n);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    return DCRT_OK;
+}
+
 DCRT_API int dcrt_tracer_counters(dcrt_tracer* t, dcrt_ray_stats* out)
 {
     TRACER_GUARD(t);

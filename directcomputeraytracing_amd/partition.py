@@ -47,6 +47,21 @@ def render_rows(height: int, world_size: int, rank: int, stripe_height: int, hal
     return [int(y) for y in np.nonzero(need)[0]]
 
 
+def stream_partition(height: int, world_size: int, rank: int, streams: int, stream: int, stripe_height: int):
+    """(world, rank, stripe height) of pipeline `stream` of the `streams` concurrent ones on
+    rank `rank` of `world_size`: virtual rank s * N + r of N * K. Any such split is exact
+    (the virtual ranks' films have disjoint supports); the stripe height is chosen so the
+    N * K virtual ranks share about as many stripes as the N ranks do without streams
+    (then, when K divides them, a rank owns exactly its stripes of the K = 1 split, dealt
+    round-robin to its pipelines and no halo row is added). One GPU: K horizontal bands."""
+    if world_size <= 1:
+        return streams, stream, -(-height // streams)
+    total = stripe_count(height, world_size, stripe_height)
+    v = world_size * streams
+    k = max(1, round(total / v))
+    return v, stream * world_size + rank, max(1, round(height / (v * k)))
+
+
 def halo_for_radius(radius: float) -> int:
     """Rows of support beyond a pixel row that SampleConvolution gathers (SampleConvolution.hlsl:77-81)."""
     return int(math.floor(radius + 0.5))

@@ -137,6 +137,10 @@ class WavefrontPathTracer:
     def copy_film_device(self, d_dst: int) -> None:
         check(self._lib.dcrt_tracer_copy_film_device(self._h, C.c_void_p(d_dst)), "CopyFilmDevice")
 
+    def add_film_device(self, d_src: int) -> None:
+        """film += the RGBA32F film at device address d_src (another partition's film)."""
+        check(self._lib.dcrt_tracer_add_film_device(self._h, C.c_void_p(d_src)), "AddFilmDevice")
+
     def resolve_image(self, params: _abi.PostFxParams | None = None, with_luminance: bool = False):
         """Post-processing (exposure + Reinhard) into sRGB8 RGBA, H x W x 4 uint8."""
         p = params or _abi.PostFxParams(1, 1, 15.0, 1.0)

@@ -359,6 +359,12 @@ DCRT_API int dcrt_tracer_film_device_ptr(dcrt_tracer* tracer, void** out_ptr);
 /* Device-to-device copy of the RGBA32F film (W*H*4 floats) into d_dst, e.g. an
  * RCCL buffer for the multi-GPU reduce; synchronous with the tracer stream. */
 DCRT_API int dcrt_tracer_copy_film_device(dcrt_tracer* tracer, void* d_dst);
+/* film += d_src (W*H*4 floats in device memory of the tracer's device), on the tracer
+ * stream, synchronous. Combines the films of film partitions rendered by several
+ * tracers of one GPU (concurrent pipelines): their supports are disjoint, so the sum
+ * is the single-tracer film bit for bit. No reference counterpart (the reference has
+ * one pipeline per device). */
+DCRT_API int dcrt_tracer_add_film_device(dcrt_tracer* tracer, const void* d_src);
 DCRT_API int dcrt_tracer_counters(dcrt_tracer* tracer, dcrt_ray_stats* out_stats);
 /* counters != 0: traversal work counters in the cast kernels; ext_timing != 0: plain
  * (non-graph) launches with HIP events around every EXTENSION_RAY_CAST launch. */

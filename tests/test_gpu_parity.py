@@ -192,6 +192,46 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
         assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
 
+def test_concurrent_stream_partitions_sum_to_single_film(native_lib, golden_luts):
+    """bench --streams 2: two tracers on one GPU render their bands concurrently (two host
+    threads, two streams); add_film_device of one film into the other == 1-tracer film."""
+    import threading
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    from directcomputeraytracing_amd.partition import stream_partition
+    s = cornell(160, 120, 3)
+    ref = WavefrontPathTracer(path_pool_size=1 << 15)
+    try:
+        ref.set_luts(golden_luts)
+        ref.on_scene_loaded(s)
+        ref.clear_film()
+        ref.render_images(0, 3)
+        want = ref.read_film()
+    finally:
+        ref.destroy()
+    ts = []
+    try:
+        for k in range(2):
+            t = WavefrontPathTracer(path_pool_size=1 << 14)
+            t.set_luts(golden_luts)
+            t.on_scene_loaded(s)
+            w, v, sh = stream_partition(120, 1, 0, 2, k, 64)
+            t.set_film_partition(w, v, sh)
+            t.clear_film()
+            ts.append(t)
+        th = [threading.Thread(target=t.render_images, args=(0, 3)) for t in ts]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        for t in ts:
+            t.synchronize()
+        ts[0].add_film_device(ts[1].film_device_ptr())
+        assert same_bits(ts[0].read_film(), want).all()
+    finally:
+        for t in ts:
+            t.destroy()
+
+
 def test_partition_rejects_filter_wider_than_halo(native_lib, golden_luts):
     from directcomputeraytracing_amd import DCRTError, FILTER_BOX, FilterParams, WavefrontPathTracer
     s = cornell(64, 48, 2)

@@ -38,6 +38,26 @@ def test_partition_rows_cover_film():
                 assert total / H - 1 < 0.035 * halo            # halo overhead (16 stripes at S = 64)
 
 
+def test_stream_partition_covers_film_once():
+    """Concurrent pipelines per GPU (bench --streams K): virtual ranks s * N + r of N * K
+    own every row exactly once, and with K = 2 a rank keeps exactly its K = 1 rows."""
+    from directcomputeraytracing_amd.partition import owned_rows, stream_partition
+    for H, S in ((1080, 64), (144, 16), (2160, 64), (97, 16)):
+        for world in (1, 2, 3, 4, 8):
+            for streams in (1, 2, 3):
+                cover = np.zeros(H, int)
+                for r in range(world):
+                    mine = np.zeros(H, int)
+                    for s in range(streams):
+                        w, v, sh = stream_partition(H, world, r, streams, s, S)
+                        assert 0 <= v < w == max(1, world * streams) or (world == 1 and w == streams)
+                        mine += owned_rows(H, w, v, sh)
+                    cover += mine
+                    if world > 1 and streams == 2 and H == 1080:
+                        assert np.array_equal(mine > 0, owned_rows(H, world, r, S))
+                assert cover.min() == 1 and cover.max() == 1
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
