@@ -11,6 +11,7 @@ from __future__ import annotations
 import argparse
 import json
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -51,29 +52,53 @@ def run(name, args):
     W, H = scene.resolution
     # several images in flight (an image batch), so each batch drains once: 8 images at 1080p, 8 at 4K
     pool = args.pool or (1 << 24 if W * H <= (1 << 21) else 1 << 26)
+    filt = scene.filter_params()
+    # the timed images on --streams concurrent pipelines (film bands, bench.py --streams)
+    from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
+    K = max(1, args.streams)
+    subs = []
+    for s_ in range(K):
+        t = WavefrontPathTracer(path_pool_size=pool // K, iterations_per_render=16)
+        t.on_scene_loaded(scene)
+        if K > 1:
+            w, v, sh = stream_partition(H, 1, 0, K, s_, 64)
+            t.set_film_partition(w, v, sh, max(1, halo_for_radius(filt.radius)))
+        subs.append(t)
+
+    def render_all(first, count):
+        th = [threading.Thread(target=t.render_images, args=(first, count, filt)) for t in subs]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        for t in subs:
+            t.synchronize()
+
+    try:
+        for t in subs:
+            t.clear_film()
+        render_all(10_000, args.warmup)
+        for t in subs:
+            t.reset_stats()
+        t0 = time.perf_counter()
+        render_all(0, args.spp)
+        el = time.perf_counter() - t0
+        rays = sum(t.counters()["extension_rays"] + t.counters()["shadow_rays"] for t in subs)
+    finally:
+        for t in subs:
+            t.destroy()
     tr = WavefrontPathTracer(path_pool_size=pool, iterations_per_render=16)
     try:
         tr.on_scene_loaded(scene)
-        filt = scene.filter_params()
-        tr.clear_film()
-        tr.render_images(10_000, args.warmup, filt)
-        tr.reset_stats()
-        tr.synchronize()
-        t0 = time.perf_counter()
-        tr.render_images(0, args.spp, filt)
-        tr.synchronize()
-        el = time.perf_counter() - t0
-        c = tr.counters()
-        rays = c["extension_rays"] + c["shadow_rays"]
         # roofline leg (same seeds): counts from the instrumented casts, time from HIP events
         tr.set_instrumentation(True, False)
         tr.reset_stats()
-        tr.render_images(0, 2, filt)
+        tr.render_images(0, args.spp, filt)
         st = tr.traversal_stats()
         cr = tr.counters()
         tr.set_instrumentation(False, True)
         tr.reset_stats()
-        tr.render_images(0, 2, filt)
+        tr.render_images(0, args.spp, filt)
         tm = tr.traversal_stats()
         tr.set_instrumentation(False, False)
         ext_bytes = (56 * cr["extension_rays"] + 32 * st["ext_node_visits"] + 48 * st["ext_triangle_tests"]
@@ -83,7 +108,7 @@ def run(name, args):
         # the timed launch is the merged EXTENSION+SHADOW cast kernel (as in bench.py)
         achieved = (ext_bytes + shadow_bytes) / (tm["ext_kernel_ms"] * 1e-3) / 1e9
         info = scene.bvh_info()
-        return {"config": name, "workload": desc, "resolution": [W, H], "spp": args.spp, "path_pool": pool,
+        return {"config": name, "workload": desc, "resolution": [W, H], "spp": args.spp, "path_pool": pool, "streams": K,
                 "value": round(rays / el / 1e6, 1), "unit": "Mrays/s", "ms_per_spp": round(el * 1e3 / args.spp, 2),
                 "rays_per_spp": int(rays / args.spp), "triangles_bvh_nodes": info["total_nodes"],
                 "scene_load_s": round(load_s, 2),
@@ -104,6 +129,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--configs", default="cornell,coffee,spaceship,lamp")
     ap.add_argument("--scene-dir", default="/tmp/dcrt_scenes")
+    ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines (bench.py --streams)")
     ap.add_argument("--pool", type=int, default=0, help="path pool slots (0: 2^24 at 1080p, 2^26 at 4K)")
     ap.add_argument("--small", action="store_true", help="small meshes (CI smoke)")
     args = ap.parse_args()
