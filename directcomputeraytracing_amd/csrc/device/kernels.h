@@ -16,6 +16,10 @@ constexpr uint32_t kFlagIdle = 0x80000000u;           // WavefrontPathTracing.hl
 constexpr uint32_t kFlagShadowRayHit = 0x40000000u;
 constexpr uint32_t kFlagTerminate = 0x20000000u;
 constexpr uint32_t kBlockW = 8, kBlockH = 8;           // one wave64 = one 8x8 pixel block
+#ifndef DCRT_CONTROL_BLOCK
+#define DCRT_CONTROL_BLOCK 256
+#endif
+constexpr uint32_t kControlBlock = DCRT_CONTROL_BLOCK;  // CONTROL workgroup (the path pool is a multiple of it)
 
 // Queue counters are sharded: producer workgroup b appends to shard b % kShards,
 // each shard counter on its own 256-B line. One returning device-scope atomic on

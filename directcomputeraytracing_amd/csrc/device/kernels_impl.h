@@ -78,7 +78,7 @@ __global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32
 }
 
 // ---- CONTROL (+ NEW_PATH) -------------------------------------------------------
-__global__ __launch_bounds__(256) void control_kernel(PathPool pool, Film film, const FrameConstants* fc, Counters* cnt,
+__global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, Film film, const FrameConstants* fc, Counters* cnt,
                                                        Globals* g, uint32_t debugRng)
 {
     __shared__ uint32_t sm[64];

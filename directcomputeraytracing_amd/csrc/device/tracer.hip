@@ -43,7 +43,6 @@ namespace {
 constexpr uint32_t kDefaultPoolSize = 1u << 20;      // 2^20 slots: 16 waves x 256 CUs x 256 (MI355X)
 constexpr uint32_t kDefaultIterations = 8;
 constexpr uint32_t kMaxImageBatch = 64;               // images in flight per RenderImages batch (sample textures: 24 B/px each)
-constexpr uint32_t kControlBlock = 256;
 constexpr uint32_t kMaterialBlock = 256;
 constexpr uint32_t kMaxPersistentBlocks = 256 * 8;   // CUs x resident workgroups
 #ifndef DCRT_CONTROL_MAX_BLOCKS
@@ -224,7 +223,10 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
         ownsStream = true;
     }
     poolSize = cfg.path_pool_size ? cfg.path_pool_size : kDefaultPoolSize;
-    poolSize = (poolSize + 255u) & ~255u;   // whole 256-thread workgroups of whole waves
+    // whole CONTROL workgroups of whole waves, and at least one CONTROL workgroup per
+    // pixel-block shard (workgroup b claims the blocks of shard b % kShards)
+    poolSize = std::max<uint32_t>(poolSize, kControlBlock * kShards);
+    poolSize = (poolSize + kControlBlock - 1) / kControlBlock * kControlBlock;
     iterationsPerRender = cfg.iterations_per_render ? cfg.iterations_per_render : kDefaultIterations;
     debugRng = cfg.debug_rng != 0;
     if (const char* split = std::getenv("DCRT_SPLIT_CASTS")) mergedCasts = std::atoi(split) == 0;

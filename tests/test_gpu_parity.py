@@ -232,6 +232,24 @@ def test_concurrent_stream_partitions_sum_to_single_film(native_lib, golden_luts
             t.destroy()
 
 
+def test_tiny_pool_renders_every_pixel(native_lib, golden_luts, oracle_mod):
+    """A pool smaller than one CONTROL workgroup per pixel-block shard is grown to it:
+    every shard's pixel blocks get claimed and the image completes bit-exact."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    s = cornell(40, 24, 2)
+    t = WavefrontPathTracer(path_pool_size=300)
+    try:
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s, frame_seed=4)
+        t.clear_film()
+        t.render_images(4, 1)
+        pos, val = t.read_samples()
+    finally:
+        t.destroy()
+    p_ref, v_ref, _, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(4), oracle_mod.WAVEFRONT)
+    assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
+
+
 def test_partition_rejects_filter_wider_than_halo(native_lib, golden_luts):
     from directcomputeraytracing_amd import DCRTError, FILTER_BOX, FilterParams, WavefrontPathTracer
     s = cornell(64, 48, 2)
