@@ -11,6 +11,7 @@ max / mean rank time per step and the implied weak-scaling efficiency vs N = 1.
 import argparse
 import json
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -25,10 +26,11 @@ def main():
     ap.add_argument("--image-batch", type=int, default=0)
     ap.add_argument("--stripe", type=int, default=64)
     ap.add_argument("--pool", type=int, default=1 << 24)
+    ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines per rank (bench.py --streams)")
     ap.add_argument("--rank0-only", action="store_true", help="time rank 0's share only (sweeps)")
     args = ap.parse_args()
     from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
-    from directcomputeraytracing_amd.partition import halo_for_radius
+    from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
     scene = Scene((1920, 1080))
     scenes.setup_cornell(scene, 1920, 1080, 8)
     filt = scene.filter_params()
@@ -36,29 +38,45 @@ def main():
     for n in [int(x) for x in args.gpus.split(",")]:
         times, rays, iters = [], [], []
         for r in range(1 if args.rank0_only else n):
-            t = WavefrontPathTracer(path_pool_size=args.pool, iterations_per_render=16)
+            # the rank's K concurrent pipelines, as bench.py --streams K runs them
+            K = max(1, args.streams)
+            ts = []
             try:
-                t.on_scene_loaded(scene)
-                t.set_image_batch(args.image_batch)
-                if n > 1:
-                    t.set_film_partition(n, r, args.stripe, max(1, halo_for_radius(filt.radius)))
-                t.clear_film()
-                t.render_images(10_000, n, filt)
-                t.synchronize()
-                t.reset_stats()
+                for s_ in range(K):
+                    t = WavefrontPathTracer(path_pool_size=args.pool // K, iterations_per_render=16)
+                    ts.append(t)
+                    t.on_scene_loaded(scene)
+                    t.set_image_batch(args.image_batch)
+                    if n > 1 or K > 1:
+                        w, v, sh = stream_partition(1080, n, r, K, s_, args.stripe)
+                        t.set_film_partition(w, v, sh, max(1, halo_for_radius(filt.radius)))
+                    t.clear_film()
+
+                def run(first, count):
+                    th = [threading.Thread(target=t.render_images, args=(first, count, filt)) for t in ts]
+                    for x in th:
+                        x.start()
+                    for x in th:
+                        x.join()
+                    for t in ts:
+                        t.synchronize()
+
+                run(10_000, n)
+                for t in ts:
+                    t.reset_stats()
                 t0 = time.perf_counter()
-                t.render_images(0, args.steps * n, filt)
-                t.synchronize()
+                run(0, args.steps * n)
                 times.append((time.perf_counter() - t0) * 1e3 / args.steps)
-                c = t.counters()
-                rays.append((c["extension_rays"] + c["shadow_rays"]) / args.steps)
-                iters.append(c.get("iterations", 0) / args.steps)
+                cs = [t.counters() for t in ts]
+                rays.append(sum(c["extension_rays"] + c["shadow_rays"] for c in cs) / args.steps)
+                iters.append(max(c.get("iterations", 0) for c in cs) / args.steps)
             finally:
-                t.destroy()
+                for t in ts:
+                    t.destroy()
         mx, mean = max(times), sum(times) / len(times)
         base = base or mx
         print(json.dumps({"n_gpus": n, "ms_per_step_max_rank": round(mx, 3), "ms_per_step_mean_rank": round(mean, 3),
-                          "weak_efficiency": round(base / mx, 3), "image_batch": args.image_batch, "pool": args.pool,
+                          "weak_efficiency": round(base / mx, 3), "image_batch": args.image_batch, "pool": args.pool, "streams": args.streams,
                           "mrays_per_step_mean_rank": round(sum(rays) / len(rays) / 1e6, 3),
                           "ns_per_ray_mean_rank": round(mean * 1e6 / (sum(rays) / len(rays)), 4),
                           "iterations_per_step_mean_rank": round(sum(iters) / len(iters), 2)}), flush=True)
