@@ -11,6 +11,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -278,8 +280,21 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
 
 // BxDFTexturesBuilding::Build (BxDFTexturesBuilding.cpp:106-475) as three
 // integration launches + one conversion/average launch.
+// The LUTs depend on nothing but the integration constants, so a process integrates
+// them once per device (≈ 0.24 s of GPU time) and every further tracer copies them
+// (the cache's device copies live until the process exits).
+static std::mutex g_lutMutex;
+static std::map<int, dcrt_bxdf_luts*> g_lutCache;
+
 int dcrt_tracer::BuildLuts()
 {
+    std::lock_guard<std::mutex> lock(g_lutMutex);
+    auto hit = g_lutCache.find(device);
+    if (hit != g_lutCache.end()) {
+        HIPCHECK(hipMemcpyAsync(dLuts, hit->second, sizeof(dcrt_bxdf_luts), hipMemcpyDeviceToDevice, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        return DCRT_OK;
+    }
     std::vector<void*> tmp;
     float *brdf = nullptr, *brdfd = nullptr, *bsdf = nullptr;
     CHECKED(DeviceAlloc(&brdf, DCRT_LUT_BRDF_COUNT, &tmp));
@@ -293,6 +308,11 @@ int dcrt_tracer::BuildLuts()
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(stream));
     FreeAll(&tmp);
+    dcrt_bxdf_luts* cached = nullptr;
+    if (hipMalloc((void**)&cached, sizeof(dcrt_bxdf_luts)) == hipSuccess) {
+        if (hipMemcpy(cached, dLuts, sizeof(dcrt_bxdf_luts), hipMemcpyDeviceToDevice) == hipSuccess) g_lutCache[device] = cached;
+        else (void)hipFree(cached);
+    }
     return DCRT_OK;
 }
 
