@@ -342,6 +342,16 @@ def test_config_scenes_bit_exact(gpu_tracer, golden_luts, oracle_mod, name, cube
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 1]))
 
 
+def test_full_size_spaceship_mesh_bit_exact(gpu_tracer, golden_luts, oracle_mod, tmp_path):
+    """configs[3] at its full mesh size (261 120 triangles x 8 instances, 522 k BVH nodes,
+    stack depth 30: most nodes outside the LDS scene cache), 320x180, 8 bounces, 1 spp."""
+    from directcomputeraytracing_amd import Scene, scenes
+    s = Scene((320, 180))
+    s.load_from_file(scenes.write_spaceship(tmp_path, 320, 180, nu=512, nv=256, ships=8))
+    assert s.bvh_info()["total_nodes"] > 500_000
+    list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [3]))
+
+
 def test_postfx_resolve_bit_exact(native_lib, golden_luts, oracle_mod):
     """Exposure (manual / auto via the two-stage log-luminance reduction) + Reinhard + sRGB8."""
     from directcomputeraytracing_amd import PostFxParams, WavefrontPathTracer, srgb_thresholds
