@@ -43,7 +43,7 @@ struct Globals {
     uint32_t imagesDone, imageTarget, seedBase;
     uint32_t batchImages;     // images path-traced together in the current batch (image index in [0, batchImages))
     uint32_t batchCap;        // RenderImages' batch size
-    unsigned long long extRays, shadowRays, newPaths, iterations;
+    unsigned long long extRays, shadowRays, iterations;
 };
 
 DEV uint32_t* qctr(Counters* c, uint32_t q, uint32_t s) { return c->w + (q * kShards + s) * kShardStride; }

@@ -102,6 +102,7 @@ struct dcrt_tracer {
     uint32_t iterationsPerRender = kDefaultIterations;
     bool debugRng = false;
     uint32_t refillLanes = 16, parkLanes = 32;   // DCRT_TRAVERSAL_TUNE="refill,park" overrides
+    uint64_t imagesCompleted = 0;                // since the last ResetStats (counters())
 
     std::vector<void*> poolAllocs, sceneAllocs, filmAllocs, sampleAllocs, rowAllocs;
     PathPool pool{};
@@ -763,6 +764,7 @@ int dcrt_tracer::Render(uint32_t maxIterations)
     CHECKED(RunIterations(maxIterations ? maxIterations : iterationsPerRender));
     bool complete = false;
     CHECKED(ReadCompletion(&complete));
+    if (complete) ++imagesCompleted;
     imageComplete = complete;
     newImage = complete;   // WavefrontPathTracer.cpp:500
     return DCRT_OK;
@@ -828,6 +830,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
         HIPCHECK(hipStreamSynchronize(stream));
         imageComplete = true;
         newImage = true;
+        imagesCompleted += count;
         return DCRT_OK;
     }
     const uint32_t batch = AutoBatch(count);
@@ -879,6 +882,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     }
     imageComplete = true;
     newImage = true;
+    imagesCompleted += count;
     lastSlot = (count - 1) % batch;
     return DCRT_OK;
 }
@@ -1061,9 +1065,10 @@ DCRT_API int dcrt_tracer_counters(dcrt_tracer* t, dcrt_ray_stats* out)
     HIPCHECK(hipStreamSynchronize(t->stream));
     out->extension_rays = g.extRays;
     out->shadow_rays = g.shadowRays;
-    out->new_paths = g.newPaths;
+    // every rendered pixel (film rows of this tracer, halo included) starts one path per image
+    out->new_paths = t->imagesCompleted * (uint64_t)t->rowCount * t->filmW;
     out->iterations = g.iterations;
-    out->images_completed = 0;
+    out->images_completed = t->imagesCompleted;
     return DCRT_OK;
 }
 
@@ -1109,7 +1114,8 @@ DCRT_API int dcrt_tracer_reset_stats(dcrt_tracer* t)
     Globals g;
     HIPCHECK(hipMemcpyAsync(&g, t->dGlobals, sizeof(Globals), hipMemcpyDeviceToHost, t->stream));
     HIPCHECK(hipStreamSynchronize(t->stream));
-    g.extRays = g.shadowRays = g.newPaths = g.iterations = 0;
+    g.extRays = g.shadowRays = g.iterations = 0;
+    t->imagesCompleted = 0;
     HIPCHECK(hipMemcpyAsync(t->dGlobals, &g, sizeof(Globals), hipMemcpyHostToDevice, t->stream));
     HIPCHECK(hipStreamSynchronize(t->stream));
     t->eventsUsed = 0;

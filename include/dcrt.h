@@ -234,13 +234,14 @@ typedef struct dcrt_tracer_config {
     uint32_t debug_rng;           /* nonzero: keep each pixel's terminal RNG state    */
 } dcrt_tracer_config;
 
-/* Counters of the last rendered image(s). */
+/* Counters since the last dcrt_tracer_reset_stats (or create). */
 typedef struct dcrt_ray_stats {
-    uint64_t extension_rays;
-    uint64_t shadow_rays;
-    uint64_t new_paths;
-    uint64_t iterations;
-    uint64_t images_completed;
+    uint64_t extension_rays;      /* EXTENSION_RAY_CAST rays traced                   */
+    uint64_t shadow_rays;         /* SHADOW_RAY_CAST rays traced                      */
+    uint64_t new_paths;           /* paths started by the completed images (one per
+                                     rendered pixel, halo rows included, per image)   */
+    uint64_t iterations;          /* RenderOneIteration equivalents launched          */
+    uint64_t images_completed;    /* images finished by render / render_images        */
 } dcrt_ray_stats;
 
 /* Rows of the film a tracer renders and convolves (multi-GPU film tiling).

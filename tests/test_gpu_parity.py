@@ -183,6 +183,8 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
             t.render_images(5, 3)
             films.append(t.read_film())
             samples.append(t.read_samples())
+            c = t.counters()
+            assert c["images_completed"] == 3 and c["new_paths"] == 3 * 96 * 64
         finally:
             t.destroy()
     for f in films[1:]:
