@@ -276,11 +276,14 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
     }
 }
 
-// Cast-kernel occupancy: 6 waves per SIMD (<= 80 VGPRs; the compiler alone takes ~99,
-// i.e. 4 waves). Measured on the 1080p Cornell bench: 4 waves 5.51, 5 waves 5.46,
-// 6 waves 5.37, 7 waves 5.77 (spills), 8 waves 7.19 ms/spp (tools/ab_libs.sh).
+// Cast-kernel occupancy: 5 waves per SIMD (<= 96 VGPRs; the compiler alone takes ~99,
+// i.e. 4 waves). Measured on the 1080p Cornell bench, one pipeline: 4 waves 5.51,
+// 5 waves 5.46, 6 waves 5.37, 7 waves 5.77 (spills), 8 waves 7.19 ms/spp; with the
+// two concurrent pipelines of the default bench 5 waves leave the other pipeline's
+// kernels room on the CU: 4.60 vs 4.66 ms/spp at 6 (3 repeats, tools/ab_libs.sh),
+// although a lone launch is 3 % slower (106 vs 102.5 us).
 #ifndef DCRT_CAST_WAVES_PER_EU
-#define DCRT_CAST_WAVES_PER_EU 6
+#define DCRT_CAST_WAVES_PER_EU 5
 #endif
 #if DCRT_CAST_WAVES_PER_EU > 0
 #define DCRT_CAST_OCCUPANCY __attribute__((amdgpu_waves_per_eu(DCRT_CAST_WAVES_PER_EU, 8)))
