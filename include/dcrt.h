@@ -342,8 +342,12 @@ DCRT_API int dcrt_tracer_render(dcrt_tracer* tracer, uint32_t max_iterations);
  * image, in order, so the film is the same as with one image at a time. */
 DCRT_API int dcrt_tracer_render_images(dcrt_tracer* tracer, uint32_t first_seed, uint32_t image_count,
                                        const dcrt_filter_params* filter);
-/* Images per render_images batch (0 = automatic: about twice the path pool's worth of
- * pixels, at most 16). */
+/* Allocate / capture now what dcrt_tracer_render_images(image_count) would on its first
+ * call (the batch's sample textures, the iteration graph), e.g. before a timed region.
+ * No reference counterpart (the reference allocates at Create and scene load). */
+DCRT_API int dcrt_tracer_prepare_images(dcrt_tracer* tracer, uint32_t image_count);
+/* Images per render_images batch (0 = automatic: as many as the path pool holds, at most
+ * 64, the images cut into equal batches). */
 DCRT_API int dcrt_tracer_set_image_batch(dcrt_tracer* tracer, uint32_t images);
 /* 0 = wavefront (CWavefrontPathTracer, default), 1 = megakernel (CMegakernelPathTracer,
  * MegakernelPathTracing.hlsl) for dcrt_tracer_render_images. */

@@ -79,6 +79,7 @@ def run(name, args):
             t.clear_film()
         render_all(10_000, args.warmup)
         for t in subs:
+            t.prepare_images(args.spp)
             t.reset_stats()
         t0 = time.perf_counter()
         render_all(0, args.spp)

@@ -63,6 +63,7 @@ def main():
 
                 run(10_000, n)
                 for t in ts:
+                    t.prepare_images(args.steps * n)
                     t.reset_stats()
                 t0 = time.perf_counter()
                 run(0, args.steps * n)
@@ -79,7 +80,9 @@ def main():
                           "weak_efficiency": round(base / mx, 3), "image_batch": args.image_batch, "pool": args.pool, "streams": args.streams,
                           "mrays_per_step_mean_rank": round(sum(rays) / len(rays) / 1e6, 3),
                           "ns_per_ray_mean_rank": round(mean * 1e6 / (sum(rays) / len(rays)), 4),
-                          "iterations_per_step_mean_rank": round(sum(iters) / len(iters), 2)}), flush=True)
+                          "iterations_per_step_mean_rank": round(sum(iters) / len(iters), 2),
+                          "ms_per_step_by_rank": [round(x, 3) for x in times],
+                          "iterations_per_step_by_rank": [round(x, 2) for x in iters]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -61,6 +61,7 @@ def main():
                 t.clear_film()
             run_all(10_000, 2)
             for t in ts:
+                t.prepare_images(args.steps)
                 t.clear_film()
                 t.reset_stats()
             t0 = time.perf_counter()
