@@ -19,7 +19,6 @@ import argparse
 import json
 import os
 import sys
-import threading
 import time
 from pathlib import Path
 
@@ -112,7 +111,7 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     import numpy as np
-    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, render_images_concurrently, scenes
     luts_arrays = dict(np.load(ROOT / "tests" / "golden" / "bxdf_luts.npz"))
 
     scene = Scene((args.width, args.height))
@@ -141,14 +140,7 @@ def main():
     tracer = tracers[0]
 
     def render_all(first, count):
-        if K == 1:
-            tracer.render_images(first, count, filt)
-            return
-        th = [threading.Thread(target=t.render_images, args=(first, count, filt)) for t in tracers]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
+        render_images_concurrently(tracers, first, count, filt)
 
     def barrier_sync():
         for t in tracers:

@@ -227,3 +227,30 @@ def device_count() -> int:
     n = C.c_int()
     check(lib.dcrt_device_count(C.byref(n)))
     return n.value
+
+
+def render_images_concurrently(tracers, first_seed: int, count: int, filter_params=None) -> None:
+    """render_images on several tracers at once (one host thread each; the C ABI runs with
+    the GIL released and every tracer owns its stream), then synchronize them all. An
+    error in any tracer is raised here, after every thread has finished."""
+    import threading
+    errors = []
+
+    def run(t):
+        try:
+            t.render_images(first_seed, count, filter_params)
+        except BaseException as e:   # re-raised in the caller's thread
+            errors.append(e)
+
+    if len(tracers) == 1:
+        run(tracers[0])
+    else:
+        th = [threading.Thread(target=run, args=(t,)) for t in tracers]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    if errors:
+        raise errors[0]
+    for t in tracers:
+        t.synchronize()

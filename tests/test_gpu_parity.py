@@ -197,8 +197,7 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
 def test_concurrent_stream_partitions_sum_to_single_film(native_lib, golden_luts):
     """bench --streams 2: two tracers on one GPU render their bands concurrently (two host
     threads, two streams); add_film_device of one film into the other == 1-tracer film."""
-    import threading
-    from directcomputeraytracing_amd import WavefrontPathTracer
+    from directcomputeraytracing_amd import WavefrontPathTracer, render_images_concurrently
     from directcomputeraytracing_amd.partition import stream_partition
     s = cornell(160, 120, 3)
     ref = WavefrontPathTracer(path_pool_size=1 << 15)
@@ -220,13 +219,7 @@ def test_concurrent_stream_partitions_sum_to_single_film(native_lib, golden_luts
             t.set_film_partition(w, v, sh)
             t.clear_film()
             ts.append(t)
-        th = [threading.Thread(target=t.render_images, args=(0, 3)) for t in ts]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        for t in ts:
-            t.synchronize()
+        render_images_concurrently(ts, 0, 3)
         ts[0].add_film_device(ts[1].film_device_ptr())
         assert same_bits(ts[0].read_film(), want).all()
     finally:

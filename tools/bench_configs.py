@@ -11,7 +11,6 @@ from __future__ import annotations
 import argparse
 import json
 import sys
-import threading
 import time
 from pathlib import Path
 
@@ -45,7 +44,7 @@ def setup(name, scene_dir: Path, small: bool):
 
 
 def run(name, args):
-    from directcomputeraytracing_amd import WavefrontPathTracer
+    from directcomputeraytracing_amd import WavefrontPathTracer, render_images_concurrently
     t0 = time.perf_counter()
     scene, desc = setup(name, Path(args.scene_dir), args.small)
     load_s = time.perf_counter() - t0
@@ -66,13 +65,7 @@ def run(name, args):
         subs.append(t)
 
     def render_all(first, count):
-        th = [threading.Thread(target=t.render_images, args=(first, count, filt)) for t in subs]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        for t in subs:
-            t.synchronize()
+        render_images_concurrently(subs, first, count, filt)
 
     try:
         for t in subs:

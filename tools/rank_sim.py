@@ -11,7 +11,6 @@ max / mean rank time per step and the implied weak-scaling efficiency vs N = 1.
 import argparse
 import json
 import sys
-import threading
 import time
 from pathlib import Path
 
@@ -29,7 +28,7 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines per rank (bench.py --streams)")
     ap.add_argument("--rank0-only", action="store_true", help="time rank 0's share only (sweeps)")
     args = ap.parse_args()
-    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, render_images_concurrently, scenes
     from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
     scene = Scene((1920, 1080))
     scenes.setup_cornell(scene, 1920, 1080, 8)
@@ -53,13 +52,7 @@ def main():
                     t.clear_film()
 
                 def run(first, count):
-                    th = [threading.Thread(target=t.render_images, args=(first, count, filt)) for t in ts]
-                    for x in th:
-                        x.start()
-                    for x in th:
-                        x.join()
-                    for t in ts:
-                        t.synchronize()
+                    render_images_concurrently(ts, first, count, filt)
 
                 run(10_000, n)
                 for t in ts:

@@ -12,7 +12,6 @@ partition films sum to the single-tracer film bit for bit.
 import argparse
 import json
 import sys
-import threading
 import time
 from pathlib import Path
 
@@ -31,7 +30,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     args = ap.parse_args()
     import numpy as np
-    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, render_images_concurrently, scenes
     from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
     scene = Scene((1920, 1080))
     scenes.setup_cornell(scene, 1920, 1080, 8)
@@ -48,13 +47,7 @@ def main():
             ts.append(t)
 
         def run_all(first, count):
-            th = [threading.Thread(target=t.render_images, args=(first, count, filt)) for t in ts]
-            for x in th:
-                x.start()
-            for x in th:
-                x.join()
-            for t in ts:
-                t.synchronize()
+            render_images_concurrently(ts, first, count, filt)
 
         try:
             for t in ts:
