@@ -179,6 +179,8 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
             t.set_luts(golden_luts)
             t.on_scene_loaded(s)
             t.set_image_batch(batch)
+            if batch == 2:
+                t.prepare_images(3)    # allocate + capture ahead: same bits
             t.clear_film()
             t.render_images(5, 3)
             films.append(t.read_film())
