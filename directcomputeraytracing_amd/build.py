@@ -99,6 +99,25 @@ def build_native(force: bool = False, verbose: bool = False, out: Path | None = 
     return lib_path
 
 
+EXAMPLE_SRC = ROOT / "examples" / "dcrt_render.cpp"
+EXAMPLE_BIN = ROOT / "examples" / "dcrt_render"
+
+
+def build_examples(force: bool = False) -> Path:
+    """examples/dcrt_render: a C++ host of libdcrt.so through the C ABI alone."""
+    lib = build_native()
+    digest = _digest([EXAMPLE_SRC, ROOT / "include" / "dcrt.h", lib])
+    stamp = EXAMPLE_BIN.with_suffix(".sha256")
+    if not force and EXAMPLE_BIN.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+        return EXAMPLE_BIN
+    cxx = shutil.which("g++") or "g++"
+    cmd = [cxx, "-O2", "-std=c++17", "-Wall", str(EXAMPLE_SRC), "-I", str(ROOT / "include"), "-L", str(PKG_DIR), "-ldcrt",
+           "-Wl,-rpath,$ORIGIN/../directcomputeraytracing_amd", "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(EXAMPLE_BIN)]
+    subprocess.run(cmd, check=True)
+    stamp.write_text(digest)
+    return EXAMPLE_BIN
+
+
 def build_oracle(force: bool = False) -> Path:
     """TEST INFRASTRUCTURE: compile the CPU restatement (gcc, no contraction)."""
     src = [ORACLE_DIR / "dcrt_oracle.c", ORACLE_DIR / "dcrt_oracle.h", ROOT / "include" / "dcrt.h"]
@@ -115,3 +134,4 @@ def build_oracle(force: bool = False) -> Path:
 if __name__ == "__main__":
     print(build_native(force="--force" in sys.argv, verbose=True))
     print(build_oracle(force="--force" in sys.argv))
+    print(build_examples(force="--force" in sys.argv))

@@ -349,6 +349,36 @@ def test_full_size_spaceship_mesh_bit_exact(gpu_tracer, golden_luts, oracle_mod,
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [3]))
 
 
+def test_cpp_host_example_matches_python_host(native_lib, tmp_path):
+    """examples/dcrt_render (C++ host over the C ABI, the reference's frame loop: Render /
+    IsImageComplete / SampleConvolution per image) and its --batch mode (render_images)
+    write the same BMP as the Python host's render_images + resolve_image."""
+    import subprocess
+    from directcomputeraytracing_amd import WavefrontPathTracer, save_bmp, scenes
+    from directcomputeraytracing_amd.build import build_examples
+    exe = build_examples()
+    W, H, spp, bounces = 96, 64, 3, 4
+    px, col = scenes.POINT_LIGHT_POSITION, scenes.POINT_LIGHT_COLOR
+    light = ["--point", *map(str, px), *map(str, col)]
+    out = {}
+    for mode in ("frame", "batch"):
+        bmp = tmp_path / f"{mode}.bmp"
+        args = [str(exe), str(scenes.CORNELL_OBJ), str(W), str(H), str(spp), str(bounces), str(bmp), *light]
+        r = subprocess.run(args + (["--batch"] if mode == "batch" else []), capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        out[mode] = bmp.read_bytes()
+    s = cornell(W, H, bounces)
+    t = WavefrontPathTracer(path_pool_size=1 << 16)
+    try:
+        t.on_scene_loaded(s)
+        t.clear_film()
+        t.render_images(0, spp)
+        save_bmp(tmp_path / "py.bmp", t.resolve_image(s.postfx_params()))
+    finally:
+        t.destroy()
+    assert out["frame"] == out["batch"] == (tmp_path / "py.bmp").read_bytes()
+
+
 def test_postfx_resolve_bit_exact(native_lib, golden_luts, oracle_mod):
     """Exposure (manual / auto via the two-stage log-luminance reduction) + Reinhard + sRGB8."""
     from directcomputeraytracing_amd import PostFxParams, WavefrontPathTracer, srgb_thresholds
