@@ -8,6 +8,9 @@ image, so per-GPU work per step is one full image: weak scaling. ``--gpus N``
 > 1 is launched by torch.distributed.run; one RCCL reduce of the RGBA32F film
 closes the timed region.
 
+``--config coffee|spaceship|lamp`` runs BASELINE.json's other configs (procedural
+scenes, their resolutions) through the same path, on 1 or N GPUs.
+
 Prints ONE JSON line (rank 0). Besides the contract fields it carries
 ``roofline`` (EXTENSION_RAY_CAST: algorithmic bytes / HIP-event kernel time
 against the MI355X HBM peak) and ``cpu_baseline`` (the oracle's scalar
@@ -39,8 +42,11 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=8)
-    ap.add_argument("--pool", type=int, default=1 << 24,
-                    help="path pool slots (2^24 = 8 images of 1080p in flight: one drain per batch, not per image)")
+    ap.add_argument("--config", default="cornell", choices=["cornell", "coffee", "spaceship", "lamp"],
+                    help="BASELINE.json configs[1..4]; the headline (and default) is cornell = configs[1]")
+    ap.add_argument("--scene-dir", default="/tmp/dcrt_scenes", help="where the procedural config scenes are written")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="path pool slots (0: 2^24 at 1080p = 8 images in flight, one drain per batch; 2^26 at 4K)")
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
     ap.add_argument("--streams", type=int, default=2,
@@ -59,7 +65,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(scene, luts_arrays, seconds: float) -> dict:
+def cpu_baseline(scene, luts_arrays, seconds: float, label: str = "1920x1080 8-bounce Cornell") -> dict:
     """Oracle megakernel (MegakernelPathTracing.hlsl restated in C) on host cores, bounded."""
     import oracle  # cpu_baseline leg only
     threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 16))
@@ -88,7 +94,7 @@ def cpu_baseline(scene, luts_arrays, seconds: float) -> dict:
     mrays = rays / elapsed / 1e6
     return {"value": round(mrays, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"oracle megakernel (scalar C restatement of MegakernelPathTracing.hlsl), {W}x{done_rows} "
-                      f"rows ({images} image(s) of {band} rows, seeds 0..{images - 1}) of the 1920x1080 8-bounce Cornell "
+                      f"rows ({images} image(s) of {band} rows, seeds 0..{images - 1}) of the {label} "
                       f"image at 1 spp, {elapsed:.1f} s",
             "ms_per_spp_extrapolated": round(elapsed * 1e3 * H / done_rows, 1)}
 
@@ -115,7 +121,15 @@ def main():
     luts_arrays = dict(np.load(ROOT / "tests" / "golden" / "bxdf_luts.npz"))
 
     scene = Scene((args.width, args.height))
-    scenes.setup_cornell(scene, args.width, args.height, args.bounces)
+    if args.config == "cornell":
+        scenes.setup_cornell(scene, args.width, args.height, args.bounces)
+        workload = (f"cornell_box_obj {args.width}x{args.height}, {{spp}} spp ({world} spp/step, film stripes across "
+                    f"{world} GPU(s)), {args.bounces} bounces, wavefront, point light")
+    else:
+        desc = scenes.setup_config(scene, args.config, args.scene_dir)
+        args.width, args.height = scene.resolution
+        workload = f"{desc}, {{spp}} spp ({world} spp/step, film stripes across {world} GPU(s)), wavefront"
+    args.pool = args.pool or scenes.default_pool(args.width, args.height)
     filt = scene.filter_params()
     from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
     halo = max(1, halo_for_radius(filt.radius))
@@ -246,7 +260,8 @@ def main():
             traffic = None
 
     result = {
-        "metric": "Mrays/s and ms/spp at 1920x1080, 8-bounce wavefront",
+        "metric": ("Mrays/s and ms/spp at 1920x1080, 8-bounce wavefront" if args.config == "cornell"
+                   else f"Mrays/s and ms/spp at {args.width}x{args.height}, {args.config} config, wavefront"),
         "value": round(rays / elapsed / 1e6, 2),
         "unit": "Mrays/s",
         "n_gpus": world,
@@ -259,9 +274,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": f"cornell_box_obj {args.width}x{args.height}, {images} spp ({world} spp/step, film "
-                               f"stripes across {world} GPU(s)), {args.bounces} bounces, wavefront, point light",
-                   "resolution": [args.width, args.height], "spp": images, "max_bounce": args.bounces,
+        "config": {"workload": workload.format(spp=images), "name": args.config,
+                   "resolution": [args.width, args.height], "spp": images,
+                   "max_bounce": args.bounces if args.config == "cornell" else scene.frame_params(0).max_bounce_count,
                    "path_pool": args.pool, "streams_per_gpu": K,
                    "parallelism": (f"film stripes x{world}" if world > 1 else "single GPU")
                                   + (f", {K} concurrent pipelines per GPU" if K > 1 else ""),
@@ -282,7 +297,8 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(scene, luts_arrays, args.cpu_seconds)
+        label = "1920x1080 8-bounce Cornell" if args.config == "cornell" else f"{args.config} config"
+        result["cpu_baseline"] = cpu_baseline(scene, luts_arrays, args.cpu_seconds, label)
     if rank == 0:
         print(json.dumps(result), flush=True)
     tracer.destroy()

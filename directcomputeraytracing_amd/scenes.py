@@ -414,3 +414,33 @@ def write_anyhit(directory: Path | str, width: int = 64, height: int = 48) -> Pa
     p = d / "anyhit.xml"
     p.write_text(_xml(body))
     return p
+
+
+CONFIGS = ("cornell", "coffee", "spaceship", "lamp")
+
+
+def setup_config(scene, name: str, scene_dir: Path | str, small: bool = False) -> str:
+    """BASELINE.json configs[1..4] as procedural scenes (written into `scene_dir`), loaded
+    into `scene` at their resolutions; returns a workload description."""
+    d = Path(scene_dir)
+    if name == "cornell":
+        setup_cornell(scene, 1920, 1080, 8)
+        return "Cornell box OBJ 1920x1080, 8 bounces, point light (configs[1])"
+    if name == "coffee":
+        scene.load_from_file(write_coffee(d, 1920, 1080, segments=48 if small else 96))
+        scene.set_environment_light((1.0, 1.0, 1.0), env_cube(64))
+        return "coffee-like Mitsuba XML 1920x1080, env cube + constant, max_depth 8 (configs[2])"
+    if name == "spaceship":
+        nu, nv = (64, 32) if small else (512, 256)
+        scene.load_from_file(write_spaceship(d, 3840, 2160, nu=nu, nv=nv, ships=8))
+        return f"spaceship-like Mitsuba XML 3840x2160, {2 * nu * (nv - 1)} tris x 8 instances (configs[3])"
+    if name == "lamp":
+        scene.load_from_file(write_lamp(d, 3840, 2160, segments=48 if small else 96))
+        return "lamp-like Mitsuba XML 3840x2160, thin lens, triangle emitters (configs[4])"
+    raise ValueError(f"unknown config {name!r} (one of {', '.join(CONFIGS)})")
+
+
+def default_pool(width: int, height: int) -> int:
+    """Path-pool slots for several images in flight: 2^24 at 1080p, 2^26 at 4K."""
+    return 1 << 24 if width * height <= (1 << 21) else 1 << 26
+

@@ -44,3 +44,18 @@ def test_two_rank_bench_film_equals_single_rank(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     a = np.load(single)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_bench_runs_other_baseline_configs(tmp_path):
+    """bench.py --config: BASELINE configs[2] (coffee-like XML scene) through the same
+    path; one JSON line with its own metric name and the ray totals."""
+    import json
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", "coffee", "--steps", "1", "--warmup", "0",
+                        "--no-cpu-baseline", "--scene-dir", str(tmp_path)], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    assert d["config"]["name"] == "coffee" and "coffee" in d["metric"] and d["config"]["rays"] > 0
+

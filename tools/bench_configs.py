@@ -23,24 +23,7 @@ HBM_PEAK_GBS = 8000.0
 def setup(name, scene_dir: Path, small: bool):
     from directcomputeraytracing_amd import Scene, scenes
     s = Scene((1920, 1080))
-    if name == "cornell":
-        scenes.setup_cornell(s, 1920, 1080, 8)
-        return s, "Cornell box OBJ 1920x1080, 8 bounces (configs[1])"
-    if name == "coffee":
-        p = scenes.write_coffee(scene_dir, 1920, 1080, segments=48 if small else 96)
-        s.load_from_file(p)
-        s.set_environment_light((1.0, 1.0, 1.0), scenes.env_cube(64))
-        return s, "coffee-like XML 1920x1080, env cube + constant, max_depth 8 (configs[2])"
-    if name == "spaceship":
-        nu, nv = (64, 32) if small else (512, 256)
-        p = scenes.write_spaceship(scene_dir, 3840, 2160, nu=nu, nv=nv, ships=8)
-        s.load_from_file(p)
-        return s, f"spaceship-like XML 3840x2160, {2 * nu * (nv - 1)} tris x 8 instances (configs[3], 1 GPU)"
-    if name == "lamp":
-        p = scenes.write_lamp(scene_dir, 3840, 2160, segments=48 if small else 96)
-        s.load_from_file(p)
-        return s, "lamp-like XML 3840x2160, thin lens, triangle emitters (configs[4], 1 GPU)"
-    raise ValueError(name)
+    return s, scenes.setup_config(s, name, scene_dir, small)
 
 
 def run(name, args):
@@ -50,7 +33,8 @@ def run(name, args):
     load_s = time.perf_counter() - t0
     W, H = scene.resolution
     # several images in flight (an image batch), so each batch drains once: 8 images at 1080p, 8 at 4K
-    pool = args.pool or (1 << 24 if W * H <= (1 << 21) else 1 << 26)
+    from directcomputeraytracing_amd import scenes
+    pool = args.pool or scenes.default_pool(W, H)
     filt = scene.filter_params()
     # the timed images on --streams concurrent pipelines (film bands, bench.py --streams)
     from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
