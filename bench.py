@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--config", default="cornell", choices=["cornell", "coffee", "spaceship", "lamp"],
                     help="BASELINE.json configs[1..4]; the headline (and default) is cornell = configs[1]")
     ap.add_argument("--scene-dir", default="/tmp/dcrt_scenes", help="where the procedural config scenes are written")
+    ap.add_argument("--snapshot-spp", type=int, default=0,
+                    help="progressive: reduce the film onto rank 0 every K images (configs[4]); 0 = once at the end")
     ap.add_argument("--pool", type=int, default=0,
                     help="path pool slots (0: 2^24 at 1080p = 8 images in flight, one drain per batch; 2^26 at 4K)")
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
@@ -116,6 +118,11 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
+    if args.snapshot_spp and world == 1:
+        # torch (its own HIP runtime) must own the device before libdcrt's runtime does
+        import torch
+        torch.cuda.set_device(device)
+
     import numpy as np
     from directcomputeraytracing_amd import Scene, WavefrontPathTracer, render_images_concurrently, scenes
     luts_arrays = dict(np.load(ROOT / "tests" / "golden" / "bxdf_luts.npz"))
@@ -176,6 +183,28 @@ def main():
         import torch
         film_buf = torch.empty(args.width * args.height * 4, dtype=torch.float32, device="cuda" if on_device else "cpu")
 
+    snap_dev = snap_tmp = None
+    if args.snapshot_spp:
+        import torch
+        n4 = args.width * args.height * 4
+        snap_dev = film_buf if (film_buf is not None and on_device) else torch.empty(n4, dtype=torch.float32, device="cuda")
+        snap_tmp = torch.empty(n4, dtype=torch.float32, device="cuda") if K > 1 else None
+
+    def snapshot_film():
+        # the rank's film = sum of its pipelines' films (disjoint supports), then the reduce
+        import torch
+        for t in tracers:
+            t.synchronize()
+        tracers[0].copy_film_device(snap_dev.data_ptr())
+        for t in tracers[1:]:
+            t.copy_film_device(snap_tmp.data_ptr())
+            snap_dev.add_(snap_tmp)
+        torch.cuda.synchronize()
+        if dist is not None:
+            if not on_device:
+                film_buf.copy_(snap_dev.cpu())
+            dist.reduce(film_buf, dst=0, op=dist.ReduceOp.SUM)
+
     def reduce_film():
         # the one data-path collective: SUM of the disjointly-supported stripe films on rank 0
         if on_device:
@@ -197,10 +226,21 @@ def main():
         t.reset_stats()
     barrier_sync()
     t0 = time.perf_counter()
-    render_all(0, images)
-    combine_films()
-    if dist is not None:
-        reduce_film()
+    if args.snapshot_spp and args.snapshot_spp < images:
+        # progressive rendering (configs[4]): every K images the films so far are summed
+        # over the pipelines and reduced onto rank 0 (a preview); the tracers' films keep
+        # accumulating, so the last snapshot is the whole render
+        done = 0
+        while done < images:
+            n = min(args.snapshot_spp, images - done)
+            render_all(done, n)
+            done += n
+            snapshot_film()
+    else:
+        render_all(0, images)
+        combine_films()
+        if dist is not None:
+            reduce_film()
     barrier_sync()
     elapsed = time.perf_counter() - t0
     rays = 0
@@ -218,7 +258,8 @@ def main():
         elapsed, rays = float(tmax.item()), float(tsum.item())
 
     if args.save_film and rank == 0:
-        film = film_buf.cpu().numpy() if dist is not None else tracer.read_film()
+        film = (film_buf if dist is not None else snap_dev).cpu().numpy() if (dist is not None or args.snapshot_spp) \
+            else tracer.read_film()
         np.save(args.save_film, film.reshape(args.height, args.width, 4))
 
     # ---- roofline leg: same workload (seeds 0..R-1), counters then HIP-event timing, on
@@ -252,7 +293,9 @@ def main():
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     traffic = None
     cands = sorted((ROOT / "profiles").glob("r*_pmc_traffic.json"))
-    tj = Path(args.traffic_json) if args.traffic_json else (cands[-1] if cands else Path("/nonexistent"))
+    # the committed PMC summary is the headline config's; other configs report null unless given one
+    default_tj = cands[-1] if (cands and args.config == "cornell") else Path("/nonexistent")
+    tj = Path(args.traffic_json) if args.traffic_json else default_tj
     if tj.exists():
         try:
             traffic = json.loads(tj.read_text()).get("ext_hbm_bytes_per_launch")
@@ -277,7 +320,7 @@ def main():
         "config": {"workload": workload.format(spp=images), "name": args.config,
                    "resolution": [args.width, args.height], "spp": images,
                    "max_bounce": args.bounces if args.config == "cornell" else scene.frame_params(0).max_bounce_count,
-                   "path_pool": args.pool, "streams_per_gpu": K,
+                   "path_pool": args.pool, "streams_per_gpu": K, "snapshot_spp": args.snapshot_spp or images,
                    "parallelism": (f"film stripes x{world}" if world > 1 else "single GPU")
                                   + (f", {K} concurrent pipelines per GPU" if K > 1 else ""),
                    "rays": int(rays)},

@@ -59,3 +59,28 @@ def test_bench_runs_other_baseline_configs(tmp_path):
     d = json.loads(line[0])
     assert d["config"]["name"] == "coffee" and "coffee" in d["metric"] and d["config"]["rays"] > 0
 
+
+def test_progressive_snapshots_give_the_same_film(tmp_path):
+    """bench.py --snapshot-spp K (configs[4]'s progressive reduce every K images, two
+    pipelines summed per snapshot): the last snapshot is the film of one pass, bit for bit."""
+    common = ["--steps", "3", "--warmup", "0", "--width", "160", "--height", "96", "--bounces", "4",
+              "--pool", str(1 << 16), "--no-cpu-baseline", "--roofline-images", "1"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    films = []
+    for extra in ([], ["--snapshot-spp", "1"]):
+        out = tmp_path / f"film{len(films)}.npy"
+        r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *common, *extra, "--save-film", str(out)],
+                           capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        films.append(np.load(out))
+    assert np.array_equal(films[0].view(np.uint32), films[1].view(np.uint32))
+
+
+def test_torch_rccl_buffer_interop():
+    """The N-GPU film path's buffer handoff (libdcrt <-> torch tensor <-> RCCL reduce,
+    device-side film add), in a fresh process: tools/interop_check.py."""
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "interop_check.py"), str(_port())], capture_output=True,
+                       text=True, timeout=600, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, (r.stdout[-1000:], r.stderr[-2000:])
+    assert "copy True reduce True add True" in r.stdout
+
