@@ -43,6 +43,11 @@ struct Globals {
     uint32_t imagesDone, imageTarget, seedBase;
     uint32_t batchImages;     // images path-traced together in the current batch (image index in [0, batchImages))
     uint32_t batchCap;        // RenderImages' batch size
+    // Batch start without atomics: RenderImages' first CONTROL pass of a batch finds every
+    // slot idle, so wave j (in workgroup order) of shard s takes the shard's j-th pixel
+    // block outright and the shard cursors are preset past those blocks (staticGrid =
+    // CONTROL workgroups, 0 = off); cleared after that iteration.
+    uint32_t staticFill, staticGrid;
     unsigned long long extRays, shadowRays, iterations;
 };
 

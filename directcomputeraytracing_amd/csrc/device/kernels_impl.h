@@ -59,7 +59,22 @@ __global__ void set_idle_kernel(PathPool pool, Counters* counters, Globals* g, u
         g->stopped = 0u;
         g->imagesDone = 0u;
         g->imageTarget = 1u;
+        g->staticFill = 0u;
+        g->staticGrid = 0u;
     }
+}
+
+// Preset the shard cursors for a batch start (see Globals::staticFill): shard s's first
+// min(waves of its CONTROL workgroups, its blocks) blocks are taken statically.
+__device__ __forceinline__ void begin_batch_claims(Globals* g)
+{
+    const uint32_t G = g->staticGrid, wavesPerGroup = kControlBlock >> 6;
+    for (uint32_t s = 0; s < kShards; ++s) {
+        const uint32_t blocks = g->totalBlocks > s ? (g->totalBlocks - s + kShards - 1) / kShards : 0u;
+        const uint32_t waves = G > s ? ((G - s + kShards - 1) / kShards) * wavesPerGroup : 0u;
+        g->nextBlock[s * kShardStride] = G ? min(blocks, waves) : 0u;
+    }
+    g->staticFill = G ? 1u : 0u;
 }
 
 __global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32_t* triangles, uint32_t count, float4* out)
@@ -88,6 +103,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     uint32_t* cursor = &g->nextBlock[shard * kShardStride];
     // pixel blocks of this shard: shard, shard + kShards, ...
     const uint32_t shardBlocks = g->totalBlocks > shard ? (g->totalBlocks - shard + kShards - 1) / kShards : 0u;
+    const bool staticFill = g->staticFill != 0u;   // (the grid then covers the pool exactly once)
     for (uint32_t base = blockIdx.x * blockDim.x; base < pool.size; base += gridDim.x * blockDim.x) {
     const uint32_t tid = base + threadIdx.x;
     const uint32_t flags = pool.flags[tid];
@@ -114,13 +130,21 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     const uint32_t mslot = block_append(!idle, qctr(cnt, kQMaterial, shard), sm);
     if (!idle) pool.materialQueue[(size_t)shard * pool.size + mslot] = tid;
 
-    // A fully idle wave claims the next 8x8 block (one atomic per workgroup).
+    // A fully idle wave claims the next 8x8 block (one atomic per workgroup); at a batch
+    // start (all slots idle, cursors preset) wave j of the shard takes block j outright.
     const bool waveIdle = __ballot(!idle) == 0ull;
-    bool want = false;
-    if (waveIdle && lane == 0) want = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shardBlocks;
-    const uint32_t bslot = block_append(want, cursor, sm);
-    const uint32_t claimed = (uint32_t)__shfl((int)bslot, 0, 64);
-    const bool got = __shfl((int)want, 0, 64) != 0 && claimed < shardBlocks;
+    uint32_t claimed = 0;
+    bool got = false;
+    if (staticFill) {
+        claimed = (blockIdx.x / kShards) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        got = waveIdle && claimed < shardBlocks;
+    } else {
+        bool want = false;
+        if (waveIdle && lane == 0) want = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shardBlocks;
+        const uint32_t bslot = block_append(want, cursor, sm);
+        claimed = (uint32_t)__shfl((int)bslot, 0, 64);
+        got = __shfl((int)want, 0, 64) != 0 && claimed < shardBlocks;
+    }
     const uint32_t block = shard + claimed * kShards;
     bool newPath = false;
     if (got) {
@@ -439,6 +463,7 @@ __device__ __forceinline__ void end_iteration(const Counters* cnt, Counters* nex
             g->extRays += ext;
             g->shadowRays += shadowRays;
             g->iterations += 1ull;
+            g->staticFill = 0u;   // only a batch's first CONTROL pass claims statically
             // IsImageComplete (WavefrontPathTracer.cpp:508-523), exact and on the device
             g->imageComplete = (material == 0u && ext == 0u && !g->stopped) ? 1u : 0u;
         }
@@ -816,13 +841,14 @@ __global__ void advance_image_kernel(FrameConstants* fc, Globals* g)
         fc->frameSeed = g->seedBase + g->imagesDone;
         g->batchImages = min(g->batchCap, g->imageTarget - g->imagesDone);
         g->totalBlocks = fc->blocksPerImage * g->batchImages;
-        for (uint32_t s = 0; s < kShards; ++s) g->nextBlock[s * kShardStride] = 0u;
+        begin_batch_claims(g);
     } else {
         g->stopped = 1u;
     }
 }
 
-__global__ void begin_images_kernel(Globals* g, const FrameConstants* fc, uint32_t count, uint32_t firstSeed, uint32_t batchCap)
+__global__ void begin_images_kernel(Globals* g, const FrameConstants* fc, uint32_t count, uint32_t firstSeed, uint32_t batchCap,
+                                    uint32_t staticGrid)
 {
     if (threadIdx.x != 0) return;
     g->imagesDone = 0u;
@@ -833,6 +859,8 @@ __global__ void begin_images_kernel(Globals* g, const FrameConstants* fc, uint32
     g->totalBlocks = fc->blocksPerImage * g->batchImages;
     g->stopped = count == 0u ? 1u : 0u;
     g->imageComplete = 0u;
+    g->staticGrid = staticGrid;
+    begin_batch_claims(g);
 }
 
 // ---- post-processing: SumLuminance.hlsl + PostProcessings.hlsl ---------------------------

@@ -861,7 +861,11 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     frame.frame_seed = firstSeed;
     CHECKED(UploadFilter(filter));
     CHECKED(BeginImage());
-    hipLaunchKernelGGL(begin_images_kernel, dim3(1), dim3(64), 0, stream, dGlobals, (const FrameConstants*)dFrame, count, firstSeed, batch);
+    // static batch-start claims need one CONTROL thread per slot (an uncapped grid)
+    const uint32_t controlGrid = poolSize / kControlBlock;
+    const uint32_t staticGrid = controlGrid <= kControlMaxBlocks ? controlGrid : 0u;
+    hipLaunchKernelGGL(begin_images_kernel, dim3(1), dim3(64), 0, stream, dGlobals, (const FrameConstants*)dFrame, count, firstSeed, batch,
+                       staticGrid);
     HIPCHECK(hipGetLastError());
     // a path needs maxBounce + 3 iterations; cap the total so a broken scene cannot spin forever
     const uint64_t maxIterations = ((uint64_t)count + 2) * (frame.max_bounce_count + 8) * (1 + (filmW * (uint64_t)filmH) / poolSize) + 64;
