@@ -782,6 +782,25 @@ __device__ __forceinline__ float evaluate_filter(const FilterConsts& c, float px
 
 // SampleConvolution (SampleConvolution.hlsl:67-106), grid-stride over pixels. With
 // `guard` set it runs only in the iteration that completed an image (RenderImages).
+// One 16x16 pixel tile per workgroup: each image's samples of the tile plus the filter's
+// halo are staged in LDS once (instead of every pixel fetching its (2r+1)^2 window from
+// memory), then every pixel gathers its window from LDS. Per pixel the arithmetic and its
+// order are those of the direct gather (images in order, window rows then columns).
+constexpr int kFilmTile = 16;
+constexpr int kFilmMaxHalo = 4;
+constexpr int kFilmSpan = kFilmTile + 2 * kFilmMaxHalo;
+
+__device__ __forceinline__ void film_pixel_window(const FilterConsts& c, uint32_t px, uint32_t py, uint32_t W, uint32_t H,
+                                                  int* xs, int* xe, int* ys, int* ye)
+{
+    const float r = c.radius;
+    const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
+    *xs = (int)floorf(cx - r); *xs = *xs < 0 ? 0 : *xs;
+    *xe = (int)floorf(cx + r); *xe = *xe > (int)W - 1 ? (int)W - 1 : *xe;
+    *ys = (int)floorf(cy - r); *ys = *ys < 0 ? 0 : *ys;
+    *ye = (int)floorf(cy + r); *ye = *ye > (int)H - 1 ? (int)H - 1 : *ye;
+}
+
 __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t images, const Globals* guard)
 {
     if (guard && !guard->imageComplete) return;
@@ -791,33 +810,73 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
     const FilterConsts c = *fcon;
     const uint32_t W = film.width, H = film.height;
     const uint32_t total = W * H;
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
-        const uint32_t py = p / W, px = p - py * W;
-        if (film.rowOwned && !film.rowOwned[py]) continue;
-        const float r = c.radius;
-        const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
-        int xs = (int)floorf(cx - r); xs = xs < 0 ? 0 : xs;
-        int xe = (int)floorf(cx + r); xe = xe > (int)W - 1 ? (int)W - 1 : xe;
-        int ys = (int)floorf(cy - r); ys = ys < 0 ? 0 : ys;
-        int ye = (int)floorf(cy + r); ye = ye > (int)H - 1 ? (int)H - 1 : ye;
-        float4 v = film.accum[p];
-        for (uint32_t b = 0; b < count; ++b) {
-            const float2* sPos = film.samplePosition + (size_t)b * total;
-            const float4* sVal = film.sampleValue + (size_t)b * total;
-            float wsum = 0.0f;
-            V3 sum = mk(0.0f, 0.0f, 0.0f);
-            for (int y = ys; y <= ye; ++y)
-                for (int x = xs; x <= xe; ++x) {
-                    const size_t q = (size_t)y * W + x;
-                    const float2 sp = sPos[q];
-                    const float4 sv = sVal[q];
-                    const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
-                    sum = sum + mk(sv.x, sv.y, sv.z) * w;
-                    wsum = wsum + w;
-                }
-            v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
+    const int halo = (int)floorf(c.radius + 0.5f);
+    const uint32_t tilesX = (W + kFilmTile - 1) / kFilmTile, tiles = tilesX * ((H + kFilmTile - 1) / kFilmTile);
+    __shared__ float2 tPos[kFilmSpan * kFilmSpan];
+    __shared__ float4 tVal[kFilmSpan * kFilmSpan];
+    for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        const int x0 = (int)(tile % tilesX) * kFilmTile, y0 = (int)(tile / tilesX) * kFilmTile;
+        const uint32_t px = (uint32_t)x0 + (threadIdx.x % kFilmTile), py = (uint32_t)y0 + (threadIdx.x / kFilmTile);
+        const bool mine = px < W && py < H && !(film.rowOwned && !film.rowOwned[py]);
+        int xs = 0, xe = -1, ys = 0, ye = -1;
+        float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (mine) {
+            film_pixel_window(c, px, py, W, H, &xs, &xe, &ys, &ye);
+            v = film.accum[(size_t)py * W + px];
         }
-        film.accum[p] = v;
+        if (halo > kFilmMaxHalo) {
+            // wide filters: the direct gather from memory
+            for (uint32_t b = 0; b < count && mine; ++b) {
+                const float2* sPos = film.samplePosition + (size_t)b * total;
+                const float4* sVal = film.sampleValue + (size_t)b * total;
+                const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
+                float wsum = 0.0f;
+                V3 sum = mk(0.0f, 0.0f, 0.0f);
+                for (int y = ys; y <= ye; ++y)
+                    for (int x = xs; x <= xe; ++x) {
+                        const size_t q = (size_t)y * W + x;
+                        const float2 sp = sPos[q];
+                        const float4 sv = sVal[q];
+                        const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
+                        sum = sum + mk(sv.x, sv.y, sv.z) * w;
+                        wsum = wsum + w;
+                    }
+                v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
+            }
+        } else {
+            const int span = kFilmTile + 2 * halo, ox = x0 - halo, oy = y0 - halo;
+            for (uint32_t b = 0; b < count; ++b) {
+                const float2* sPos = film.samplePosition + (size_t)b * total;
+                const float4* sVal = film.sampleValue + (size_t)b * total;
+                __syncthreads();   // the previous image's tile is no longer read
+                for (int i = (int)threadIdx.x; i < span * span; i += (int)blockDim.x) {
+                    const int gx = ox + i % span, gy = oy + i / span;
+                    if (gx >= 0 && gy >= 0 && gx < (int)W && gy < (int)H) {
+                        const size_t q = (size_t)gy * W + gx;
+                        tPos[i] = sPos[q];
+                        tVal[i] = sVal[q];
+                    }
+                }
+                __syncthreads();
+                if (mine) {
+                    const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
+                    float wsum = 0.0f;
+                    V3 sum = mk(0.0f, 0.0f, 0.0f);
+                    for (int y = ys; y <= ye; ++y)
+                        for (int x = xs; x <= xe; ++x) {
+                            const int i = (y - oy) * span + (x - ox);
+                            const float2 sp = tPos[i];
+                            const float4 sv = tVal[i];
+                            const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
+                            sum = sum + mk(sv.x, sv.y, sv.z) * w;
+                            wsum = wsum + w;
+                        }
+                    v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
+                }
+            }
+        }
+        if (mine) film.accum[(size_t)py * W + px] = v;
+        __syncthreads();   // the tile buffers are reused by the next tile
     }
 }
 

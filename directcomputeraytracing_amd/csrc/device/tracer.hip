@@ -182,7 +182,8 @@ struct dcrt_tracer {
             g.iters = 0;
         }
     }
-    uint32_t FilmGrid() const { return std::max<uint32_t>(1u, std::min<uint32_t>((filmW * filmH + 255) / 256, kMaxPersistentBlocks)); }
+    // film_kernel: one 16x16 tile per workgroup (grid-stride beyond the cap)
+    uint32_t FilmGrid() const { return std::max<uint32_t>(1u, std::min<uint32_t>(((filmW + 15) / 16) * ((filmH + 15) / 16), 8u * kMaxPersistentBlocks)); }
     uint32_t castResident = 0;         // persistent cast grid: resident workgroups on the whole chip
     uint32_t castResidentOpacity = 0;  // the same for the ALLOW_ANYHIT_SHADER variant
     uint32_t megaResident = 0;         // persistent megakernel grid
