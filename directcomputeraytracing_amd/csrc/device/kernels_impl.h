@@ -174,7 +174,8 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     }
     const uint32_t eslot = block_append(newPath, qctr(cnt, kQExt, shard), sm);
     if (newPath) pool.extQueue[(size_t)shard * pool.size + eslot] = tid;
-    pool.flags[tid] = (idle ? kFlagIdle : 0u) | (carryShadowHit ? kFlagShadowRayHit : 0u) | (bounce & 0xFFu);
+    const uint32_t newFlags = (idle ? kFlagIdle : 0u) | (carryShadowHit ? kFlagShadowRayHit : 0u) | (bounce & 0xFFu);
+    if (newFlags != flags) pool.flags[tid] = newFlags;   // a live path's flags mostly stay as they are
     }
 }
 
