@@ -11,7 +11,7 @@ for f in glob.glob(f"{d}/pass*_counter_collection.csv"):
         k = r["Kernel_Name"].replace("void ", "").replace("dcrt::dev::", "").split("(")[0]
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k in sorted(agg):
-    if not any(x in k for x in ("extension", "shadow", "material", "control")):
+    if not any(x in k for x in ("extension", "shadow", "material", "control", "cast")):
         continue
     print(k)
     for c, v in sorted(agg[k].items()):
