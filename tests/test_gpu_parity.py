@@ -111,6 +111,43 @@ def test_render_8_bounces_odd_size_bit_exact(gpu_tracer, golden_luts, oracle_mod
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 1, 5]))
 
 
+@pytest.mark.parametrize("w,h,bounces", [(1, 1, 3), (1, 9, 2), (9, 1, 2), (17, 3, 0)])
+def test_degenerate_films_bit_exact(native_lib, golden_luts, oracle_mod, w, h, bounces):
+    """Edge sizes: a single pixel, one-column / one-row films (every 8x8 pixel block
+    ragged), maxBounce 0 (CheckTermination after the camera ray only). Samples, RNG and
+    the ray counts (WavefrontPathTracer.cpp:508-523 stats) equal the oracle's."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    t = WavefrontPathTracer(path_pool_size=1 << 10, debug_rng=True)
+    try:
+        s = cornell(w, h, bounces)
+        for c, c_ref in _render_and_compare(t, oracle_mod, golden_luts, s, [2]):
+            assert c["extension_rays"] == c_ref["extension_rays"]
+            assert c["shadow_rays"] == c_ref["shadow_rays"]
+            assert c["new_paths"] == w * h
+    finally:
+        t.destroy()
+
+
+def test_scene_without_lights_bit_exact(native_lib, golden_luts, oracle_mod):
+    """lightCount 0: MATERIAL skips light sampling (no shadow rays), every sample is
+    black, paths still bounce until termination (WavefrontPathTracing.hlsl:367-391)."""
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
+    s = Scene((24, 16))
+    s.reset(24, 16)
+    s.load_from_file(scenes.CORNELL_OBJ)
+    s.set_max_bounce(3)
+    t = WavefrontPathTracer(path_pool_size=1 << 10, debug_rng=True)
+    try:
+        for c, c_ref in _render_and_compare(t, oracle_mod, golden_luts, s, [0]):
+            assert c["shadow_rays"] == 0 and c_ref["shadow_rays"] == 0
+            assert c["extension_rays"] == c_ref["extension_rays"]
+        _, val = t.read_samples()
+        assert not val[..., :3].any()
+    finally:
+        t.destroy()
+    s.close()
+
+
 def test_render_full_1080p_one_spp_bit_exact(native_lib, golden_luts, oracle_mod):
     """configs[1] resolution and depth: 1920x1080, 8 bounces, one image, whole film."""
     from directcomputeraytracing_amd import WavefrontPathTracer
