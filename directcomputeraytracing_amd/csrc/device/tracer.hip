@@ -101,7 +101,7 @@ struct dcrt_tracer {
     uint32_t poolSize = 0;
     uint32_t iterationsPerRender = kDefaultIterations;
     bool debugRng = false;
-    uint32_t refillLanes = 16, parkLanes = 32;   // DCRT_TRAVERSAL_TUNE="refill,park" overrides
+    uint32_t refillLanes = 36, parkLanes = 24;   // DCRT_TRAVERSAL_TUNE="refill,park" overrides (profiles/r01_tune_sweep.txt)
     uint64_t imagesCompleted = 0;                // since the last ResetStats (counters())
 
     std::vector<void*> poolAllocs, sceneAllocs, filmAllocs, sampleAllocs, rowAllocs;

@@ -1,6 +1,6 @@
 set -u
 mkdir -p gpurun_out
-for t in 16,32 8,32 16,16 16,48 32,32 16,64 4,24; do
+for t in ${TUNES:-16,32 24,32 32,32 40,32 48,32 32,24 32,40 32,48}; do
   DCRT_TRAVERSAL_TUNE=$t timeout -k 10 200 python bench.py --steps 24 --warmup 2 --no-cpu-baseline --roofline-images 1 > gpurun_out/sweep_$t.log 2>&1 || exit $?
   echo "$t $(python -c "import json;d=json.load(open('gpurun_out/sweep_$t.log'));print(d['ms_per_spp'], d['roofline']['avg_launch_us'])")"
 done
