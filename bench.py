@@ -12,8 +12,10 @@ closes the timed region.
 scenes, their resolutions) through the same path, on 1 or N GPUs.
 
 Prints ONE JSON line (rank 0). Besides the contract fields it carries
-``roofline`` (EXTENSION_RAY_CAST: algorithmic bytes / HIP-event kernel time
-against the MI355X HBM peak) and ``cpu_baseline`` (the oracle's scalar
+``roofline`` (the merged EXTENSION+SHADOW cast launch: algorithmic bytes per
+launch / HIP-event launch time against the MI355X HBM peak, next to the
+PMC-measured HBM bytes of the same launches when a profile of this workload is
+committed) and ``cpu_baseline`` (the oracle's scalar
 MegakernelPathTracing restatement on this host's cores, bounded sample).
 """
 from __future__ import annotations
@@ -63,7 +65,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample duration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary from tools/pmc_traffic.py (default: newest profiles/r*_pmc_traffic.json)")
+                    help="PMC summary from tools/pmc_traffic.py (default: the newest profiles/r*_pmc_traffic*.json "
+                         "whose recorded workload is this run's)")
     return ap.parse_args()
 
 
@@ -139,7 +142,7 @@ def main():
     args.pool = args.pool or scenes.default_pool(args.width, args.height)
     filt = scene.filter_params()
     from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
-    halo = max(1, halo_for_radius(filt.radius))
+    halo = max(1, halo_for_radius(filt.radius, args.height))
 
     def make_tracer(pool, part):
         t = WavefrontPathTracer(path_pool_size=pool, iterations_per_render=args.iterations, device=device)
@@ -199,6 +202,8 @@ def main():
         for t in tracers[1:]:
             t.copy_film_device(snap_tmp.data_ptr())
             snap_dev.add_(snap_tmp)
+            # the next pipeline's copy (on its own stream) overwrites snap_tmp: wait for the add
+            torch.cuda.synchronize()
         torch.cuda.synchronize()
         if dist is not None:
             if not on_device:
@@ -226,7 +231,8 @@ def main():
         t.reset_stats()
     barrier_sync()
     t0 = time.perf_counter()
-    if args.snapshot_spp and args.snapshot_spp < images:
+    snapshots = bool(args.snapshot_spp and args.snapshot_spp < images)
+    if snapshots:
         # progressive rendering (configs[4]): every K images the films so far are summed
         # over the pipelines and reduced onto rank 0 (a preview); the tracers' films keep
         # accumulating, so the last snapshot is the whole render
@@ -258,8 +264,14 @@ def main():
         elapsed, rays = float(tmax.item()), float(tsum.item())
 
     if args.save_film and rank == 0:
-        film = (film_buf if dist is not None else snap_dev).cpu().numpy() if (dist is not None or args.snapshot_spp) \
-            else tracer.read_film()
+        # the reduced film (N > 1), the last snapshot (one rank, snapshots taken), else tracer 0's
+        # film, which combine_films made the sum of the rank's pipelines
+        if dist is not None:
+            film = film_buf.cpu().numpy()
+        elif snapshots:
+            film = snap_dev.cpu().numpy()
+        else:
+            film = tracer.read_film()
         np.save(args.save_film, film.reshape(args.height, args.width, 4))
 
     # ---- roofline leg: same workload (seeds 0..R-1), counters then HIP-event timing, on
@@ -291,16 +303,24 @@ def main():
     avg_ms = tm["ext_kernel_ms"] / launches
     bytes_per_launch = cast_bytes / launches
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    cands = sorted((ROOT / "profiles").glob("r*_pmc_traffic.json"))
-    # the committed PMC summary is the headline config's; other configs report null unless given one
-    default_tj = cands[-1] if (cands and args.config == "cornell") else Path("/nonexistent")
-    tj = Path(args.traffic_json) if args.traffic_json else default_tj
-    if tj.exists():
+    # measured HBM traffic of the same cast launches: a committed rocprofv3 PMC summary of
+    # THIS workload (tools/profile.sh + tools/pmc_traffic.py record the workload they profiled),
+    # never a profile of another image count, pool or scene
+    workload_key = {"config": args.config, "resolution": [args.width, args.height], "images": R,
+                    "path_pool": args.pool, "world": world}
+    traffic, traffic_src = None, "no committed PMC profile of this workload"
+    cands = [Path(args.traffic_json)] if args.traffic_json else \
+        sorted((ROOT / "profiles").glob("r*_pmc_traffic*.json"), reverse=True)
+    for tj in cands:
         try:
-            traffic = json.loads(tj.read_text()).get("ext_hbm_bytes_per_launch")
+            d = json.loads(tj.read_text())
         except Exception:
-            traffic = None
+            continue
+        if d.get("workload") == workload_key and d.get("ext_hbm_bytes_per_launch"):
+            traffic = d["ext_hbm_bytes_per_launch"]
+            traffic_src = (f"{tj.relative_to(ROOT) if tj.is_relative_to(ROOT) else tj}: rocprofv3 PMC, "
+                           f"FETCH_SIZE x2 + WRITE_SIZE per cast launch, same workload")
+            break
 
     result = {
         "metric": ("Mrays/s and ms/spp at 1920x1080, 8-bounce wavefront" if args.config == "cornell"
@@ -325,12 +345,19 @@ def main():
                                   + (f", {K} concurrent pipelines per GPU" if K > 1 else ""),
                    "rays": int(rays)},
         "roofline": {"bound": "hbm",
+                     "basis": "algorithmic bytes: the reference's traversal counts (node visits, triangle tests, "
+                              "BLAS entries, from the instrumented kernel) x SURVEY 8(d)'s bytes per unit, "
+                              "wherever the bytes are served from (LDS scene cache, L1, L2, MALL or HBM)",
                      "kernel": "cast_kernel (EXTENSION_RAY_CAST + SHADOW_RAY_CAST, one launch)" if merged
                                else "extension_kernel (EXTENSION_RAY_CAST)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "hbm_measured": None if traffic is None else
+                     {"achieved": round(traffic / (avg_ms * 1e-3) / 1e9, 1),
+                      "frac": round(traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
                      "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 2),
-                     "launches": int(launches),
+                     "launches": int(launches), "images": R,
                      "per_ext_ray": {"nodes": st["ext_node_visits"] / max(1, cr["extension_rays"]),
                                      "tris": st["ext_triangle_tests"] / max(1, cr["extension_rays"]),
                                      "blas": st["ext_blas_entries"] / max(1, cr["extension_rays"])},

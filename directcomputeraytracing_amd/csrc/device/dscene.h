@@ -11,6 +11,39 @@
 namespace dcrt {
 namespace dev {
 
+// Scene capabilities a MATERIAL variant is compiled for (material_kernel<CAPS>). The host
+// (dcrt_tracer::UploadScene) computes what the uploaded scene uses -- material types,
+// multiscattering, textures, light types, an environment cube -- and launches the
+// smallest compiled variant that covers it (kCapAll otherwise). A variant states its
+// exclusions to the compiler (__builtin_assume) and so drops the code and the live
+// registers of paths the scene cannot take; every path the scene does take is the same
+// arithmetic in every variant, so results do not depend on the variant.
+constexpr uint32_t kCapMatDiffuse = 1u << 0;       // bit = 1 << DCRT_MATERIAL_TYPE_*
+constexpr uint32_t kCapMatPlastic = 1u << 1;
+constexpr uint32_t kCapMatConductor = 1u << 2;
+constexpr uint32_t kCapMatDielectric = 1u << 3;
+constexpr uint32_t kCapMatThin = 1u << 4;
+constexpr uint32_t kCapMultiscatter = 1u << 5;     // DCRT_MATERIAL_FLAG_MULTISCATTERING on some material
+constexpr uint32_t kCapTextures = 1u << 6;         // albedo textures or the roughness checkerboard
+constexpr uint32_t kCapLightPoint = 1u << 7;       // bit = DCRT_LIGHT_FLAGS_* << 7
+constexpr uint32_t kCapLightMesh = 1u << 8;
+constexpr uint32_t kCapLightDirectional = 1u << 9;
+constexpr uint32_t kCapLightEnv = 1u << 10;
+constexpr uint32_t kCapEnvCube = 1u << 11;
+constexpr uint32_t kCapAll = (1u << 12) - 1u;
+constexpr uint32_t kCapMaterialsMask = 0x1Fu;
+constexpr uint32_t kCapLightShift = 7;
+// Opaque delta-lit scenes (the Cornell configs): diffuse / plastic / conductor
+// materials without multiscattering or textures, point and directional lights.
+constexpr uint32_t kCapOpaqueDelta = kCapMatDiffuse | kCapMatPlastic | kCapMatConductor | kCapLightPoint | kCapLightDirectional;
+
+// Light-type flags a variant admits (the reference's light flags are one type bit each).
+template <uint32_t CAPS>
+DEV void assume_light_caps(uint32_t flags)
+{
+    if constexpr (CAPS != kCapAll) __builtin_assume((flags & ~((CAPS >> kCapLightShift) & 0xFu) & 0xFu) == 0u);
+}
+
 struct TextureDesc {
     uint32_t width, height, format, offset;   // offset into the texel blob (bytes)
 };
@@ -499,6 +532,7 @@ DEV V3 bary3(V3 p0, V3 p1, V3 p2, float u, float v)   // Math.inc.hlsl:35-43
     return r1;
 }
 
+template <uint32_t CAPS = kCapAll>
 DEV void hit_to_intersection(const DeviceScene& s, const HitRecord& h, Intersection& it)
 {
     const uint32_t inst = h.inst, tri = h.tri & 0x7FFFFFFFu;
@@ -527,6 +561,15 @@ DEV void hit_to_intersection(const DeviceScene& s, const HitRecord& h, Intersect
     it.geometryNormal = normalize(cross(p2 - p0, p1 - p0));
     const uint32_t mid = ov != DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE ? ov : s.materialIds[tri];
     const dcrt_material& m = s.materials[mid];
+    if constexpr ((CAPS & kCapTextures) == 0u) {
+        __builtin_assume(m.albedo_texture_index == -1);
+        __builtin_assume((m.flags & DCRT_MATERIAL_FLAG_ROUGHNESS_TEXTURE) == 0u);
+    }
+    if constexpr ((CAPS & kCapMultiscatter) == 0u) __builtin_assume((m.flags & DCRT_MATERIAL_FLAG_MULTISCATTERING) == 0u);
+    if constexpr ((CAPS & kCapMaterialsMask) != kCapMaterialsMask) {
+        __builtin_assume((m.flags & DCRT_MATERIAL_FLAG_TYPE_MASK) <= DCRT_MATERIAL_TYPE_THIN_DIELECTRIC);
+        __builtin_assume(((CAPS >> (m.flags & DCRT_MATERIAL_FLAG_TYPE_MASK)) & 1u) != 0u);
+    }
     // VectorBaryCentric2 (Math.inc.hlsl:23-33)
     float r1x = V1.texcoord[0] - V0.texcoord[0], r1y = V1.texcoord[1] - V0.texcoord[1];
     float r2x = V2.texcoord[0] - V0.texcoord[0], r2y = V2.texcoord[1] - V0.texcoord[1];
@@ -566,6 +609,7 @@ struct LightSample {
 };
 DEV V3 tri_pos(const DeviceScene& s, uint32_t tri, int k) { return ld3(s.vertices[s.triangles[tri * 3 + k]].position); }
 
+template <uint32_t CAPS = kCapAll>
 DEV LightSample sample_light(const DeviceScene& s, V3 p, uint32_t lightCount, Rng& rng)
 {
     LightSample r;
@@ -573,6 +617,8 @@ DEV LightSample sample_light(const DeviceScene& s, V3 p, uint32_t lightCount, Rn
     const float sel = next1(rng);
     const uint32_t li = (uint32_t)floorf(sel * (float)lightCount);
     const dcrt_light& L = s.lights[li];
+    assume_light_caps<CAPS>(L.flags);
+    if constexpr ((CAPS & kCapEnvCube) == 0u) __builtin_assume(s.envCube == nullptr);
     if (L.flags & DCRT_LIGHT_FLAGS_POINT_LIGHT) {
         r.wi = ld3(L.position_or_triangle_range) - p;
         r.distance = length(r.wi);
@@ -624,12 +670,15 @@ DEV LightSample sample_light(const DeviceScene& s, V3 p, uint32_t lightCount, Rn
     return r;
 }
 
+template <uint32_t CAPS = kCapAll>
 DEV void evaluate_light(const DeviceScene& s, uint32_t li, uint32_t tri, V3 normal, V3 wi, float distance, uint32_t lightCount,
                         V3* radiance, float* pdf)
 {
     *radiance = mk(0.0f, 0.0f, 0.0f);
     *pdf = 0.0f;
     const dcrt_light& L = s.lights[li];
+    assume_light_caps<CAPS>(L.flags);
+    if constexpr ((CAPS & kCapEnvCube) == 0u) __builtin_assume(s.envCube == nullptr);
     if (L.flags & DCRT_LIGHT_FLAGS_MESH_LIGHT) {
         const float4* M = s.transforms + (size_t)asu(L.position_or_triangle_range[2]) * 3;
         const V3 v0 = mul43(tri_pos(s, tri, 0), 1.0f, M), v1 = mul43(tri_pos(s, tri, 1), 1.0f, M), v2 = mul43(tri_pos(s, tri, 2), 1.0f, M);

@@ -185,6 +185,9 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
 #else
 #define DCRT_MATERIAL_OCCUPANCY
 #endif
+// CAPS: the scene capabilities this variant is compiled for (kCapAll = any scene; see
+// kCapOpaqueDelta in dscene.h and dcrt_tracer::UploadScene).
+template <uint32_t CAPS>
 __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt)
 {
     __shared__ uint32_t sm[64];
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         Intersection it;
         it.lightIndex = DCRT_LIGHT_INDEX_INVALID; it.triangleIndex = 0;
         it.geometryNormal = mk(0.0f, 0.0f, 0.0f);
-        if (hasHit) hit_to_intersection(sc, hit, it);
+        if (hasHit) hit_to_intersection<CAPS>(sc, hit, it);
         V3 T = mk(thr.x, thr.y, thr.z);
         V3 L = mk(li.x, li.y, li.z);
         // Evaluate light :331-349
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             const bool visible = (features & DCRT_FEATURE_LIGHT_VISIBLE) != 0;
             if (visible ? lightIndex != DCRT_LIGHT_INDEX_INVALID : (bounce > 0 && lightIndex != DCRT_LIGHT_INDEX_INVALID)) {
                 V3 radiance; float lightPdf;
-                evaluate_light(sc, lightIndex, it.triangleIndex, it.geometryNormal, dir, hit.t, fc->lightCount, &radiance, &lightPdf);
+                evaluate_light<CAPS>(sc, lightIndex, it.triangleIndex, it.geometryNormal, dir, hit.t, fc->lightCount, &radiance, &lightPdf);
                 if (lightPdf > 0.0f) {
                     const float weight = !(li.w != 0.0f) ? power_heuristic(thr.w, lightPdf) : 1.0f;
                     L = L + T * radiance * weight;
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             const V3 wo = -dir;
             const BsdfFrame bf = bsdf_frame(sc, wo, it);
             if (fc->lightCount != 0) {
-                const LightSample ls = sample_light(sc, it.position, fc->lightCount, rng);
+                const LightSample ls = sample_light<CAPS>(sc, it.position, fc->lightCount, rng);
                 if (any_pos(ls.radiance) && ls.pdf > 0.0f) {
                     const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, bf, it);
                     const float NdotWI = fabsf(dot(it.normal, ls.wi));
@@ -811,7 +814,6 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
     const FilterConsts c = *fcon;
     const uint32_t W = film.width, H = film.height;
     const uint32_t total = W * H;
-    const int halo = (int)floorf(c.radius + 0.5f);
     const uint32_t tilesX = (W + kFilmTile - 1) / kFilmTile, tiles = tilesX * ((H + kFilmTile - 1) / kFilmTile);
     __shared__ float2 tPos[kFilmSpan * kFilmSpan];
     __shared__ float4 tVal[kFilmSpan * kFilmSpan];
@@ -825,7 +827,16 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
             film_pixel_window(c, px, py, W, H, &xs, &xe, &ys, &ye);
             v = film.accum[(size_t)py * W + px];
         }
-        if (halo > kFilmMaxHalo) {
+        // The tile's staged span is the union of its pixels' windows, taken from the
+        // windows of its first and last pixel: floorf(p + 0.5 -/+ r) is monotone in p, so
+        // every window of the tile lies inside, whatever the rounding of p + 0.5 + r does
+        // (for r just below k + 0.5 a window can reach floor(r + 0.5) + 1 pixels out).
+        int txs, txe, tys, tye, unused0, unused1;
+        film_pixel_window(c, (uint32_t)x0, (uint32_t)y0, W, H, &txs, &unused0, &tys, &unused1);
+        film_pixel_window(c, min((uint32_t)x0 + kFilmTile - 1u, W - 1u), min((uint32_t)y0 + kFilmTile - 1u, H - 1u), W, H,
+                          &unused0, &txe, &unused1, &tye);
+        const int spanX = txe - txs + 1, spanY = tye - tys + 1;
+        if (spanX > kFilmSpan || spanY > kFilmSpan) {
             // wide filters: the direct gather from memory
             for (uint32_t b = 0; b < count && mine; ++b) {
                 const float2* sPos = film.samplePosition + (size_t)b * total;
@@ -845,18 +856,16 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
                 v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
             }
         } else {
-            const int span = kFilmTile + 2 * halo, ox = x0 - halo, oy = y0 - halo;
+            // staged span [txs, txe] x [tys, tye]: inside the film by construction
+            const int span = spanX, ox = txs, oy = tys;
             for (uint32_t b = 0; b < count; ++b) {
                 const float2* sPos = film.samplePosition + (size_t)b * total;
                 const float4* sVal = film.sampleValue + (size_t)b * total;
                 __syncthreads();   // the previous image's tile is no longer read
-                for (int i = (int)threadIdx.x; i < span * span; i += (int)blockDim.x) {
-                    const int gx = ox + i % span, gy = oy + i / span;
-                    if (gx >= 0 && gy >= 0 && gx < (int)W && gy < (int)H) {
-                        const size_t q = (size_t)gy * W + gx;
-                        tPos[i] = sPos[q];
-                        tVal[i] = sVal[q];
-                    }
+                for (int i = (int)threadIdx.x; i < spanX * spanY; i += (int)blockDim.x) {
+                    const size_t q = (size_t)(oy + i / spanX) * W + (size_t)(ox + i % spanX);
+                    tPos[i] = sPos[q];
+                    tVal[i] = sVal[q];
                 }
                 __syncthreads();
                 if (mine) {

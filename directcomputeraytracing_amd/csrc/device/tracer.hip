@@ -92,6 +92,24 @@ FilterConsts MakeFilter(const dcrt_filter_params& p)   // SampleConvolution.cpp:
     return c;
 }
 
+// Rows beyond its own that a film row's SampleConvolution window reaches
+// (SampleConvolution.hlsl:77-81), with the kernel's float arithmetic
+// (film_pixel_window): floor(r + 0.5) in exact arithmetic, one more where py + 0.5 + r
+// rounds up to the next integer (r just below k + 0.5).
+uint32_t FilterSupportRows(float r, uint32_t H)
+{
+    if (!(r < (float)H)) return H;
+    uint32_t rows = 0;
+    for (uint32_t py = 0; py < H; ++py) {
+        const float cy = (float)py + 0.5f;
+        int ys = (int)std::floor(cy - r), ye = (int)std::floor(cy + r);
+        ys = std::max(ys, 0);
+        ye = std::min(ye, (int)H - 1);
+        rows = std::max<uint32_t>(rows, (uint32_t)std::max(ye - (int)py, (int)py - ys));
+    }
+    return rows;
+}
+
 }  // namespace
 
 struct dcrt_tracer {
@@ -111,6 +129,8 @@ struct dcrt_tracer {
     uint32_t castBlock = 256;
     size_t castLds = 0;
     bool mergedCasts = true;           // one cast_kernel per iteration (DCRT_SPLIT_CASTS=1: EXT then SHADOW)
+    uint32_t sceneCaps = kCapAll;      // what the uploaded scene uses (kCap* of dscene.h)
+    uint32_t materialCaps = kCapAll;   // the MATERIAL variant launched for it
 
     dcrt_bxdf_luts* dLuts = nullptr;
     Film film{};
@@ -427,6 +447,20 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     d.triangleCount = s.triangle_count;
     d.stackSize = std::max<uint32_t>(s.bvh_traversal_stack_size, 1u);
     scene = d;
+    // MATERIAL variant: the smallest compiled one whose capabilities cover the scene
+    sceneCaps = dEnv ? kCapEnvCube : 0u;
+    for (uint32_t i = 0; i < s.material_count; ++i) {
+        const dcrt_material& m = s.materials[i];
+        const uint32_t type = m.flags & DCRT_MATERIAL_FLAG_TYPE_MASK;
+        sceneCaps |= type <= DCRT_MATERIAL_TYPE_THIN_DIELECTRIC ? (1u << type) : kCapAll;
+        if (m.flags & DCRT_MATERIAL_FLAG_MULTISCATTERING) sceneCaps |= kCapMultiscatter;
+        if (m.albedo_texture_index != -1 || (m.flags & DCRT_MATERIAL_FLAG_ROUGHNESS_TEXTURE)) sceneCaps |= kCapTextures;
+    }
+    for (uint32_t i = 0; i < s.light_count; ++i) sceneCaps |= (s.lights[i].flags & 0xFu) << kCapLightShift;
+    materialCaps = (sceneCaps & ~kCapOpaqueDelta) == 0u ? kCapOpaqueDelta : kCapAll;
+    if (const char* g = std::getenv("DCRT_MATERIAL_GENERIC")) {   // A/B: always the generic variant
+        if (std::atoi(g)) materialCaps = kCapAll;
+    }
     // LDS stack: [stackSize][block] u32; keep a workgroup's stack <= 32 KiB
     // (+1: a spare slot per lane that the branch-free push may write, never read)
     castBlock = 256;
@@ -665,7 +699,8 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     const uint32_t castGrid = CastGrid(castBlock, opacity);
     hipLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, pool, film, (const FrameConstants*)dFrame, cnt,
                        dGlobals, (uint32_t)(film.debugRng != nullptr));
-    hipLaunchKernelGGL(material_kernel, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt);
+    auto material = materialCaps == kCapOpaqueDelta ? material_kernel<kCapOpaqueDelta> : material_kernel<kCapAll>;
+    hipLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timed) {
         while (events.size() < eventsUsed + 2) {
@@ -821,9 +856,9 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
     if (count == 0) return DCRT_OK;
     if (partition.world_size > 1) {
-        // a partitioned film's convolution reads floor(r + 0.5) rows beyond its stripes
+        // a partitioned film's convolution reads the filter's window rows beyond its stripes
         const uint32_t halo = partition.halo_rows ? partition.halo_rows : 2u;
-        if (!(filter.radius >= 0.0f) || (double)std::floor(filter.radius + 0.5f) > (double)halo) {
+        if (!(filter.radius >= 0.0f) || FilterSupportRows(filter.radius, filmH) > halo) {
             SetLastError("filter radius needs more halo rows than the film partition renders");
             return DCRT_E_INVALID_ARG;
         }

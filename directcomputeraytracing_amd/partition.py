@@ -12,8 +12,6 @@ csrc/device.
 """
 from __future__ import annotations
 
-import math
-
 import numpy as np
 
 BLOCK_H = 8
@@ -62,9 +60,18 @@ def stream_partition(height: int, world_size: int, rank: int, streams: int, stre
     return v, stream * world_size + rank, max(1, round(height / (v * k)))
 
 
-def halo_for_radius(radius: float) -> int:
-    """Rows of support beyond a pixel row that SampleConvolution gathers (SampleConvolution.hlsl:77-81)."""
-    return int(math.floor(radius + 0.5))
+def halo_for_radius(radius: float, height: int = 65535) -> int:
+    """Rows of support beyond a pixel row that SampleConvolution gathers (SampleConvolution.hlsl:77-81),
+    in the kernel's float32 arithmetic over the film's rows (dcrt_tracer FilterSupportRows): floor(r + 0.5),
+    or one more where py + 0.5 + r rounds up to an integer (r just below k + 0.5)."""
+    r = np.float32(radius)
+    if not r < height:
+        return int(height)
+    py = np.arange(height, dtype=np.int64)
+    cy = py.astype(np.float32) + np.float32(0.5)
+    ys = np.maximum(np.floor(cy - r).astype(np.int64), 0)
+    ye = np.minimum(np.floor(cy + r).astype(np.int64), height - 1)
+    return int(max(int((ye - py).max()), int((py - ys).max()), 0))
 
 
 def row_runs(rows) -> list:

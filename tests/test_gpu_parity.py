@@ -184,6 +184,88 @@ def test_film_accumulation_matches_oracle(native_lib, golden_luts, oracle_mod):
         t.destroy()
 
 
+def test_film_radius_just_below_half_integer(native_lib, golden_luts, oracle_mod):
+    """A pixel's window [floor(c - r), floor(c + r)] reaches floor(r + 0.5) + 1 pixels out where
+    c + r rounds up to an integer (r = nextafter(1.5, 0) at c = 100.5): the LDS-staged film pass
+    stages each tile's exact window union, so such films stay bit-exact (odd film size: partial tiles)."""
+    from directcomputeraytracing_amd import FILTER_BOX, FILTER_GAUSSIAN, FILTER_TRIANGLE, FilterParams, \
+        WavefrontPathTracer
+    below = lambda x: float(np.nextafter(np.float32(x), np.float32(0)))
+    t = WavefrontPathTracer(path_pool_size=1 << 15)
+    try:
+        s = cornell(150, 70, 2)
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        flat = s.flat()
+        for filt in (FilterParams(FILTER_BOX, below(1.5), 1.5, 1 / 3, 1 / 3, 3),
+                     FilterParams(FILTER_TRIANGLE, below(1.5), 1.5, 1 / 3, 1 / 3, 3),
+                     FilterParams(FILTER_GAUSSIAN, below(2.5), 2.0, 1 / 3, 1 / 3, 3),
+                     FilterParams(FILTER_BOX, below(4.5), 1.5, 1 / 3, 1 / 3, 3)):
+            t.clear_film()
+            t.render_images(0, 2, filt)
+            film = t.read_film()
+            ref = np.zeros_like(film)
+            for seed in range(2):
+                p, v, _, _ = oracle_mod.render(flat, golden_luts, s.frame_params(seed), oracle_mod.WAVEFRONT)
+                oracle_mod.sample_convolution(filt, p, v, ref)
+            assert same_bits(film, ref).all(), f"filter {filt.filter} r={filt.radius!r}"
+    finally:
+        t.destroy()
+
+
+def test_film_partition_halo_for_radius_just_below_half_integer(native_lib, golden_luts):
+    """Partitioned films with r = nextafter(1.5, 0): the window reaches 2 rows out, so the partition
+    needs halo_for_radius(r) = 2 rows (1 is refused), and the rank films then sum to the 1-GPU film."""
+    from directcomputeraytracing_amd import DCRTError, FILTER_BOX, FilterParams, WavefrontPathTracer
+    from directcomputeraytracing_amd.partition import halo_for_radius
+    r = float(np.nextafter(np.float32(1.5), np.float32(0)))
+    filt = FilterParams(FILTER_BOX, r, 1.5, 1 / 3, 1 / 3, 3)
+    s = cornell(96, 120, 2)
+    halo = halo_for_radius(r, 120)
+    assert halo == 2
+    films = []
+    for world, rank, h in [(1, 0, 0), (3, 0, halo), (3, 1, halo), (3, 2, halo), (3, 1, 1)]:
+        t = WavefrontPathTracer(path_pool_size=1 << 15)
+        try:
+            t.set_luts(golden_luts)
+            t.on_scene_loaded(s)
+            t.set_film_partition(world, rank, 16, h)
+            t.clear_film()
+            if h == 1:
+                with pytest.raises(DCRTError):
+                    t.render_images(0, 2, filt)
+                continue
+            t.render_images(0, 2, filt)
+            films.append(t.read_film())
+        finally:
+            t.destroy()
+    assert same_bits(films[1] + films[2] + films[3], films[0]).all()
+
+
+def test_material_variant_matches_generic(native_lib, golden_luts, monkeypatch):
+    """The Cornell scene (diffuse/plastic, point light) runs the capability-specialised MATERIAL
+    variant (material_kernel<kCapOpaqueDelta>); forcing the generic variant gives the same bits
+    (samples, RNG states and film)."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    s = cornell(128, 72, 6)
+    out = []
+    for generic in ("0", "1"):
+        monkeypatch.setenv("DCRT_MATERIAL_GENERIC", generic)
+        t = WavefrontPathTracer(path_pool_size=1 << 14, debug_rng=True)
+        try:
+            t.set_luts(golden_luts)
+            t.on_scene_loaded(s)
+            t.clear_film()
+            t.render_images(3, 2)
+            out.append((t.read_samples(), t.read_rng(), t.read_film()))
+        finally:
+            t.destroy()
+    (p0, v0), r0, f0 = out[0]
+    (p1, v1), r1, f1 = out[1]
+    assert np.array_equal(r0, r1)
+    assert same_bits(p0, p1).all() and same_bits(v0, v1).all() and same_bits(f0, f1).all()
+
+
 def test_film_partition_sums_to_single_gpu(native_lib, golden_luts):
     """Stripes + halo per rank: the rank films sum to the 1-GPU film exactly."""
     from directcomputeraytracing_amd import WavefrontPathTracer

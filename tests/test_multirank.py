@@ -16,6 +16,24 @@ import pytest
 from conftest import GOLDEN, ROOT
 
 
+def test_halo_for_radius_matches_window_arithmetic():
+    """halo_for_radius = the furthest row a window [floor(py + 0.5 - r), floor(py + 0.5 + r)] reaches,
+    in float32 (film_kernel's arithmetic): floor(r + 0.5), one more for r just below k + 0.5."""
+    from directcomputeraytracing_amd.partition import halo_for_radius
+    below = lambda x: float(np.nextafter(np.float32(x), np.float32(0)))
+    H = 1080
+    for r in (0.5, 1.0, below(1.5), 1.5, 2.0, below(2.5), 2.5, 3.3, below(4.5)):
+        r32 = np.float32(r)
+        reach = 0
+        for py in range(H):
+            cy = np.float32(py) + np.float32(0.5)
+            ys = max(0, int(np.floor(cy - r32)))
+            ye = min(H - 1, int(np.floor(cy + r32)))
+            reach = max(reach, ye - py, py - ys)
+        assert halo_for_radius(r, H) == reach, r
+    assert halo_for_radius(below(1.5), H) == 2 and halo_for_radius(1.0, H) == 1
+
+
 def test_partition_rows_cover_film():
     from directcomputeraytracing_amd.partition import owned_rows, render_rows
     H, S = 1080, 64

@@ -7,7 +7,7 @@
   doubled; WRITE_SIZE is taken as is. Traffic is averaged per launch over the
   same whole-image launch mix the bench's roofline leg uses.
 
-Usage: python tools/pmc_traffic.py gpurun_out/prof profiles/r01
+Usage: python tools/pmc_traffic.py gpurun_out/prof profiles/r02_i20   (-> profiles/r02_i20_pmc_traffic.json)
 """
 import collections
 import csv
@@ -54,6 +54,15 @@ def main(src, dst_prefix):
     ext = next((v for k, v in out["kernels"].items() if k.startswith("dcrt::dev::cast_kernel<false")), None) or \
         next((v for k, v in out["kernels"].items() if k.startswith("dcrt::dev::extension_kernel<false")), {})
     out["ext_hbm_bytes_per_launch"] = ext.get("hbm_bytes_per_launch")
+    # the workload the PMC passes profiled (bench.py matches its own run against it)
+    log = src / "pmc_FETCH_SIZE.log"
+    line = next((l for l in (log.read_text().splitlines() if log.exists() else []) if l.startswith("{")), None)
+    if line:
+        b = json.loads(line)
+        cfg, roof = b["config"], b["roofline"]
+        out["workload"] = {"config": cfg["name"], "resolution": cfg["resolution"], "images": roof["images"],
+                           "path_pool": cfg["path_pool"], "world": b["n_gpus"]}
+        out["bench_avg_launch_us"] = roof["avg_launch_us"]
     Path(dst_prefix + "_pmc_traffic.json").write_text(json.dumps(out, indent=1, sort_keys=True))
     print(json.dumps({"ext_hbm_bytes_per_launch": out["ext_hbm_bytes_per_launch"]}))
 
