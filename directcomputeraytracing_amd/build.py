@@ -35,6 +35,11 @@ HIPCC_FLAGS = [
     "-fPIC",
     "-ffp-contract=off",      # no FMA contraction: bit-identical to the oracle
     "-fno-fast-math",
+    # no SLP vectorisation: its packed-f32 ops (v_pk_mul/add_f32, same IEEE results) cost
+    # registers (cast kernel 96 -> 78 VGPRs, MATERIAL 117 -> 104, 152 -> 125 without) and
+    # pair the refill's prefetch register with operands that then wait for it: Cornell
+    # 1080p 3.75 -> 3.49 ms/spp (tools/ab_libs.sh, two passes)
+    "-fno-slp-vectorize",
     "-fno-gpu-rdc",
     "-Wall",
     "-Wno-unused-function",

@@ -79,6 +79,7 @@ struct DeviceScene {
     uint32_t stackSize;           // per-lane traversal stack entries
     uint32_t cachedNodes;         // nodes [0, cachedNodes) are mirrored in LDS (scene_cache_load)
     uint32_t cachedTris;          // triVerts of triangles [0, cachedTris) likewise, after the nodes
+    uint32_t cachedInstances;     // 0, or instanceCount: every inverse transform + identity flag, after the triangles
 };
 
 // LDS scene cache of the traversal kernels: after the per-lane stacks ([stackSize + 1]
@@ -97,6 +98,12 @@ DEV void scene_cache_load(const DeviceScene& sc, uint32_t* stackMem, uint32_t sh
     const uint32_t nn = sc.cachedNodes * 2u, nt = sc.cachedTris * 3u;
     for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) c[i] = sc.nodes[i];
     for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) c[nn + i] = sc.triVerts[i];
+    // per instance: the inverse float4x3 (3 x float4), then (identity flag, 0, 0, 0)
+    for (uint32_t i = threadIdx.x; i < sc.cachedInstances * 4u; i += blockDim.x) {
+        const uint32_t inst = i >> 2, k = i & 3u;
+        c[nn + nt + i] = k < 3u ? sc.transforms[(size_t)(sc.instanceCount + inst) * 3 + k]
+                                : make_float4(__uint_as_float(sc.instanceIdentity[inst]), 0.0f, 0.0f, 0.0f);
+    }
     __syncthreads();
 }
 
@@ -217,6 +224,7 @@ struct TravState {
     uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked)
     bool inBlas, shearValid, found, parked, noZero;   // noZero: no component of o, d is +-0
     bool anyHit;          // merged cast kernel: this lane's ray is a shadow ray (first hit ends it)
+    uint32_t pathFlags;   // shadow ray: the path's flags as MATERIAL wrote them (shadowD.w)
     Shear sh;
     HitRecord hit;
     // ALLOW_ANYHIT_SHADER only (dead, and removed by the compiler, otherwise)
@@ -291,12 +299,22 @@ DEV bool trav_pop(const DeviceScene& sc, TravState& s, const uint32_t* lds, uint
 // Written without divergent branches: the push always stores (slot `count`, or the
 // spare slot `stackSize` past the end, which nothing reads), the pop always loads
 // the top, and selects pick the outcome; the lanes of a wave stay convergent.
-template <bool INSTR>
+// ALL_CACHED: the whole BVH and every triangle sit in the LDS scene cache (small scenes),
+// so node and triangle fetches are plain ds_read_b128 (no FLAT select, no global path).
+template <bool INSTR, bool ALL_CACHED = false>
 DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
+    // the stack top (read only by a pop) is issued together with the node fetch: this
+    // visit's push writes slot `count`, never the slot read here, so the two LDS round
+    // trips of a visit overlap instead of following each other
+    const uint32_t top = lds[(s.count > 0u ? min(s.count - 1u, sc.stackSize) : sc.stackSize) << shift];
     float4 a, b;
-    if (s.node < sc.cachedNodes) {
+    if (ALL_CACHED) {
+        const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
+        a = c[s.node * 2];
+        b = c[s.node * 2 + 1];
+    } else if (s.node < sc.cachedNodes) {
         const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
         a = c[s.node * 2];
         b = c[s.node * 2 + 1];
@@ -317,7 +335,6 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds
     const bool neg = f2b && ((axis == 0u && nx) | (axis == 1u && ny) | (axis == 2u && nz));
     const uint32_t nearChild = neg ? right : s.node + 1;
     const uint32_t farChild = neg ? s.node + 1 : right;
-    const uint32_t top = lds[(s.count > 0u ? min(s.count - 1u, sc.stackSize) : sc.stackSize) << shift];
     lds[min(s.count, sc.stackSize) << shift] = (farChild & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
     const bool pop = !hit && s.count > 0u;
     const bool done = !hit && s.count == 0u;
@@ -343,19 +360,27 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds
 // Phase B: the parked leaf's work. TLAS leaf: move the ray into the instance and
 // continue at its BLAS root. BLAS leaf: test triangles [ref, ref + count), then pop.
 // LANE_ANY: any-hit is a per-lane choice (s.anyHit), for the merged ray-cast kernel
-template <bool ANY_HIT, bool INSTR, bool OPACITY = false, bool LANE_ANY = false>
+template <bool ANY_HIT, bool INSTR, bool OPACITY = false, bool LANE_ANY = false, bool ALL_CACHED = false>
 DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     s.parked = false;
     const uint32_t primOrInst = (s.leafMisc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
     if (s.leafMisc & 0x4u) {
-        if (s.noZero && sc.instanceIdentity[primOrInst]) {
+        const float4* M;
+        uint32_t identity;
+        if (ALL_CACHED) {
+            M = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u + sc.cachedTris * 3u + primOrInst * 4u;
+            identity = __float_as_uint(M[3].x);
+        } else {
+            M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
+            identity = sc.instanceIdentity[primOrInst];
+        }
+        if (s.noZero && identity) {
             // x*1 + y*0 + z*0 + w*0 == x exactly for finite nonzero components
             s.lo = mk(s.o.x, s.o.y, s.o.z);
             s.ld = mk(s.d.x, s.d.y, s.d.z);
             s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
         } else {
-            const float4* M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
             s.lo = mul43(s.o, 1.0f, M);
             s.ld = mul43(s.d, 0.0f, M);
             s.inv = inv_dir(s.ld);
@@ -377,7 +402,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
     for (uint32_t p = begin; p < end; ++p) {
         if (INSTR) ++st.tris;
         float4 q0, q1, q2;
-        if (p < sc.cachedTris) {
+        if (ALL_CACHED || p < sc.cachedTris) {
             const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u;
             q0 = c[p * 3]; q1 = c[p * 3 + 1]; q2 = c[p * 3 + 2];
         } else {

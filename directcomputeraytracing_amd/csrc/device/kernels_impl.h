@@ -292,6 +292,9 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         }
         if (!hasShadow) flags = flags & ~kFlagShadowRayHit;
         pool.flags[path] = flags;
+        // the shadow cast writes the path's flags with the occlusion bit (a plain store, no
+        // read of the flags in front of it): it takes them from shadowD.w (tMin, unused: 0)
+        if (hasShadow) reinterpret_cast<float*>(&pool.shadowD[path])[3] = asf(flags);
         pool.rng[path] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
         pool.throughput[path] = make_float4(T.x, T.y, T.z, thr.w);
         pool.li[path] = make_float4(L.x, L.y, L.z, li.w);
@@ -349,16 +352,18 @@ __device__ uint32_t g_waveItems[2][16][8192];
 #define DCRT_WAVE_TAG(g) (-1)
 #endif
 
-template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, typename Fetch, typename Emit>
+template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, typename Lookup, typename Fetch,
+          typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
-                                                 uint32_t kParkLanes, uint32_t* lds, uint32_t shift, Fetch fetch, Emit emit,
-                                                 TraversalStats& st, int waveTag = -1)
+                                                 uint32_t kParkLanes, uint32_t* lds, uint32_t shift, Lookup lookup, Fetch fetch,
+                                                 Emit emit, TraversalStats& st, int waveTag = -1)
 {
     const bool watertight = (features & DCRT_FEATURE_WATERTIGHT) != 0;
     const bool f2b = (features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
     const uint32_t wavesPerBlock = blockDim.x >> 6;
     const uint32_t waves = gridDim.x * wavesPerBlock;
     const uint32_t waveId = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
     // Work split: the queue is cut into groups of kInterleave consecutive items (one
     // region of the image / one producer workgroup each) dealt round-robin to the
     // waves, so every wave samples the whole queue and per-wave costs even out
@@ -369,24 +374,49 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
     uint32_t cursor = 0;
     const uint32_t end = myGroups * kInterleave;
     const uint32_t chunk = end;   // (diagnostics)
+    // (24-bit multiply: a 32-bit a * b + c becomes v_mad_u64_u32 with an arbitrary VGPR as
+    // the unused high addend, which made the refill wait for the window's pending load)
+    auto itemIndex = [&](uint32_t k) { return (waveId + __umul24(k / kInterleave, waves)) * kInterleave + k % kInterleave; };
+    // Prefetch window: lane L holds `ahead` = lookup() of the wave's item k = L (mod 64)
+    // in [cursor, cursor + 64), loaded one refill or more before a lane takes it, so a
+    // refill waits for the ray loads only, not for the queue read in front of them.
+    uint32_t ahead = 0;
+    if (lane < end && itemIndex(lane) < n) ahead = lookup(itemIndex(lane));
     TravState s;
     bool active = false;
+    bool pending = false;   // this lane's ray is finished and its result not yet written
     uint32_t item = 0;
 #ifdef DCRT_WAVE_TIMELINE
     const unsigned long long tStart = wall_clock64();
 #endif
     for (;;) {
-        // refill only when at least kRefillLanes lanes are idle: the fetch (queue
-        // read, ray loads, three IEEE divisions) is then shared by many lanes
+        // refill only when at least kRefillLanes lanes are idle: the fetch (ray loads,
+        // three IEEE divisions) is then shared by many lanes
         const unsigned long long need = __ballot(!active);
-        if ((uint32_t)__popcll(need) >= kRefillLanes && cursor < end) {
-            const uint32_t k = cursor + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-            const uint32_t idx = (waveId + (k / kInterleave) * waves) * kInterleave + k % kInterleave;
+        const uint32_t nNeed = (uint32_t)__popcll(need);
+        const bool refill = nNeed >= kRefillLanes && cursor < end;
+        const uint32_t k = cursor + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        uint32_t path = 0;
+        if (refill) path = (uint32_t)__shfl((int)ahead, (int)(k & 63u), 64);   // every lane: a full-wave bpermute
+        // Finished rays are written here, after the window read and just before the ray
+        // loads: stores count in vmcnt too, so written earlier they would make the window
+        // read wait for their acknowledgement, and the ray loads then wait once more.
+        if (pending) {
+            emit(item, s);
+            pending = false;
+        }
+        if (refill) {
+            const uint32_t idx = itemIndex(k);
             if (!active && k < end && idx < n) {
-                item = fetch(idx, s);
+                item = fetch(idx, path, s);
                 active = true;
             }
-            cursor = min(cursor + (uint32_t)__popcll(need), end);
+            const uint32_t used = min(nNeed, end - cursor);
+            // this lane's window item cursor + ((L - cursor) mod 64) was taken: look up the one 64 later
+            const uint32_t off = (lane - cursor) & 63u;
+            const uint32_t k2 = cursor + off + 64u;
+            if (off < used && k2 < end && itemIndex(k2) < n) ahead = lookup(itemIndex(k2));
+            cursor += used;
         }
         if (__ballot(active) == 0ull) break;
         // phase A: node visits only, until enough lanes are parked at leaves (or
@@ -397,7 +427,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         for (;;) {
 #pragma unroll
             for (int k = 0; k < kVisitsPerCheck; ++k) {
-                if (active && !done && !s.parked && trav_visit<INSTR>(sc, s, f2b, lds, shift, st)) done = true;
+                if (active && !done && !s.parked && trav_visit<INSTR, ALL_CACHED>(sc, s, f2b, lds, shift, st)) done = true;
             }
             const unsigned long long runnable = __ballot(active && !done && !s.parked);
             const uint32_t parked = (uint32_t)__popcll(__ballot(active && !done && s.parked));
@@ -405,12 +435,12 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             if (runnable == 0ull || parked >= kParkLanes || (idle >= kRefillLanes && cursor < end)) break;
         }
         if (done) {
-            emit(item, s);
+            pending = true;
             active = false;
         }
         // phase B: the parked lanes' leaf work, shared by many lanes at once
-        if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY>(sc, s, watertight, lds, shift, st)) {
-            emit(item, s);
+        if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED>(sc, s, watertight, lds, shift, st)) {
+            pending = true;
             active = false;
         }
     }
@@ -420,6 +450,23 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         g_waveLog[ANY_HIT ? 1 : 0][waveTag & 15][waveId][1] = wall_clock64();
         g_waveItems[ANY_HIT ? 1 : 0][waveTag & 15][waveId] = chunk;
     }
+#endif
+}
+
+// Kernel arguments the cast kernels select between per lane (extension vs shadow ray):
+// pinned in SGPRs, so the select is a v_cndmask of two values and not a per-lane load
+// of the pointer from the kernel-argument segment in front of every ray fetch.
+// (The asm takes the pointer in the global address space and the result is cast back,
+// so the loads through it stay global_load, not FLAT; the host pass only parses it.)
+template <typename T>
+__device__ __forceinline__ T* sgpr_ptr(T* p)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    __attribute__((address_space(1))) T* g = (__attribute__((address_space(1))) T*)p;
+    asm volatile("" : "+s"(g));
+    return (T*)g;
+#else
+    return p;
 #endif
 }
 
@@ -442,8 +489,8 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<false, INSTR, OPACITY>(
         sc, qm.prefix[kShards], fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
-        [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
-            const uint32_t path = qentry(pool.extQueue, pool.size, qm, i);
+        [&](uint32_t i) __attribute__((always_inline)) { return qentry(pool.extQueue, pool.size, qm, i); },
+        [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
             const float4 o = pool.rayO[path], d = pool.rayD[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf());
             if (OPACITY) s.opacitySample = pool.extOpacity[path];
@@ -487,16 +534,17 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<true, INSTR, OPACITY>(
         sc, n, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
-        [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
-            const uint32_t path = qentry(pool.shadowQueue, pool.size, qm, i);
+        [&](uint32_t i) __attribute__((always_inline)) { return qentry(pool.shadowQueue, pool.size, qm, i); },
+        [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
             const float4 o = pool.shadowO[path], d = pool.shadowD[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, o.w);
+            s.pathFlags = asu(d.w);
             if (OPACITY) s.opacitySample = pool.shadowOpacity[path];
             return path;
         },
         [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
-            const uint32_t f = pool.flags[path];
-            pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (f & 0xBFFFFFFFu);
+            // the path's flags as MATERIAL wrote them (carried in shadowD.w): a plain store
+            pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (s.pathFlags & ~kFlagShadowRayHit);
         },
         st, DCRT_WAVE_TAG(g));
     if (INSTR) flush_stats(st, instr + 3);
@@ -509,7 +557,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
 // iteration instead of two, and a shadow ray can fill a lane an extension ray left
 // idle. Per lane the ray keeps its own semantics (closest hit vs first hit), so the
 // results are those of the two separate kernels.
-template <bool INSTR, bool OPACITY>
+template <bool INSTR, bool OPACITY, bool ALL_CACHED>
 __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void cast_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
                                                                      Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
@@ -519,25 +567,35 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void cast_kernel(PathPool 
     qmap(cnt, kQExt, &qe);
     qmap(cnt, kQShadow, &qs);
     const uint32_t nExt = qe.prefix[kShards], nShadow = qs.prefix[kShards];
+    const uint32_t* extQueue = sgpr_ptr(pool.extQueue);
+    const uint32_t* shQueue = sgpr_ptr(pool.shadowQueue);
+    const float4* rayO = sgpr_ptr(pool.rayO);
+    const float4* rayD = sgpr_ptr(pool.rayD);
+    const float4* shO = sgpr_ptr(pool.shadowO);
+    const float4* shD = sgpr_ptr(pool.shadowD);
     TraversalStats st = {0u, 0u, 0u};
     TraversalStats stExt = {0u, 0u, 0u}, stShadow = {0u, 0u, 0u};
-    persistent_trace<false, INSTR, OPACITY, true>(
+    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
-        [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
+        [&](uint32_t i) __attribute__((always_inline)) {
             const bool shadow = i >= nExt;
-            const uint32_t path = shadow ? qentry(pool.shadowQueue, pool.size, qs, i - nExt) : qentry(pool.extQueue, pool.size, qe, i);
-            const float4 o = shadow ? pool.shadowO[path] : pool.rayO[path];
-            const float4 d = shadow ? pool.shadowD[path] : pool.rayD[path];
+            return qentry(shadow ? shQueue : extQueue, pool.size, shadow ? qs : qe, shadow ? i - nExt : i);
+        },
+        [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
+            const bool shadow = i >= nExt;
+            const float4 o = (shadow ? shO : rayO)[path];
+            const float4 d = (shadow ? shD : rayD)[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, shadow ? o.w : inf());
             s.anyHit = shadow;
+            s.pathFlags = asu(d.w);
             if (OPACITY) s.opacitySample = shadow ? pool.shadowOpacity[path] : pool.extOpacity[path];
             if (INSTR) { st.nodes = 0u; st.tris = 0u; st.blas = 0u; }
             return path;
         },
         [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
             if (s.anyHit) {
-                const uint32_t f = pool.flags[path];
-                pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (f & 0xBFFFFFFFu);
+                // the path's flags as MATERIAL wrote them (carried in shadowD.w): a plain store
+                pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (s.pathFlags & ~kFlagShadowRayHit);
             } else {
                 pool.hit[path] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
                 pool.hitInst[path] = s.found ? s.hit.inst : 0u;
@@ -715,7 +773,8 @@ __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const 
     TraversalStats st = {0u, 0u, 0u};
     persistent_trace<ANY, true, false>(
         sc, n, features, 16u, 32u, stackMem + threadIdx.x, block_shift(),
-        [&](uint32_t i, TravState& s) __attribute__((always_inline)) {
+        [&](uint32_t i) __attribute__((always_inline)) { return i; },
+        [&](uint32_t i, uint32_t, TravState& s) __attribute__((always_inline)) {
             const dcrt_ray r = rays[i];
             trav_init(s, ld3(r.origin), ld3(r.direction), 0.0f, ANY ? r.t_max : inf());
             return i;
@@ -1117,10 +1176,14 @@ template __global__ void shadow_kernel<false, false>(PathPool, DeviceScene, cons
 template __global__ void shadow_kernel<false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void shadow_kernel<true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void shadow_kernel<true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void megakernel<false>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void megakernel<true>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void batch_trace_kernel<false>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);

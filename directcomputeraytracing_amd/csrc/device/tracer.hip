@@ -110,6 +110,17 @@ uint32_t FilterSupportRows(float r, uint32_t H)
     return rows;
 }
 
+using CastFn = void (*)(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+// cast_kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER x whole scene in the LDS cache
+CastFn CastKernel(bool instr, bool opacity, bool allCached)
+{
+    static const CastFn table[8] = {
+        cast_kernel<false, false, false>, cast_kernel<false, false, true>, cast_kernel<false, true, false>,
+        cast_kernel<false, true, true>, cast_kernel<true, false, false>, cast_kernel<true, false, true>,
+        cast_kernel<true, true, false>, cast_kernel<true, true, true>};
+    return table[(instr ? 4 : 0) + (opacity ? 2 : 0) + (allCached ? 1 : 0)];
+}
+
 }  // namespace
 
 struct dcrt_tracer {
@@ -128,6 +139,7 @@ struct dcrt_tracer {
     bool hasScene = false;
     uint32_t castBlock = 256;
     size_t castLds = 0;
+    bool castAllCached = false;        // the scene fits the LDS cache: cast_kernel<., ., true>
     bool mergedCasts = true;           // one cast_kernel per iteration (DCRT_SPLIT_CASTS=1: EXT then SHADOW)
     uint32_t sceneCaps = kCapAll;      // what the uploaded scene uses (kCap* of dscene.h)
     uint32_t materialCaps = kCapAll;   // the MATERIAL variant launched for it
@@ -471,7 +483,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         // LDS scene cache in what the cast kernel's register-limited occupancy leaves of the
         // CU's 160 KiB per workgroup: BVH nodes first, then pre-gathered triangles
         int regPerCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false>, (int)castBlock, castLds));
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false, false>, (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, extension_kernel<false, false>, (int)castBlock, castLds));
         const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
         const size_t budget = castLds < perBlock ? perBlock - castLds : 0;
@@ -480,7 +492,10 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {   // A/B experiments
             if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
         }
-        castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * 48;
+        castAllCached = d.cachedNodes == s.bvh_node_count && d.cachedTris == s.triangle_count &&
+                        budget - (size_t)d.cachedNodes * 32 - (size_t)d.cachedTris * 48 >= (size_t)s.instance_count * 64;
+        d.cachedInstances = castAllCached ? s.instance_count : 0u;
+        castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * 48 + (size_t)d.cachedInstances * 64;
         scene = d;
     }
     {
@@ -488,7 +503,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         hipDeviceProp_t prop;
         HIPCHECK(hipGetDeviceProperties(&prop, device));
         int perCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, cast_kernel<false, false>, (int)castBlock, castLds));
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, CastKernel(false, false, castAllCached), (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false, false>, (int)castBlock, castLds));
         if (const char* b = std::getenv("DCRT_CAST_BLOCKS_PER_CU")) {   // tuning experiments
             const int v = std::atoi(b);
@@ -496,7 +511,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         }
         castResident = (uint32_t)std::max(1, perCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int opacityPerCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, cast_kernel<false, true>, (int)castBlock, castLds));
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, CastKernel(false, true, castAllCached), (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLds));
         castResidentOpacity = (uint32_t)std::max(1, std::min(opacityPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int megaPerCU = 0;
@@ -715,8 +730,7 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     // (hipExtLaunchKernelGGL), so the duration is the kernel's, as rocprofv3 reports it.
     // kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER
     if (mergedCasts) {
-        auto cast = instrCounters ? (opacity ? cast_kernel<true, true> : cast_kernel<true, false>)
-                                  : (opacity ? cast_kernel<false, true> : cast_kernel<false, false>);
+        auto cast = CastKernel(instrCounters, opacity, castAllCached);
         hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), castLds, stream, e0, e1, 0, pool, scene,
                               (const FrameConstants*)dFrame, cnt, next, dGlobals, dInstr);
     } else {
