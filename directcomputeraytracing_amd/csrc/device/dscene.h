@@ -122,7 +122,7 @@ DEV bool ray_aabb(V3 o, V3 inv, float tMin, float tMax, float4 a, float4 b)
     const float tz1 = (b.y - o.z) * inv.z;
     t0 = fmaxf(t0, fminf(tz0, tz1));
     t1 = fminf(t1, fmaxf(tz0, tz1));
-    return t1 >= t0 && (t0 < tMax && t1 >= tMin);
+    return (t1 >= t0) & (t0 < tMax) & (t1 >= tMin);   // (bitwise: no exec-mask branch per node)
 }
 
 struct Shear {
@@ -225,6 +225,9 @@ struct TravState {
     bool inBlas, shearValid, found, parked, noZero;   // noZero: no component of o, d is +-0
     bool anyHit;          // merged cast kernel: this lane's ray is a shadow ray (first hit ends it)
     uint32_t pathFlags;   // shadow ray: the path's flags as MATERIAL wrote them (shadowD.w)
+    // Near/far choice of the current space: bit a = (ld[a] < 0) for the axes a = 0..2,
+    // bit 3 = front-to-back order on (0: the whole mask is 0, near child = node + 1 always)
+    uint32_t negMask;
     Shear sh;
     HitRecord hit;
     // ALLOW_ANYHIT_SHADER only (dead, and removed by the compiler, otherwise)
@@ -233,8 +236,17 @@ struct TravState {
     bool opaque;              // the current instance's INSTANCE_FLAG_OPAQUE
 };
 
-DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax)
+// BVHAccel.inc.hlsl's near/far test `dir[axis] < 0` for all three axes at once, kept per
+// space (world, instance) so a node visit selects one bit instead of comparing three signs
+DEV uint32_t neg_mask(V3 d, uint32_t current)
 {
+    return (current & 8u) ? 8u | (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u) : 0u;
+}
+
+// f2b = false (DCRT_FEATURE_NO_FRONT_TO_BACK): near child is always node + 1
+DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax, bool f2b = true)
+{
+    s.negMask = neg_mask(d, f2b ? 8u : 0u);
     s.o = o; s.d = d; s.invW = inv_dir(d);
     s.lo = o; s.ld = d; s.inv = inv_dir(d);
     s.tMin = tMin; s.tMax = tMax;
@@ -288,6 +300,7 @@ DEV bool trav_pop(const DeviceScene& sc, TravState& s, const uint32_t* lds, uint
         s.lo = mk(s.o.x, s.o.y, s.o.z);
         s.ld = mk(s.d.x, s.d.y, s.d.z);
         s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+        s.negMask = neg_mask(s.d, s.negMask);
         s.shearValid = false;
     }
     return false;
@@ -302,13 +315,14 @@ DEV bool trav_pop(const DeviceScene& sc, TravState& s, const uint32_t* lds, uint
 // ALL_CACHED: the whole BVH and every triangle sit in the LDS scene cache (small scenes),
 // so node and triangle fetches are plain ds_read_b128 (no FLAT select, no global path).
 template <bool INSTR, bool ALL_CACHED = false>
-DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds, uint32_t shift, TraversalStats& st)
+DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
     // the stack top (read only by a pop) is issued together with the node fetch: this
     // visit's push writes slot `count`, never the slot read here, so the two LDS round
     // trips of a visit overlap instead of following each other
-    const uint32_t top = lds[(s.count > 0u ? min(s.count - 1u, sc.stackSize) : sc.stackSize) << shift];
+    // (count - 1 wraps to 0xFFFFFFFF at an empty stack: the spare slot, read but unused)
+    const uint32_t top = lds[min(s.count - 1u, sc.stackSize) << shift];
     float4 a, b;
     if (ALL_CACHED) {
         const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
@@ -327,12 +341,8 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds
     const uint32_t right = asu(b.z);
     const bool leaf = (misc & 0x4u) != 0u || ((misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT) != 0u;
     const bool descend = hit && !leaf;
-    // near/far by the split axis' direction sign. All three signs, combined with bit
-    // ops: a select over the components would become a variable-offset access that
-    // pins the state in scratch.
-    const uint32_t axis = misc & 0x3u;
-    const bool nx = s.ld.x < 0.0f, ny = s.ld.y < 0.0f, nz = s.ld.z < 0.0f;
-    const bool neg = f2b && ((axis == 0u && nx) | (axis == 1u && ny) | (axis == 2u && nz));
+    // near/far by the split axis' direction sign (one bit of the space's sign mask)
+    const bool neg = ((s.negMask >> (misc & 0x3u)) & 1u) != 0u;
     const uint32_t nearChild = neg ? right : s.node + 1;
     const uint32_t farChild = neg ? s.node + 1 : right;
     lds[min(s.count, sc.stackSize) << shift] = (farChild & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
@@ -349,6 +359,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, bool f2b, uint32_t* lds
         s.lo = mk(s.o.x, s.o.y, s.o.z);
         s.ld = mk(s.d.x, s.d.y, s.d.z);
         s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+        s.negMask = neg_mask(s.d, s.negMask);
         s.shearValid = false;
     }
     s.parked = hit && leaf;
@@ -385,6 +396,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
             s.ld = mul43(s.d, 0.0f, M);
             s.inv = inv_dir(s.ld);
         }
+        s.negMask = neg_mask(s.ld, s.negMask);
         s.shearValid = false;
         s.inBlas = true;
         s.inst = primOrInst;

@@ -409,6 +409,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             const uint32_t idx = itemIndex(k);
             if (!active && k < end && idx < n) {
                 item = fetch(idx, path, s);
+                if (!f2b) s.negMask = 0u;
                 active = true;
             }
             const uint32_t used = min(nNeed, end - cursor);
@@ -427,7 +428,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         for (;;) {
 #pragma unroll
             for (int k = 0; k < kVisitsPerCheck; ++k) {
-                if (active && !done && !s.parked && trav_visit<INSTR, ALL_CACHED>(sc, s, f2b, lds, shift, st)) done = true;
+                if (active && !done && !s.parked && trav_visit<INSTR, ALL_CACHED>(sc, s, lds, shift, st)) done = true;
             }
             const unsigned long long runnable = __ballot(active && !done && !s.parked);
             const uint32_t parked = (uint32_t)__popcll(__ballot(active && !done && s.parked));
@@ -620,11 +621,11 @@ __device__ __forceinline__ bool trace_full(const DeviceScene& sc, V3 o, V3 d, fl
                                            float opacitySample, uint32_t* lds, uint32_t shift, HitRecord* hit)
 {
     TravState s;
-    trav_init(s, o, d, 0.0f, tMax);
+    trav_init(s, o, d, 0.0f, tMax, f2b);
     s.opacitySample = opacitySample;
     TraversalStats st = {0u, 0u, 0u};
     for (;;) {
-        if (trav_visit<false>(sc, s, f2b, lds, shift, st)) break;
+        if (trav_visit<false>(sc, s, lds, shift, st)) break;
         if (s.parked && trav_leaf<ANY_HIT, false, OPACITY>(sc, s, watertight, lds, shift, st)) break;
     }
     *hit = s.hit;
