@@ -82,14 +82,14 @@ struct DeviceScene {
     uint32_t cachedInstances;     // 0, or instanceCount: every inverse transform + identity flag, after the triangles
 };
 
-// LDS scene cache of the traversal kernels: after the per-lane stacks ([stackSize + 1]
-// x blockDim words) the block holds a copy of the first cachedNodes BVH nodes and the
+// LDS scene cache of the traversal kernels: after the per-lane stacks ([stackSize + 2]
+// x blockDim words, see stack_at) the block holds a copy of the first cachedNodes BVH nodes and the
 // first cachedTris pre-gathered triangles (the whole BVH and mesh of a small scene, the
 // TLAS and the first BLAS nodes of a large one), so most node and triangle fetches are
 // ds_read_b128 instead of vector-memory gathers through the texture path.
 DEV float4* scene_cache(const DeviceScene& sc, uint32_t* stackMem, uint32_t shift)
 {
-    return (float4*)(stackMem + ((sc.stackSize + 1u) << shift));
+    return (float4*)(stackMem + ((sc.stackSize + 2u) << shift));
 }
 // Every thread of the block: fill the cache, then a barrier.
 DEV void scene_cache_load(const DeviceScene& sc, uint32_t* stackMem, uint32_t shift)
@@ -220,9 +220,11 @@ struct TravState {
     V3 o, d, invW;        // world ray and 1/d (restored on BLAS -> TLAS without dividing again)
     V3 lo, ld, inv;       // ray in the current space (world or instance)
     float tMin, tMax;
-    uint32_t node, count, inst;
-    uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked)
-    bool inBlas, shearValid, found, parked, noZero;   // noZero: no component of o, d is +-0
+    uint32_t node;        // node index | 0x80000000 in a BLAS (the stack entries' packing)
+    uint32_t sp;          // stack entries x stride (bytes): see stack_at
+    uint32_t inst;
+    uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked; not kept with ALL_CACHED)
+    bool shearValid, found, parked, noZero;   // noZero: no component of o, d is +-0
     bool anyHit;          // merged cast kernel: this lane's ray is a shadow ray (first hit ends it)
     uint32_t pathFlags;   // shadow ray: the path's flags as MATERIAL wrote them (shadowD.w)
     // Near/far choice of the current space: bit a = (ld[a] < 0) for the axes a = 0..2,
@@ -250,9 +252,9 @@ DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax, bool f2b = 
     s.o = o; s.d = d; s.invW = inv_dir(d);
     s.lo = o; s.ld = d; s.inv = inv_dir(d);
     s.tMin = tMin; s.tMax = tMax;
-    s.node = 0; s.count = 0; s.inst = 0;
+    s.node = 0; s.sp = 0; s.inst = 0;
     s.leafRef = 0; s.leafMisc = 0;
-    s.inBlas = false; s.shearValid = false; s.found = false; s.parked = false; s.anyHit = false;
+    s.shearValid = false; s.found = false; s.parked = false; s.anyHit = false;
     s.noZero = o.x != 0.0f && o.y != 0.0f && o.z != 0.0f && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
     s.hit.t = 0.0f; s.hit.u = 0.0f; s.hit.v = 0.0f; s.hit.tri = 0u; s.hit.inst = 0u;
     s.opacitySample = 0.0f; s.matOverride = DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE; s.opaque = false;
@@ -285,16 +287,26 @@ DEV bool any_hit_shader(const DeviceScene& sc, uint32_t tri, uint32_t ov, float 
     return opacitySample < opacity;
 }
 
+// Per-lane traversal stack in LDS: row r of a lane's column sits at byte offset
+// r * stride (stride = 4 * blockDim: consecutive lanes on consecutive banks). With
+// `count` entries (sp = count * stride) the top entry is row count and a push goes to
+// row count + 1; row 0 (read as the top of an empty stack) and row stackSize + 1 (the
+// branch-free push of a full stack) are spares whose contents nothing uses.
+DEV uint32_t& stack_at(uint32_t* lds, uint32_t byteOffset) { return *(uint32_t*)((char*)lds + byteOffset); }
+// ALL_CACHED kernels run 256-thread workgroups (tracer.hip): a compile-time stride
+// becomes the ds_write's immediate offset
+template <bool ALL_CACHED>
+DEV uint32_t stack_stride(uint32_t shift) { return ALL_CACHED ? 1024u : 4u << shift; }
+
 // Pop the next node (BVHAccel.inc.hlsl stack pop); true when the stack is empty.
-DEV bool trav_pop(const DeviceScene& sc, TravState& s, const uint32_t* lds, uint32_t shift)
+DEV bool trav_pop(TravState& s, uint32_t* lds, uint32_t stride)
 {
-    if (s.count == 0) return true;
-    --s.count;
-    const uint32_t packed = s.count < sc.stackSize ? lds[s.count << shift] : 0u;
-    const bool wasBlas = s.inBlas;
-    s.node = packed & 0x7FFFFFFFu;
-    s.inBlas = (packed & 0x80000000u) != 0;
-    if (wasBlas != s.inBlas) {
+    if (s.sp == 0u) return true;
+    const uint32_t packed = stack_at(lds, s.sp);
+    s.sp -= stride;
+    const bool restore = (int)s.node < 0 && (int)packed >= 0;   // BLAS -> TLAS
+    s.node = packed;
+    if (restore) {
         // component-wise: a struct copy inside the state becomes an alloca-local
         // memcpy that keeps SROA from promoting the state to registers
         s.lo = mk(s.o.x, s.o.y, s.o.z);
@@ -318,41 +330,44 @@ template <bool INSTR, bool ALL_CACHED = false>
 DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
+    const uint32_t stride = stack_stride<ALL_CACHED>(shift);
     // the stack top (read only by a pop) is issued together with the node fetch: this
-    // visit's push writes slot `count`, never the slot read here, so the two LDS round
-    // trips of a visit overlap instead of following each other
-    // (count - 1 wraps to 0xFFFFFFFF at an empty stack: the spare slot, read but unused)
-    const uint32_t top = lds[min(s.count - 1u, sc.stackSize) << shift];
+    // visit's push writes the row above it, so the two LDS round trips of a visit overlap
+    const uint32_t top = stack_at(lds, s.sp);
+    const uint32_t idx = s.node & 0x7FFFFFFFu;
     float4 a, b;
     if (ALL_CACHED) {
         const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
-        a = c[s.node * 2];
-        b = c[s.node * 2 + 1];
-    } else if (s.node < sc.cachedNodes) {
+        a = c[idx * 2];
+        b = c[idx * 2 + 1];
+    } else if (idx < sc.cachedNodes) {
         const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
-        a = c[s.node * 2];
-        b = c[s.node * 2 + 1];
+        a = c[idx * 2];
+        b = c[idx * 2 + 1];
     } else {
-        a = sc.nodes[s.node * 2];
-        b = sc.nodes[s.node * 2 + 1];
+        a = sc.nodes[idx * 2];
+        b = sc.nodes[idx * 2 + 1];
     }
     const bool hit = ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a, b);
     const uint32_t misc = asu(b.w);
     const uint32_t right = asu(b.z);
-    const bool leaf = (misc & 0x4u) != 0u || ((misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT) != 0u;
+    // leaf: TLAS-leaf bit (4) or a primitive count (bits 3 and up)
+    const bool leaf = misc > 3u;
     const bool descend = hit && !leaf;
-    // near/far by the split axis' direction sign (one bit of the space's sign mask)
+    // near/far by the split axis' direction sign (one bit of the space's sign mask);
+    // children keep the BLAS bit of the packed node reference
     const bool neg = ((s.negMask >> (misc & 0x3u)) & 1u) != 0u;
-    const uint32_t nearChild = neg ? right : s.node + 1;
-    const uint32_t farChild = neg ? s.node + 1 : right;
-    lds[min(s.count, sc.stackSize) << shift] = (farChild & 0x7FFFFFFFu) | (s.inBlas ? 0x80000000u : 0u);
-    const bool pop = !hit && s.count > 0u;
-    const bool done = !hit && s.count == 0u;
-    const bool popBlas = (top & 0x80000000u) != 0u;
-    const bool restore = pop && s.inBlas && !popBlas;    // BLAS -> TLAS: back to the world ray
-    s.node = descend ? nearChild : (pop ? (top & 0x7FFFFFFFu) : s.node);
-    s.count = descend ? s.count + 1u : (pop ? s.count - 1u : s.count);
-    s.inBlas = pop ? popBlas : s.inBlas;
+    const uint32_t next = s.node + 1u;
+    const uint32_t rightRef = right | (s.node & 0x80000000u);
+    const uint32_t nearChild = neg ? rightRef : next;
+    const uint32_t farChild = neg ? next : rightRef;
+    stack_at(lds, s.sp + stride) = farChild;
+    const bool empty = s.sp == 0u;
+    const bool pop = !hit && !empty;
+    const bool done = !hit && empty;
+    const bool restore = pop && (int)s.node < 0 && (int)top >= 0;    // BLAS -> TLAS: back to the world ray
+    s.node = descend ? nearChild : (pop ? top : s.node);
+    s.sp = descend ? s.sp + stride : (pop ? s.sp - stride : s.sp);
     // rare (about once per ray): a branch the wave skips when no lane restores; as
     // selects it cost nine v_cndmask per visit (measured 2.5 % of the cast kernel)
     if (__builtin_expect(restore, 0)) {
@@ -363,8 +378,10 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         s.shearValid = false;
     }
     s.parked = hit && leaf;
-    s.leafRef = right;
-    s.leafMisc = misc;
+    if (!ALL_CACHED) {   // (ALL_CACHED: phase B reads them from the LDS copy of the node)
+        s.leafRef = right;
+        s.leafMisc = misc;
+    }
     return done;
 }
 
@@ -375,8 +392,14 @@ template <bool ANY_HIT, bool INSTR, bool OPACITY = false, bool LANE_ANY = false,
 DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     s.parked = false;
-    const uint32_t primOrInst = (s.leafMisc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
-    if (s.leafMisc & 0x4u) {
+    uint32_t leafRef = s.leafRef, leafMisc = s.leafMisc;
+    if (ALL_CACHED) {   // the parked leaf is s.node (a leaf visit neither descends nor pops)
+        const float4 b = scene_cache(sc, lds - threadIdx.x, shift)[(s.node & 0x7FFFFFFFu) * 2 + 1];
+        leafRef = asu(b.z);
+        leafMisc = asu(b.w);
+    }
+    const uint32_t primOrInst = (leafMisc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
+    if (leafMisc & 0x4u) {
         const float4* M;
         uint32_t identity;
         if (ALL_CACHED) {
@@ -398,9 +421,8 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         }
         s.negMask = neg_mask(s.ld, s.negMask);
         s.shearValid = false;
-        s.inBlas = true;
         s.inst = primOrInst;
-        s.node = s.leafRef;
+        s.node = leafRef | 0x80000000u;   // the BLAS root
         if (OPACITY) {   // BVHAccel.inc.hlsl:136-139
             s.opaque = (sc.instanceFlags[primOrInst] & DCRT_INSTANCE_FLAG_OPAQUE) != 0u;
             s.matOverride = sc.overrides[primOrInst];
@@ -409,7 +431,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         return false;
     }
     if (watertight && !s.shearValid) { s.sh = make_shear(s.ld); s.shearValid = true; }
-    const uint32_t begin = s.leafRef;
+    const uint32_t begin = leafRef;
     const uint32_t end = begin + primOrInst;
     for (uint32_t p = begin; p < end; ++p) {
         if (INSTR) ++st.tris;
@@ -436,7 +458,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
             s.hit.inst = s.inst;
         }
     }
-    return trav_pop(sc, s, lds, shift);
+    return trav_pop(s, lds, stack_stride<ALL_CACHED>(shift));
 }
 
 // ---- texture emulation ----------------------------------------------------------

@@ -352,6 +352,23 @@ __device__ uint32_t g_waveItems[2][16][8192];
 #define DCRT_WAVE_TAG(g) (-1)
 #endif
 
+#ifdef DCRT_PHASE_CLOCKS
+// Diagnostic build only (tools/phase_clocks.py): shader-clock cycles the cast kernels'
+// waves spend per phase of the persistent loop, summed over all waves:
+// [0] hand-over + result stores + ray set-up, [1] phase A (node visits), [2] phase B
+// (leaf work), [3] loop trips, [4] phase-A checks, [5] phase-B entries.
+__device__ unsigned long long g_phaseClk[8];
+#define DCRT_PHASE_INIT unsigned long long clk_[6] = {0, 0, 0, 0, 0, 0}; unsigned long long tP_ = __builtin_amdgcn_s_memtime()
+#define DCRT_PHASE(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); clk_[i] += t_ - tP_; tP_ = t_; } while (0)
+#define DCRT_PHASE_COUNT(i) (++clk_[i])
+#define DCRT_PHASE_FLUSH() do { if ((threadIdx.x & 63u) == 0) for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phaseClk[i_], clk_[i_]); } while (0)
+#else
+#define DCRT_PHASE_INIT do {} while (0)
+#define DCRT_PHASE(i) do {} while (0)
+#define DCRT_PHASE_COUNT(i) do {} while (0)
+#define DCRT_PHASE_FLUSH() do {} while (0)
+#endif
+
 template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, typename Lookup, typename Fetch,
           typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
@@ -389,7 +406,9 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
 #ifdef DCRT_WAVE_TIMELINE
     const unsigned long long tStart = wall_clock64();
 #endif
+    DCRT_PHASE_INIT;
     for (;;) {
+        DCRT_PHASE_COUNT(3);
         // refill only when at least kRefillLanes lanes are idle: the fetch (ray loads,
         // three IEEE divisions) is then shared by many lanes
         const unsigned long long need = __ballot(!active);
@@ -419,6 +438,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             if (off < used && k2 < end && itemIndex(k2) < n) ahead = lookup(itemIndex(k2));
             cursor += used;
         }
+        DCRT_PHASE(0);
         if (__ballot(active) == 0ull) break;
         // phase A: node visits only, until enough lanes are parked at leaves (or
         // enough are idle to refill, or none can advance)
@@ -433,18 +453,23 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             const unsigned long long runnable = __ballot(active && !done && !s.parked);
             const uint32_t parked = (uint32_t)__popcll(__ballot(active && !done && s.parked));
             const uint32_t idle = (uint32_t)__popcll(__ballot(!active || done));
+            DCRT_PHASE_COUNT(4);
             if (runnable == 0ull || parked >= kParkLanes || (idle >= kRefillLanes && cursor < end)) break;
         }
+        DCRT_PHASE(1);
         if (done) {
             pending = true;
             active = false;
         }
         // phase B: the parked lanes' leaf work, shared by many lanes at once
+        if (__ballot(active && s.parked) != 0ull) DCRT_PHASE_COUNT(5);
         if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED>(sc, s, watertight, lds, shift, st)) {
             pending = true;
             active = false;
         }
+        DCRT_PHASE(2);
     }
+    DCRT_PHASE_FLUSH();
 #ifdef DCRT_WAVE_TIMELINE
     if (waveTag >= 0 && n > 0 && (threadIdx.x & 63u) == 0 && waveId < 8192) {
         g_waveLog[ANY_HIT ? 1 : 0][waveTag & 15][waveId][0] = tStart;

@@ -473,11 +473,11 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     if (const char* g = std::getenv("DCRT_MATERIAL_GENERIC")) {   // A/B: always the generic variant
         if (std::atoi(g)) materialCaps = kCapAll;
     }
-    // LDS stack: [stackSize][block] u32; keep a workgroup's stack <= 32 KiB
-    // (+1: a spare slot per lane that the branch-free push may write, never read)
+    // LDS stack: [stackSize + 2][block] u32 (two spare rows per lane, see stack_at in
+    // dscene.h); keep a workgroup's stack <= 32 KiB
     castBlock = 256;
-    while (castBlock > 64 && (size_t)(d.stackSize + 1) * castBlock * 4 > 32768) castBlock >>= 1;
-    castLds = (size_t)(d.stackSize + 1) * castBlock * 4;
+    while (castBlock > 64 && (size_t)(d.stackSize + 2) * castBlock * 4 > 32768) castBlock >>= 1;
+    castLds = (size_t)(d.stackSize + 2) * castBlock * 4;
     if (castLds > 65536) { SetLastError("BVH traversal stack too deep for LDS"); return DCRT_E_LIMIT; }
     {
         // LDS scene cache in what the cast kernel's register-limited occupancy leaves of the
@@ -492,7 +492,8 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {   // A/B experiments
             if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
         }
-        castAllCached = d.cachedNodes == s.bvh_node_count && d.cachedTris == s.triangle_count &&
+        // (the LDS-only variant assumes 256-thread workgroups: its stack stride is a constant)
+        castAllCached = castBlock == 256 && d.cachedNodes == s.bvh_node_count && d.cachedTris == s.triangle_count &&
                         budget - (size_t)d.cachedNodes * 32 - (size_t)d.cachedTris * 48 >= (size_t)s.instance_count * 64;
         d.cachedInstances = castAllCached ? s.instance_count : 0u;
         castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * 48 + (size_t)d.cachedInstances * 64;
@@ -1370,6 +1371,19 @@ extern "C" DCRT_API int dcrt_debug_wave_timeline(dcrt_tracer* t, unsigned long l
     HIPCHECK(hipStreamSynchronize(t->stream));
     HIPCHECK(hipMemcpyFromSymbol(stamps, HIP_SYMBOL(g_waveLog), sizeof(g_waveLog)));
     HIPCHECK(hipMemcpyFromSymbol(items, HIP_SYMBOL(g_waveItems), sizeof(g_waveItems)));
+    return DCRT_OK;
+}
+#endif
+
+#ifdef DCRT_PHASE_CLOCKS
+// Diagnostic build only: read and clear the cast kernels' per-phase wave cycles.
+extern "C" DCRT_API int dcrt_debug_phase_clocks(dcrt_tracer* t, unsigned long long* out)
+{
+    TRACER_GUARD(t);
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    HIPCHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phaseClk), sizeof(g_phaseClk)));
+    const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phaseClk), zero, sizeof(zero)));
     return DCRT_OK;
 }
 #endif

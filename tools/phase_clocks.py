@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Diagnostic: where the cast kernel's waves spend their time (1080p Cornell, 8 images).
+
+Needs a library built with -DDCRT_PHASE_CLOCKS (DCRT_LIB=gpu_ab/phase.so). Prints the
+shader-clock cycles summed over all waves per phase of the persistent loop (hand-over +
+stores + ray set-up / phase A node visits / phase B leaf work) and the loop counts.
+"""
+import ctypes as C
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
+    scene = Scene((1920, 1080))
+    scenes.setup_cornell(scene, 1920, 1080, 8)
+    tr = WavefrontPathTracer(path_pool_size=1 << 24, iterations_per_render=16)
+    tr.on_scene_loaded(scene)
+    filt = scene.filter_params()
+    tr.clear_film()
+    tr.render_images(100, 2, filt)
+    fn = tr._lib.dcrt_debug_phase_clocks
+    fn.restype = C.c_int
+    out = np.zeros(8, np.uint64)
+    assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
+    tr.reset_stats()
+    tr.render_images(0, 8, filt)
+    assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
+    c = tr.counters()
+    tot = float(out[0] + out[1] + out[2])
+    for i, name in enumerate(("hand-over + stores + set-up", "phase A (node visits)", "phase B (leaf work)")):
+        print(f"{name:30s} {out[i] / 1e9:9.3f} Gcycles  {100 * out[i] / tot:5.1f} %")
+    print(f"loop trips {int(out[3])}, phase-A checks {int(out[4])}, phase-B entries {int(out[5])}")
+    rays = c["extension_rays"] + c["shadow_rays"]
+    print(f"rays {rays}, per loop trip {rays / max(1, out[3]):.2f}, cycles per ray (summed over waves) {tot / rays:.1f}")
+    tr.destroy()
+
+
+if __name__ == "__main__":
+    main()
