@@ -80,6 +80,7 @@ struct DeviceScene {
     uint32_t cachedNodes;         // nodes [0, cachedNodes) are mirrored in LDS (scene_cache_load)
     uint32_t cachedTris;          // triVerts of triangles [0, cachedTris) likewise, after the nodes
     uint32_t cachedInstances;     // 0, or instanceCount: every inverse transform + identity flag, after the triangles
+    uint32_t singlePrimLeaves;    // 1: every BLAS leaf holds exactly one triangle (BVHAccel.cpp's builder always does)
 };
 
 // LDS scene cache of the traversal kernels: after the per-lane stacks ([stackSize + 2]
@@ -91,13 +92,32 @@ DEV float4* scene_cache(const DeviceScene& sc, uint32_t* stackMem, uint32_t shif
 {
     return (float4*)(stackMem + ((sc.stackSize + 2u) << shift));
 }
+// Triangles of the cache-only variant (ALL_CACHED kernels) are stored three times, once
+// per watertight-test axis permutation: copy z holds every vertex as (v[z+1], v[z+2], v[z])
+// (mod 3) -- the (kx, ky, kz) of a ray whose dominant axis is z -- so the test reads its
+// permuted coordinates instead of selecting them.
+constexpr uint32_t kRotTriFloat4 = 9;   // float4 per triangle: 3 permutations x 3 vertices
+template <bool ROTATED>
+DEV uint32_t cache_tri_float4() { return ROTATED ? kRotTriFloat4 : 3u; }
+
 // Every thread of the block: fill the cache, then a barrier.
+template <bool ROTATED = false>
 DEV void scene_cache_load(const DeviceScene& sc, uint32_t* stackMem, uint32_t shift)
 {
     float4* c = scene_cache(sc, stackMem, shift);
-    const uint32_t nn = sc.cachedNodes * 2u, nt = sc.cachedTris * 3u;
+    const uint32_t nn = sc.cachedNodes * 2u, nt = sc.cachedTris * cache_tri_float4<ROTATED>();
     for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) c[i] = sc.nodes[i];
-    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) c[nn + i] = sc.triVerts[i];
+    for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
+        if (ROTATED) {
+            const uint32_t tri = i / kRotTriFloat4, r = i - tri * kRotTriFloat4, z = r / 3u, k = r - z * 3u;
+            const float4 q = sc.triVerts[(size_t)tri * 3 + k];
+            const float v[3] = {q.x, q.y, q.z};
+            const uint32_t x = z == 2u ? 0u : z + 1u, y = x == 2u ? 0u : x + 1u;
+            c[nn + i] = make_float4(v[x], v[y], v[z], q.w);
+        } else {
+            c[nn + i] = sc.triVerts[i];
+        }
+    }
     // per instance: the inverse float4x3 (3 x float4), then (identity flag, 0, 0, 0)
     for (uint32_t i = threadIdx.x; i < sc.cachedInstances * 4u; i += blockDim.x) {
         const uint32_t inst = i >> 2, k = i & 3u;
@@ -128,6 +148,7 @@ DEV bool ray_aabb(V3 o, V3 inv, float tMin, float tMax, float4 a, float4 b)
 struct Shear {
     int kx, ky, kz;
     float sx, sy, sz;
+    float ox, oy, oz;     // the ray origin permuted, (o[kx], o[ky], o[kz]) (rotated-triangle test)
 };
 DEV Shear make_shear(V3 d)   // BVHAccel.inc.hlsl:72-83
 {
@@ -143,6 +164,13 @@ DEV Shear make_shear(V3 d)   // BVHAccel.inc.hlsl:72-83
     s.sx = -comp(d, x) * invZ;
     s.sy = -comp(d, y) * invZ;
     s.sz = invZ;
+    s.ox = 0.0f; s.oy = 0.0f; s.oz = 0.0f;
+    return s;
+}
+DEV Shear make_shear_rot(V3 d, V3 o)
+{
+    Shear s = make_shear(d);
+    s.ox = comp(o, s.kx); s.oy = comp(o, s.ky); s.oz = comp(o, s.kz);
     return s;
 }
 
@@ -158,6 +186,34 @@ DEV bool tri_watertight(V3 o, const Shear& sh, float tMin, float tMax, V3 v0, V3
     float p0x = comp(a, sh.kx), p0y = comp(a, sh.ky), p0z = comp(a, sh.kz);
     float p1x = comp(b, sh.kx), p1y = comp(b, sh.ky), p1z = comp(b, sh.kz);
     float p2x = comp(c, sh.kx), p2y = comp(c, sh.ky), p2z = comp(c, sh.kz);
+    p0x = p0x + sh.sx * p0z; p0y = p0y + sh.sy * p0z;
+    p1x = p1x + sh.sx * p1z; p1y = p1y + sh.sy * p1z;
+    p2x = p2x + sh.sx * p2z; p2y = p2y + sh.sy * p2z;
+    const float e0 = p1x * p2y - p2x * p1y;
+    const float e1 = p2x * p0y - p0x * p2y;
+    const float e2 = p0x * p1y - p1x * p0y;
+    if ((e0 < 0.0f || e1 < 0.0f || e2 < 0.0f) && (e0 > 0.0f || e1 > 0.0f || e2 > 0.0f)) return false;
+    const float det = e0 + e1 + e2;
+    p0z = p0z * sh.sz; p1z = p1z * sh.sz; p2z = p2z * sh.sz;
+    const float tScaled = e0 * p0z + e1 * p1z + e2 * p2z;
+    const float invDet = 1.0f / det;
+    *t = tScaled * invDet;
+    *u = e1 * invDet;
+    *v = e2 * invDet;
+    *backface = (fsign(sh.sz) * det) < 0.0f;
+    return det != 0.0f && *t >= tMin && *t < tMax;
+}
+
+// The same test on a rotated triangle copy (vertices already (v[kx], v[ky], v[kz])) and
+// the permuted origin in the shear: identical operations, no component selects.
+DEV bool tri_watertight_rot(const Shear& sh, float tMin, float tMax, float4 q0, float4 q1, float4 q2,
+                            float* t, float* u, float* v, bool* backface)
+{
+    *t = 0.0f; *u = 0.0f; *v = 0.0f; *backface = false;
+    if (q0.w != 0.0f) return false;   // degenerate
+    float p0x = q0.x - sh.ox, p0y = q0.y - sh.oy, p0z = q0.z - sh.oz;
+    float p1x = q1.x - sh.ox, p1y = q1.y - sh.oy, p1z = q1.z - sh.oz;
+    float p2x = q2.x - sh.ox, p2y = q2.y - sh.oy, p2z = q2.z - sh.oz;
     p0x = p0x + sh.sx * p0z; p0y = p0y + sh.sy * p0z;
     p1x = p1x + sh.sx * p1z; p1y = p1y + sh.sy * p1z;
     p2x = p2x + sh.sx * p2z; p2y = p2y + sh.sy * p2z;
@@ -403,7 +459,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         const float4* M;
         uint32_t identity;
         if (ALL_CACHED) {
-            M = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u + sc.cachedTris * 3u + primOrInst * 4u;
+            M = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u + sc.cachedTris * kRotTriFloat4 + primOrInst * 4u;
             identity = __float_as_uint(M[3].x);
         } else {
             M = sc.transforms + (size_t)(sc.instanceCount + primOrInst) * 3;
@@ -430,24 +486,34 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         if (INSTR) ++st.blas;
         return false;
     }
-    if (watertight && !s.shearValid) { s.sh = make_shear(s.ld); s.shearValid = true; }
-    const uint32_t begin = leafRef;
-    const uint32_t end = begin + primOrInst;
-    for (uint32_t p = begin; p < end; ++p) {
+    if (watertight && !s.shearValid) {
+        s.sh = ALL_CACHED ? make_shear_rot(s.ld, s.lo) : make_shear(s.ld);
+        s.shearValid = true;
+    }
+    // one triangle test: false = go on, true = the ray is finished (any-hit)
+    auto test = [&](uint32_t p) __attribute__((always_inline)) {
         if (INSTR) ++st.tris;
-        float4 q0, q1, q2;
-        if (ALL_CACHED || p < sc.cachedTris) {
-            const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u;
-            q0 = c[p * 3]; q1 = c[p * 3 + 1]; q2 = c[p * 3 + 2];
+        float t, u, v; bool bf, h;
+        if (ALL_CACHED && watertight) {
+            const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u + p * kRotTriFloat4 + (uint32_t)s.sh.kz * 3u;
+            h = tri_watertight_rot(s.sh, s.tMin, s.tMax, c[0], c[1], c[2], &t, &u, &v, &bf);
         } else {
-            q0 = sc.triVerts[(size_t)p * 3];
-            q1 = sc.triVerts[(size_t)p * 3 + 1];
-            q2 = sc.triVerts[(size_t)p * 3 + 2];
+            float4 q0, q1, q2;
+            if (ALL_CACHED) {
+                const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u + p * kRotTriFloat4 + 6u;
+                q0 = c[0]; q1 = c[1]; q2 = c[2];   // permutation z = 2 is the identity
+            } else if (p < sc.cachedTris) {
+                const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u;
+                q0 = c[p * 3]; q1 = c[p * 3 + 1]; q2 = c[p * 3 + 2];
+            } else {
+                q0 = sc.triVerts[(size_t)p * 3];
+                q1 = sc.triVerts[(size_t)p * 3 + 1];
+                q2 = sc.triVerts[(size_t)p * 3 + 2];
+            }
+            const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
+            h = watertight ? tri_watertight(s.lo, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
+                           : tri_moller(s.lo, s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
         }
-        const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
-        float t, u, v; bool bf;
-        bool h = watertight ? tri_watertight(s.lo, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
-                            : tri_moller(s.lo, s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
         if (OPACITY && h && !s.opaque) h = any_hit_shader(sc, p, s.matOverride, u, v, s.opacitySample);
         if (h) {
             s.found = true;
@@ -457,6 +523,14 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
             s.hit.tri = (p & 0x7FFFFFFFu) | (bf ? 0x80000000u : 0u);
             s.hit.inst = s.inst;
         }
+        return false;
+    };
+    if (sc.singlePrimLeaves) {   // (uniform: straight-line code, no loop)
+        if (test(leafRef)) return true;
+    } else {
+        const uint32_t end = leafRef + primOrInst;
+        for (uint32_t p = leafRef; p < end; ++p)
+            if (test(p)) return true;
     }
     return trav_pop(s, lds, stack_stride<ALL_CACHED>(shift));
 }

@@ -588,7 +588,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void cast_kernel(PathPool 
                                                                      Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
-    scene_cache_load(sc, stackMem, block_shift());
+    scene_cache_load<ALL_CACHED>(sc, stackMem, block_shift());
     QueueMap qe, qs;
     qmap(cnt, kQExt, &qe);
     qmap(cnt, kQShadow, &qs);

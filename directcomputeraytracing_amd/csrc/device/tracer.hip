@@ -458,6 +458,12 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     d.nodeCount = s.bvh_node_count;
     d.triangleCount = s.triangle_count;
     d.stackSize = std::max<uint32_t>(s.bvh_traversal_stack_size, 1u);
+    // BLAS leaves (no TLAS-leaf bit, a primitive count) all with one triangle
+    d.singlePrimLeaves = 1u;
+    for (uint32_t i = 0; i < s.bvh_node_count; ++i) {
+        const uint32_t misc = s.bvh_nodes[i].misc;
+        if (!(misc & 0x4u) && ((misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT) > 1u) { d.singlePrimLeaves = 0u; break; }
+    }
     scene = d;
     // MATERIAL variant: the smallest compiled one whose capabilities cover the scene
     sceneCaps = dEnv ? kCapEnvCube : 0u;
@@ -493,10 +499,11 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
             if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
         }
         // (the LDS-only variant assumes 256-thread workgroups: its stack stride is a constant)
+        // (the cache-only variant keeps three permuted copies of every triangle: 144 B each)
         castAllCached = castBlock == 256 && d.cachedNodes == s.bvh_node_count && d.cachedTris == s.triangle_count &&
-                        budget - (size_t)d.cachedNodes * 32 - (size_t)d.cachedTris * 48 >= (size_t)s.instance_count * 64;
+                        (size_t)d.cachedNodes * 32 + (size_t)s.triangle_count * 144 + (size_t)s.instance_count * 64 <= budget;
         d.cachedInstances = castAllCached ? s.instance_count : 0u;
-        castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * 48 + (size_t)d.cachedInstances * 64;
+        castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * (castAllCached ? 144 : 48) + (size_t)d.cachedInstances * 64;
         scene = d;
     }
     {

@@ -450,6 +450,32 @@ def test_xml_scene_mesh_lights_bit_exact(gpu_tracer, golden_luts, oracle_mod):
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 7]))
 
 
+@pytest.mark.parametrize("cache", ["lds", "global"])
+@pytest.mark.parametrize("features", [0x05, 0x0F, 0x07])
+@pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
+def test_traversal_variants_wavefront_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, scene_name, features, cache):
+    """The merged cast kernel's traversal variants through the whole wavefront path:
+    Moller-Trumbore (WATERTIGHT off), BVH_NO_FRONT_TO_BACK_TRAVERSAL, both; the cache-only
+    kernel (scene, permuted triangle copies and instance transforms in LDS: both scenes
+    fit) and the global-memory kernel (DCRT_NO_LDS_CACHE). xml_mix has transformed
+    rectangle instances (instance-space rays in the BLAS)."""
+    from conftest import GOLDEN
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer
+    if cache == "global":
+        monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+    if scene_name == "cornell":
+        s = cornell(64, 48, 6)
+    else:
+        s = Scene((32, 32))
+        s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
+    s.features = features
+    t = WavefrontPathTracer(path_pool_size=1 << 12, debug_rng=True)
+    try:
+        list(_render_and_compare(t, oracle_mod, golden_luts, s, [0, 3]))
+    finally:
+        t.destroy()
+
+
 @pytest.mark.parametrize("name,cube", [("coffee", True), ("spaceship", False), ("lamp", False)])
 def test_config_scenes_bit_exact(gpu_tracer, golden_luts, oracle_mod, name, cube):
     """configs[2..4] (coffee / spaceship / lamp, procedural XML fixtures) at 160x90, 8 bounces."""
