@@ -400,8 +400,11 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
     uint32_t ahead = 0;
     if (lane < end && itemIndex(lane) < n) ahead = lookup(itemIndex(lane));
     TravState s;
-    bool active = false;
-    bool pending = false;   // this lane's ray is finished and its result not yet written
+    // lane state, one integer (per-lane bools cost mask <-> register conversions per step):
+    // kIdle no ray; kRun visiting nodes; kPark at a leaf (phase B work pending); kFin ray
+    // finished, its result not yet written
+    constexpr uint32_t kIdle = 0, kRun = 1, kPark = 2, kFin = 3;
+    uint32_t ls = kIdle;
     uint32_t item = 0;
 #ifdef DCRT_WAVE_TIMELINE
     const unsigned long long tStart = wall_clock64();
@@ -411,7 +414,8 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         DCRT_PHASE_COUNT(3);
         // refill only when at least kRefillLanes lanes are idle: the fetch (ray loads,
         // three IEEE divisions) is then shared by many lanes
-        const unsigned long long need = __ballot(!active);
+        const bool free = ls == kIdle || ls == kFin;
+        const unsigned long long need = __ballot(free);
         const uint32_t nNeed = (uint32_t)__popcll(need);
         const bool refill = nNeed >= kRefillLanes && cursor < end;
         const uint32_t k = cursor + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
@@ -420,16 +424,16 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         // Finished rays are written here, after the window read and just before the ray
         // loads: stores count in vmcnt too, so written earlier they would make the window
         // read wait for their acknowledgement, and the ray loads then wait once more.
-        if (pending) {
+        if (ls == kFin) {
             emit(item, s);
-            pending = false;
+            ls = kIdle;
         }
         if (refill) {
             const uint32_t idx = itemIndex(k);
-            if (!active && k < end && idx < n) {
+            if (free && k < end && idx < n) {
                 item = fetch(idx, path, s);
                 if (!f2b) s.negMask = 0u;
-                active = true;
+                ls = kRun;
             }
             const uint32_t used = min(nNeed, end - cursor);
             // this lane's window item cursor + ((L - cursor) mod 64) was taken: look up the one 64 later
@@ -439,34 +443,30 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             cursor += used;
         }
         DCRT_PHASE(0);
-        if (__ballot(active) == 0ull) break;
+        if (__ballot(ls != kIdle) == 0ull) break;
         // phase A: node visits only, until enough lanes are parked at leaves (or
         // enough are idle to refill, or none can advance)
-        // (a lane whose ray ends here only flags it: the result is written once, after
-        // the loop, which keeps the stores out of the unrolled visit steps)
-        bool done = false;
+        // (a lane whose ray ends here only flags it: the result is written at the next
+        // refill point, which keeps the stores out of the unrolled visit steps)
         for (;;) {
 #pragma unroll
             for (int k = 0; k < kVisitsPerCheck; ++k) {
-                if (active && !done && !s.parked && trav_visit<INSTR, ALL_CACHED>(sc, s, lds, shift, st)) done = true;
+                if (ls == kRun) {
+                    if (trav_visit<INSTR, ALL_CACHED>(sc, s, lds, shift, st)) ls = kFin;
+                    else if (s.parked) ls = kPark;
+                }
             }
-            const unsigned long long runnable = __ballot(active && !done && !s.parked);
-            const uint32_t parked = (uint32_t)__popcll(__ballot(active && !done && s.parked));
-            const uint32_t idle = (uint32_t)__popcll(__ballot(!active || done));
+            const unsigned long long runnable = __ballot(ls == kRun);
+            const uint32_t parked = (uint32_t)__popcll(__ballot(ls == kPark));
+            const uint32_t idle = 64u - (uint32_t)__popcll(runnable) - parked;
             DCRT_PHASE_COUNT(4);
             if (runnable == 0ull || parked >= kParkLanes || (idle >= kRefillLanes && cursor < end)) break;
         }
         DCRT_PHASE(1);
-        if (done) {
-            pending = true;
-            active = false;
-        }
         // phase B: the parked lanes' leaf work, shared by many lanes at once
-        if (__ballot(active && s.parked) != 0ull) DCRT_PHASE_COUNT(5);
-        if (active && s.parked && trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED>(sc, s, watertight, lds, shift, st)) {
-            pending = true;
-            active = false;
-        }
+        if (__ballot(ls == kPark) != 0ull) DCRT_PHASE_COUNT(5);
+        if (ls == kPark)
+            ls = trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED>(sc, s, watertight, lds, shift, st) ? kFin : kRun;
         DCRT_PHASE(2);
     }
     DCRT_PHASE_FLUSH();
