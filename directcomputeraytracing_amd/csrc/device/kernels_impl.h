@@ -15,6 +15,32 @@
 namespace dcrt {
 namespace dev {
 
+#ifdef DCRT_PHASE_CLOCKS
+// Diagnostic build only (tools/phase_clocks.py): shader-clock cycles the cast kernels'
+// waves spend per phase of the persistent loop, summed over all waves:
+// [0] hand-over + result stores + ray set-up, [1] phase A (node visits), [2] phase B
+// (leaf work), [3] loop trips, [4] phase-A checks, [5] phase-B entries.
+// MATERIAL: [8] loads + Li update, [9] HitInfoToIntersection, [10] emission, [11] NEE
+// (light sample, BSDF eval + pdf, shadow ray), [12] BSDF sample + new ray, [13] stores,
+// [14] queue appends, [15] items.
+__device__ unsigned long long g_phaseClk[16];
+#define DCRT_PHASE_INIT unsigned long long clk_[6] = {0, 0, 0, 0, 0, 0}; unsigned long long tP_ = __builtin_amdgcn_s_memtime()
+#define DCRT_PHASE(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); clk_[i] += t_ - tP_; tP_ = t_; } while (0)
+#define DCRT_PHASE_COUNT(i) (++clk_[i])
+#define DCRT_PHASE_FLUSH() do { if ((threadIdx.x & 63u) == 0) for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phaseClk[i_], clk_[i_]); } while (0)
+#define DCRT_MCLK_INIT unsigned long long mclk_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long mT_ = __builtin_amdgcn_s_memtime()
+#define DCRT_MCLK(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); mclk_[i] += t_ - mT_; mT_ = t_; } while (0)
+#define DCRT_MCLK_FLUSH(items) do { mclk_[7] += (items); if ((threadIdx.x & 63u) == 0) for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_phaseClk[8 + i_], mclk_[i_]); } while (0)
+#else
+#define DCRT_MCLK_INIT do {} while (0)
+#define DCRT_MCLK(i) do {} while (0)
+#define DCRT_MCLK_FLUSH(items) do {} while (0)
+#define DCRT_PHASE_INIT do {} while (0)
+#define DCRT_PHASE(i) do {} while (0)
+#define DCRT_PHASE_COUNT(i) do {} while (0)
+#define DCRT_PHASE_FLUSH() do {} while (0)
+#endif
+
 // One atomic per workgroup: wave ballot + mbcnt prefix, LDS scan over waves.
 // Every thread of the block must call it (it contains barriers).
 __device__ __forceinline__ uint32_t block_append(bool pred, uint32_t* counter, uint32_t* sm)
@@ -34,6 +60,29 @@ __device__ __forceinline__ uint32_t block_append(bool pred, uint32_t* counter, u
     const uint32_t r = sm[32] + sm[wave] + prefix;
     __syncthreads();
     return r;
+}
+
+// Two appends at once (one barrier round for both queues): returns the slots of `pa` in
+// counter a and of `pb` in counter b. sm needs 2 * (waves + 1) words; two calls in a row
+// must use different sm halves (callers alternate), so no third barrier guards reuse.
+__device__ __forceinline__ void block_append2(bool pa, uint32_t* ca, bool pb, uint32_t* cb, uint32_t* sm, uint32_t* ra, uint32_t* rb)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t waves = blockDim.x >> 6;
+    const unsigned long long ma = __ballot(pa), mb = __ballot(pb);
+    const uint32_t xa = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
+    const uint32_t xb = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+    if (lane == 0) { sm[wave] = (uint32_t)__popcll(ma); sm[16 + wave] = (uint32_t)__popcll(mb); }
+    __syncthreads();
+    if (threadIdx.x < 2) {   // thread 0: queue a, thread 1: queue b (their atomics overlap)
+        uint32_t* q = sm + threadIdx.x * 16;
+        uint32_t total = 0;
+        for (uint32_t w = 0; w < waves; ++w) { const uint32_t c = q[w]; q[w] = total; total += c; }
+        q[15] = total ? atomicAdd(threadIdx.x ? cb : ca, total) : 0u;
+    }
+    __syncthreads();
+    *ra = sm[15] + sm[wave] + xa;
+    *rb = sm[31] + sm[16 + wave] + xb;
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
@@ -195,12 +244,16 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
     qmap(cnt, kQMaterial, &qm);
     const uint32_t count = qm.prefix[kShards];
     const uint32_t shard = blockIdx.x % kShards;
+    DCRT_MCLK_INIT;
+    uint32_t itemsDone = 0;
+    uint32_t round = 0;   // grid-stride round: alternates block_append2's sm halves
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
     const bool active = i < count;
     bool terminate = false, hasShadow = false;
     uint32_t path = 0;
     if (active) {
+        ++itemsDone;
         path = qentry(pool.materialQueue, pool.size, qm, i);
         const float4 h4 = pool.hit[path];
         HitRecord hit;
@@ -227,7 +280,9 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         Intersection it;
         it.lightIndex = DCRT_LIGHT_INDEX_INVALID; it.triangleIndex = 0;
         it.geometryNormal = mk(0.0f, 0.0f, 0.0f);
+        DCRT_MCLK(0);
         if (hasHit) hit_to_intersection<CAPS>(sc, hit, it);
+        DCRT_MCLK(1);
         V3 T = mk(thr.x, thr.y, thr.z);
         V3 L = mk(li.x, li.y, li.z);
         // Evaluate light :331-349
@@ -243,6 +298,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                 }
             }
         }
+        DCRT_MCLK(2);
         V3 lsr = mk(0.0f, 0.0f, 0.0f);
         if (bounce > fc->maxBounce || !hasHit) {
             flags |= kFlagTerminate;
@@ -264,6 +320,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                     hasShadow = true;
                 }
             }
+            DCRT_MCLK(3);
             float bsdfPdf = 0.0f;
             bool isDelta = false;
             {
@@ -283,6 +340,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                     terminate = true;
                 }
             }
+            DCRT_MCLK(4);
             thr.w = bsdfPdf;
             li.w = isDelta ? 1.0f : 0.0f;
             if (features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430
@@ -300,11 +358,17 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         pool.li[path] = make_float4(L.x, L.y, L.z, li.w);
         pool.lsr[path] = make_float4(lsr.x, lsr.y, lsr.z, 0.0f);
     }
-    const uint32_t es = block_append(active && !terminate, qctr(cnt, kQExt, shard), sm);
+    DCRT_MCLK(5);
+    uint32_t es, ss;
+    block_append2(active && !terminate, qctr(cnt, kQExt, shard), active && hasShadow, qctr(cnt, kQShadow, shard),
+                  sm + (round & 1u) * 32u, &es, &ss);
     if (active && !terminate) pool.extQueue[(size_t)shard * pool.size + es] = path;
-    const uint32_t ss = block_append(active && hasShadow, qctr(cnt, kQShadow, shard), sm);
     if (active && hasShadow) pool.shadowQueue[(size_t)shard * pool.size + ss] = path;
+    DCRT_MCLK(6);
+    ++round;
     }
+    DCRT_MCLK_FLUSH(itemsDone);
+    (void)itemsDone;
 }
 
 // Cast-kernel occupancy: 5 waves per SIMD (<= 96 VGPRs; the compiler alone takes ~99,
@@ -352,22 +416,6 @@ __device__ uint32_t g_waveItems[2][16][8192];
 #define DCRT_WAVE_TAG(g) (-1)
 #endif
 
-#ifdef DCRT_PHASE_CLOCKS
-// Diagnostic build only (tools/phase_clocks.py): shader-clock cycles the cast kernels'
-// waves spend per phase of the persistent loop, summed over all waves:
-// [0] hand-over + result stores + ray set-up, [1] phase A (node visits), [2] phase B
-// (leaf work), [3] loop trips, [4] phase-A checks, [5] phase-B entries.
-__device__ unsigned long long g_phaseClk[8];
-#define DCRT_PHASE_INIT unsigned long long clk_[6] = {0, 0, 0, 0, 0, 0}; unsigned long long tP_ = __builtin_amdgcn_s_memtime()
-#define DCRT_PHASE(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); clk_[i] += t_ - tP_; tP_ = t_; } while (0)
-#define DCRT_PHASE_COUNT(i) (++clk_[i])
-#define DCRT_PHASE_FLUSH() do { if ((threadIdx.x & 63u) == 0) for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_phaseClk[i_], clk_[i_]); } while (0)
-#else
-#define DCRT_PHASE_INIT do {} while (0)
-#define DCRT_PHASE(i) do {} while (0)
-#define DCRT_PHASE_COUNT(i) do {} while (0)
-#define DCRT_PHASE_FLUSH() do {} while (0)
-#endif
 
 template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, typename Lookup, typename Fetch,
           typename Emit>

@@ -26,7 +26,7 @@ def main():
     tr.render_images(100, 2, filt)
     fn = tr._lib.dcrt_debug_phase_clocks
     fn.restype = C.c_int
-    out = np.zeros(8, np.uint64)
+    out = np.zeros(16, np.uint64)
     assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
     tr.reset_stats()
     tr.render_images(0, 8, filt)
@@ -38,6 +38,12 @@ def main():
     print(f"loop trips {int(out[3])}, phase-A checks {int(out[4])}, phase-B entries {int(out[5])}")
     rays = c["extension_rays"] + c["shadow_rays"]
     print(f"rays {rays}, per loop trip {rays / max(1, out[3]):.2f}, cycles per ray (summed over waves) {tot / rays:.1f}")
+    m = out[8:15].astype(np.float64)
+    mt = m.sum()
+    print(f"MATERIAL: {int(out[15])} lane-items (waves x items), wave-cycles per wave-item {mt / max(1, out[15]):.0f}")
+    for i, name in enumerate(("loads + Li update", "HitInfoToIntersection", "emission (EvaluateLight)", "NEE: light sample, BSDF eval/pdf, shadow ray",
+                              "BSDF sample + new ray", "stores", "queue appends")):
+        print(f"  {name:46s} {m[i] / 1e9:8.3f} Gcycles  {100 * m[i] / mt:5.1f} %")
     tr.destroy()
 
 
