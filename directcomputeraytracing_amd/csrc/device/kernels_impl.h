@@ -176,21 +176,22 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
         idle = true;
     }
     const bool carryShadowHit = !idle && shadowHit;
-    const uint32_t mslot = block_append(!idle, qctr(cnt, kQMaterial, shard), sm);
-    if (!idle) pool.materialQueue[(size_t)shard * pool.size + mslot] = tid;
-
-    // A fully idle wave claims the next 8x8 block (one atomic per workgroup); at a batch
-    // start (all slots idle, cursors preset) wave j of the shard takes block j outright.
+    // A fully idle wave claims the next 8x8 block (one atomic per workgroup, in the same
+    // barrier round as the material-queue append); at a batch start (all slots idle,
+    // cursors preset) wave j of the shard takes block j outright.
     const bool waveIdle = __ballot(!idle) == 0ull;
+    bool want = false;
+    if (!staticFill && waveIdle && lane == 0)
+        want = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shardBlocks;
+    uint32_t mslot, bslot;
+    block_append2(!idle, qctr(cnt, kQMaterial, shard), want, cursor, sm, &mslot, &bslot);
+    if (!idle) pool.materialQueue[(size_t)shard * pool.size + mslot] = tid;
     uint32_t claimed = 0;
     bool got = false;
     if (staticFill) {
         claimed = (blockIdx.x / kShards) * (blockDim.x >> 6) + (threadIdx.x >> 6);
         got = waveIdle && claimed < shardBlocks;
     } else {
-        bool want = false;
-        if (waveIdle && lane == 0) want = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shardBlocks;
-        const uint32_t bslot = block_append(want, cursor, sm);
         claimed = (uint32_t)__shfl((int)bslot, 0, 64);
         got = __shfl((int)want, 0, 64) != 0 && claimed < shardBlocks;
     }
@@ -221,7 +222,10 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             bounce = 0;
         }
     }
-    const uint32_t eslot = block_append(newPath, qctr(cnt, kQExt, shard), sm);
+    // (the other half of sm: the next round's first append reuses the first half only
+    // after every thread has passed this append's barriers)
+    uint32_t eslot, unused;
+    block_append2(newPath, qctr(cnt, kQExt, shard), false, qctr(cnt, kQExt, shard), sm + 32, &eslot, &unused);
     if (newPath) pool.extQueue[(size_t)shard * pool.size + eslot] = tid;
     const uint32_t newFlags = (idle ? kFlagIdle : 0u) | (carryShadowHit ? kFlagShadowRayHit : 0u) | (bounce & 0xFFu);
     if (newFlags != flags) pool.flags[tid] = newFlags;   // a live path's flags mostly stay as they are
