@@ -51,7 +51,8 @@ struct TextureDesc {
 // Everything a kernel needs about the scene, passed by value (kernel argument).
 struct DeviceScene {
     const float4* nodes;          // 2 x float4 per BVHNode (min.xyz,max.x | max.yz,right,misc)
-    const float4* triVerts;       // 3 x float4 per triangle: world-independent BLAS positions
+    const float4* triVerts;       // 3 x float4 per triangle: BLAS positions (q0.w degenerate flag, q1.w material id bits)
+    const float4* triShade;       // 6 x float4 per triangle: per vertex (normal.xyz, tangent.x), (tangent.yz, uv)
     const dcrt_vertex* vertices;
     const uint32_t* triangles;
     const uint32_t* materialIds;
@@ -672,14 +673,17 @@ DEV void hit_to_intersection(const DeviceScene& s, const HitRecord& h, Intersect
     it.lightIndex = s.instanceLightIndices[inst];
     it.triangleIndex = tri;
     const uint32_t ov = s.overrides[inst];
-    const dcrt_vertex& V0 = s.vertices[s.triangles[tri * 3]];
-    const dcrt_vertex& V1 = s.vertices[s.triangles[tri * 3 + 1]];
-    const dcrt_vertex& V2 = s.vertices[s.triangles[tri * 3 + 2]];
+    // the triangle's vertices as pre-gathered at upload (build_tri_*_kernel): the same
+    // values as vertices[triangles[3 tri + k]], one fetch level less
+    const float4* P = s.triVerts + (size_t)tri * 3;
+    const float4* Q = s.triShade + (size_t)tri * 6;
+    const float4 q0 = P[0], q1 = P[1], q2 = P[2];
+    const float4 a0 = Q[0], b0 = Q[1], a1 = Q[2], b1 = Q[3], a2 = Q[4], b2 = Q[5];
     const float u = h.u, v = h.v;
-    const V3 p0 = ld3(V0.position), p1 = ld3(V1.position), p2 = ld3(V2.position);
+    const V3 p0 = mk(q0.x, q0.y, q0.z), p1 = mk(q1.x, q1.y, q1.z), p2 = mk(q2.x, q2.y, q2.z);
     it.position = bary3(p0, p1, p2, u, v);
-    it.normal = normalize(bary3(ld3(V0.normal), ld3(V1.normal), ld3(V2.normal), u, v));
-    V3 tangent = bary3(ld3(V0.tangent), ld3(V1.tangent), ld3(V2.tangent), u, v);
+    it.normal = normalize(bary3(mk(a0.x, a0.y, a0.z), mk(a1.x, a1.y, a1.z), mk(a2.x, a2.y, a2.z), u, v));
+    V3 tangent = bary3(mk(a0.w, b0.x, b0.y), mk(a1.w, b1.x, b1.y), mk(a2.w, b2.x, b2.y), u, v);
     float tl = length(tangent);
     if (tl >= 0.000001f) {
         tangent = tangent - it.normal * dot(tangent, it.normal);
@@ -692,7 +696,7 @@ DEV void hit_to_intersection(const DeviceScene& s, const HitRecord& h, Intersect
     }
     it.tangent = tangent / tl;
     it.geometryNormal = normalize(cross(p2 - p0, p1 - p0));
-    const uint32_t mid = ov != DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE ? ov : s.materialIds[tri];
+    const uint32_t mid = ov != DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE ? ov : __float_as_uint(q1.w);
     const dcrt_material& m = s.materials[mid];
     if constexpr ((CAPS & kCapTextures) == 0u) {
         __builtin_assume(m.albedo_texture_index == -1);
@@ -704,10 +708,10 @@ DEV void hit_to_intersection(const DeviceScene& s, const HitRecord& h, Intersect
         __builtin_assume(((CAPS >> (m.flags & DCRT_MATERIAL_FLAG_TYPE_MASK)) & 1u) != 0u);
     }
     // VectorBaryCentric2 (Math.inc.hlsl:23-33)
-    float r1x = V1.texcoord[0] - V0.texcoord[0], r1y = V1.texcoord[1] - V0.texcoord[1];
-    float r2x = V2.texcoord[0] - V0.texcoord[0], r2y = V2.texcoord[1] - V0.texcoord[1];
+    float r1x = b1.z - b0.z, r1y = b1.w - b0.w;
+    float r2x = b2.z - b0.z, r2y = b2.w - b0.w;
     r1x = r1x * u; r1y = r1y * u; r2x = r2x * v; r2y = r2y * v;
-    r1x = r1x + V0.texcoord[0]; r1y = r1y + V0.texcoord[1];
+    r1x = r1x + b0.z; r1y = r1y + b0.w;
     float tcx = r1x + r2x, tcy = r1y + r2y;
     tcx = tcx * m.tex_tiling[0]; tcy = tcy * m.tex_tiling[1];
     V3 albedo = ld3(m.albedo);
@@ -740,7 +744,11 @@ struct LightSample {
     float pdf, distance;
     bool isDelta;
 };
-DEV V3 tri_pos(const DeviceScene& s, uint32_t tri, int k) { return ld3(s.vertices[s.triangles[tri * 3 + k]].position); }
+DEV V3 tri_pos(const DeviceScene& s, uint32_t tri, int k)
+{
+    const float4 q = s.triVerts[(size_t)tri * 3 + k];   // (the vertex position, gathered at upload)
+    return mk(q.x, q.y, q.z);
+}
 
 template <uint32_t CAPS = kCapAll>
 DEV LightSample sample_light(const DeviceScene& s, V3 p, uint32_t lightCount, Rng& rng)

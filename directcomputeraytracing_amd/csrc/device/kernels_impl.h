@@ -126,7 +126,11 @@ __device__ __forceinline__ void begin_batch_claims(Globals* g)
     g->staticFill = G ? 1u : 0u;
 }
 
-__global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32_t* triangles, uint32_t count, float4* out)
+// Upload-time gathers of the triangles' vertices (one fetch level less for the traversal
+// and for MATERIAL's HitInfoToIntersection): positions (+ the degenerate flag and the
+// per-triangle material id in the w words) and the shading attributes.
+__global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32_t* triangles, const uint32_t* materialIds,
+                                       uint32_t count, float4* out, float4* shade)
 {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= count) return;
@@ -134,11 +138,15 @@ __global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32
     for (int k = 0; k < 3; ++k) {
         const dcrt_vertex& v = vertices[triangles[t * 3 + k]];
         p[k] = mk(v.position[0], v.position[1], v.position[2]);
+        shade[(size_t)t * 6 + 2 * k] = make_float4(v.normal[0], v.normal[1], v.normal[2], v.tangent[0]);
+        shade[(size_t)t * 6 + 2 * k + 1] = make_float4(v.tangent[1], v.tangent[2], v.texcoord[0], v.texcoord[1]);
     }
     // RayTriangleIntersect's degenerate test (RayPrimitiveIntersect.inc.hlsl), hoisted to upload time
     const V3 cp = cross(p[1] - p[0], p[2] - p[0]);
     const float degenerate = dot(cp, cp) == 0.0f ? 1.0f : 0.0f;
-    for (int k = 0; k < 3; ++k) out[(size_t)t * 3 + k] = make_float4(p[k].x, p[k].y, p[k].z, k == 0 ? degenerate : 0.0f);
+    out[(size_t)t * 3] = make_float4(p[0].x, p[0].y, p[0].z, degenerate);
+    out[(size_t)t * 3 + 1] = make_float4(p[1].x, p[1].y, p[1].z, __uint_as_float(materialIds[t]));
+    out[(size_t)t * 3 + 2] = make_float4(p[2].x, p[2].y, p[2].z, 0.0f);
 }
 
 // ---- CONTROL (+ NEW_PATH) -------------------------------------------------------

@@ -404,8 +404,12 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     CHECKED(upload(&mats, s.materials, s.material_count));
     CHECKED(upload(&lights, s.lights, std::max<uint32_t>(s.light_count, 1)));
     float4* triVerts = nullptr;
+    float4* triShade = nullptr;
     CHECKED(DeviceAlloc(&triVerts, (size_t)s.triangle_count * 3, &sceneAllocs));
-    hipLaunchKernelGGL(build_tri_verts_kernel, dim3((s.triangle_count + 255) / 256), dim3(256), 0, stream, vtx, tris, s.triangle_count, triVerts);
+    CHECKED(DeviceAlloc(&triShade, (size_t)s.triangle_count * 6, &sceneAllocs));
+    if (s.triangle_count)
+        hipLaunchKernelGGL(build_tri_verts_kernel, dim3((s.triangle_count + 255) / 256), dim3(256), 0, stream, vtx, tris, mids,
+                           s.triangle_count, triVerts, triShade);
     HIPCHECK(hipGetLastError());
     // textures: one texel blob + descriptors (Scene.cpp:586-608)
     std::vector<TextureDesc> descs(std::max<uint32_t>(s.texture_count, 1));
@@ -433,6 +437,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     if (s.env_cube_rgb && s.env_cube_size) CHECKED(upload(&dEnv, s.env_cube_rgb, (size_t)6 * s.env_cube_size * s.env_cube_size * 3));
     d.nodes = (const float4*)nodes;
     d.triVerts = triVerts;
+    d.triShade = triShade;
     d.vertices = vtx;
     d.triangles = tris;
     d.materialIds = mids;
