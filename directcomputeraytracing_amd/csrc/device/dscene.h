@@ -487,8 +487,12 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         if (INSTR) ++st.blas;
         return false;
     }
-    if (watertight && !s.shearValid) {
-        s.sh = ALL_CACHED ? make_shear_rot(s.ld, s.lo) : make_shear(s.ld);
+    if (ALL_CACHED) {
+        // recomputed at every leaf instead of kept across visits: one register less, and
+        // the cache-only kernel then fits 7 waves/SIMD in 72 VGPRs (3.03 -> 2.96 ms/spp)
+        if (watertight) s.sh = make_shear_rot(s.ld, s.lo);
+    } else if (watertight && !s.shearValid) {
+        s.sh = make_shear(s.ld);
         s.shearValid = true;
     }
     // one triangle test: false = go on, true = the ray is finished (any-hit)
