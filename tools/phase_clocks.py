@@ -17,8 +17,9 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
+    bounces = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     scene = Scene((1920, 1080))
-    scenes.setup_cornell(scene, 1920, 1080, 8)
+    scenes.setup_cornell(scene, 1920, 1080, bounces)
     tr = WavefrontPathTracer(path_pool_size=1 << 24, iterations_per_render=16)
     tr.on_scene_loaded(scene)
     filt = scene.filter_params()
@@ -28,16 +29,28 @@ def main():
     fn.restype = C.c_int
     out = np.zeros(16, np.uint64)
     assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
+    # node visits of the same 8 images (instrumented kernel), then the clocked run
+    tr.set_instrumentation(True, False)
+    tr.reset_stats()
+    tr.render_images(0, 8, filt)
+    st = tr.traversal_stats()
+    tr.set_instrumentation(False, False)
+    assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
     tr.reset_stats()
     tr.render_images(0, 8, filt)
     assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
     c = tr.counters()
+    visits = st["ext_node_visits"] + st["shadow_node_visits"]
+    leaves = st["ext_triangle_tests"] + st["shadow_triangle_tests"] + st["ext_blas_entries"] + st["shadow_blas_entries"]
+    print(f"max bounce {bounces}: node visits {visits}, leaf events {leaves}")
     tot = float(out[0] + out[1] + out[2])
     for i, name in enumerate(("hand-over + stores + set-up", "phase A (node visits)", "phase B (leaf work)")):
         print(f"{name:30s} {out[i] / 1e9:9.3f} Gcycles  {100 * out[i] / tot:5.1f} %")
     print(f"loop trips {int(out[3])}, phase-A checks {int(out[4])}, phase-B entries {int(out[5])}")
     rays = c["extension_rays"] + c["shadow_rays"]
     print(f"rays {rays}, per loop trip {rays / max(1, out[3]):.2f}, cycles per ray (summed over waves) {tot / rays:.1f}")
+    print(f"wave-cycles per node visit: phase A {out[1] / max(1, visits):.2f}, all phases {tot / max(1, visits):.2f}; "
+          f"phase B per leaf event {out[2] / max(1, leaves):.2f}")
     m = out[8:15].astype(np.float64)
     mt = m.sum()
     print(f"MATERIAL: {int(out[15])} lane-items (waves x items), wave-cycles per wave-item {mt / max(1, out[15]):.0f}")
