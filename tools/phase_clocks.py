@@ -17,10 +17,15 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
-    bounces = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    arg = sys.argv[1] if len(sys.argv) > 1 else "8"
     scene = Scene((1920, 1080))
-    scenes.setup_cornell(scene, 1920, 1080, bounces)
-    tr = WavefrontPathTracer(path_pool_size=1 << 24, iterations_per_render=16)
+    if arg.isdigit():   # Cornell with this max bounce
+        bounces = int(arg)
+        scenes.setup_cornell(scene, 1920, 1080, bounces)
+    else:               # a BASELINE config scene (coffee / spaceship / lamp)
+        print(scenes.setup_config(scene, arg, "/tmp/dcrt_scenes"))
+        bounces = scene.frame_params(0).max_bounce_count
+    tr = WavefrontPathTracer(path_pool_size=scenes.default_pool(*scene.resolution), iterations_per_render=16)
     tr.on_scene_loaded(scene)
     filt = scene.filter_params()
     tr.clear_film()
@@ -32,12 +37,13 @@ def main():
     # node visits of the same 8 images (instrumented kernel), then the clocked run
     tr.set_instrumentation(True, False)
     tr.reset_stats()
-    tr.render_images(0, 8, filt)
+    images = 8 if arg.isdigit() else 2
+    tr.render_images(0, images, filt)
     st = tr.traversal_stats()
     tr.set_instrumentation(False, False)
     assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
     tr.reset_stats()
-    tr.render_images(0, 8, filt)
+    tr.render_images(0, images, filt)
     assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
     c = tr.counters()
     visits = st["ext_node_visits"] + st["shadow_node_visits"]
