@@ -281,7 +281,7 @@ struct TravState {
     uint32_t sp;          // stack entries x stride (bytes): see stack_at
     uint32_t inst;
     uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked; not kept with ALL_CACHED)
-    bool shearValid, found, parked, noZero;   // noZero: no component of o, d is +-0
+    bool found, parked, noZero;   // noZero: no component of o, d is +-0
     bool anyHit;          // merged cast kernel: this lane's ray is a shadow ray (first hit ends it)
     uint32_t pathFlags;   // shadow ray: the path's flags as MATERIAL wrote them (shadowD.w)
     // Near/far choice of the current space: bit a = (ld[a] < 0) for the axes a = 0..2,
@@ -311,7 +311,7 @@ DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax, bool f2b = 
     s.tMin = tMin; s.tMax = tMax;
     s.node = 0; s.sp = 0; s.inst = 0;
     s.leafRef = 0; s.leafMisc = 0;
-    s.shearValid = false; s.found = false; s.parked = false; s.anyHit = false;
+    s.found = false; s.parked = false; s.anyHit = false;
     s.noZero = o.x != 0.0f && o.y != 0.0f && o.z != 0.0f && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
     s.hit.t = 0.0f; s.hit.u = 0.0f; s.hit.v = 0.0f; s.hit.tri = 0u; s.hit.inst = 0u;
     s.opacitySample = 0.0f; s.matOverride = DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE; s.opaque = false;
@@ -370,7 +370,6 @@ DEV bool trav_pop(TravState& s, uint32_t* lds, uint32_t stride)
         s.ld = mk(s.d.x, s.d.y, s.d.z);
         s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
         s.negMask = neg_mask(s.d, s.negMask);
-        s.shearValid = false;
     }
     return false;
 }
@@ -432,7 +431,6 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         s.ld = mk(s.d.x, s.d.y, s.d.z);
         s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
         s.negMask = neg_mask(s.d, s.negMask);
-        s.shearValid = false;
     }
     s.parked = hit && leaf;
     if (!ALL_CACHED) {   // (ALL_CACHED: phase B reads them from the LDS copy of the node)
@@ -477,7 +475,6 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
             s.inv = inv_dir(s.ld);
         }
         s.negMask = neg_mask(s.ld, s.negMask);
-        s.shearValid = false;
         s.inst = primOrInst;
         s.node = leafRef | 0x80000000u;   // the BLAS root
         if (OPACITY) {   // BVHAccel.inc.hlsl:136-139
@@ -487,14 +484,10 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         if (INSTR) ++st.blas;
         return false;
     }
-    if (ALL_CACHED) {
-        // recomputed at every leaf instead of kept across visits: one register less, and
-        // the cache-only kernel then fits 7 waves/SIMD in 72 VGPRs (3.03 -> 2.96 ms/spp)
-        if (watertight) s.sh = make_shear_rot(s.ld, s.lo);
-    } else if (watertight && !s.shearValid) {
-        s.sh = make_shear(s.ld);
-        s.shearValid = true;
-    }
+    // the shear of the current space, recomputed at every leaf instead of kept across
+    // visits: fewer live registers (the cache-only kernel fits 7 waves/SIMD in 72 VGPRs:
+    // 3.03 -> 2.96 ms/spp; coffee / lamp configs -1 to -2 %)
+    if (watertight) s.sh = ALL_CACHED ? make_shear_rot(s.ld, s.lo) : make_shear(s.ld);
     // one triangle test: false = go on, true = the ray is finished (any-hit)
     auto test = [&](uint32_t p) __attribute__((always_inline)) {
         if (INSTR) ++st.tris;
