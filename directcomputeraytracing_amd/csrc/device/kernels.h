@@ -15,6 +15,7 @@ namespace dev {
 constexpr uint32_t kFlagIdle = 0x80000000u;           // WavefrontPathTracing.hlsl:27-64
 constexpr uint32_t kFlagShadowRayHit = 0x40000000u;
 constexpr uint32_t kFlagTerminate = 0x20000000u;
+constexpr uint32_t kFlagDelta = 0x10000000u;           // the path's last BSDF lobe was a delta (SPathAccumulation.isDelta)
 constexpr uint32_t kBlockW = 8, kBlockH = 8;           // one wave64 = one 8x8 pixel block
 #ifndef DCRT_CONTROL_BLOCK
 #define DCRT_CONTROL_BLOCK 256
@@ -131,9 +132,19 @@ DEV void generate_ray(const FrameConstants& f, float fsx, float fsy, float a0, f
     *direction = mul44(d, 0.0f, f.camera);
 }
 
+// Three floats, 12 B (dwordx3): path arrays whose fourth word would carry nothing
+struct F3 {
+    float x, y, z;
+};
+// four floats at 4-B alignment: a 16-B load at an F3 boundary (global_load_dwordx4 needs
+// dword alignment only)
+struct alignas(4) F4u {
+    float x, y, z, w;
+};
+
 struct PathPool {
-    float4* rayO;        // origin.xyz, tMax
-    float4* rayD;        // direction.xyz, tMin
+    F3* rayO;            // extension ray origin (tMax = inf, tMin = 0 implicit); size + 1 entries
+    F3* rayD;            // extension ray direction; size + 1 entries (the cast kernel's 16-B reads)
     float4* hit;         // t, u, v, asfloat(triangle | backface << 31)
     uint32_t* hitInst;
     float4* shadowO;
@@ -141,9 +152,9 @@ struct PathPool {
     uint32_t* pixel;     // sample index: image * W*H + y * W + x
     float2* pixelSample;
     uint4* rng;
-    float4* lsr;         // light sampling result
+    F3* lsr;             // light sampling result
     float4* throughput;  // T.xyz, bsdfPdf
-    float4* li;          // Li.xyz, isDeltaBxdf (0/1)
+    F3* li;              // Li (isDelta: kFlagDelta in flags)
     uint32_t* flags;
     float* extOpacity;         // ALLOW_ANYHIT_SHADER: g_ExtensionRayOpacitySamples
     float* shadowOpacity;      //                      g_ShadowRayOpacitySamples

@@ -172,8 +172,8 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     // MATERIAL does this addition as its first step (same operands, same bits), so the
     // path's Li is read and written once per iteration; the shadow-hit bit is carried.
     if (!idle && terminate) {
-        float4 li = pool.li[tid];
-        const float4 lsr = pool.lsr[tid];
+        F3 li = pool.li[tid];
+        const F3 lsr = pool.lsr[tid];
         li.x = li.x + (!shadowHit ? lsr.x : 0.0f);
         li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
         li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
@@ -219,11 +219,11 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) pool.extOpacity[tid] = next1(rng);   // :223-226
             pool.pixel[tid] = image * (film.width * film.height) + py * film.width + px;
             pool.pixelSample[tid] = make_float2(psx, psy);
-            pool.lsr[tid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            pool.lsr[tid] = F3{0.0f, 0.0f, 0.0f};
             pool.rng[tid] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
-            pool.rayO[tid] = make_float4(o.x, o.y, o.z, inf());
-            pool.rayD[tid] = make_float4(d.x, d.y, d.z, 0.0f);
-            pool.li[tid] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+            pool.rayO[tid] = F3{o.x, o.y, o.z};
+            pool.rayD[tid] = F3{d.x, d.y, d.z};
+            pool.li[tid] = F3{0.0f, 0.0f, 0.0f};   // isDelta = true: kFlagDelta below
             pool.throughput[tid] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
             newPath = true;
             idle = false;
@@ -235,7 +235,8 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     uint32_t eslot, unused;
     block_append2(newPath, qctr(cnt, kQExt, shard), false, qctr(cnt, kQExt, shard), sm + 32, &eslot, &unused);
     if (newPath) pool.extQueue[(size_t)shard * pool.size + eslot] = tid;
-    const uint32_t newFlags = (idle ? kFlagIdle : 0u) | (carryShadowHit ? kFlagShadowRayHit : 0u) | (bounce & 0xFFu);
+    const uint32_t delta = newPath ? kFlagDelta : (!idle ? flags & kFlagDelta : 0u);
+    const uint32_t newFlags = (idle ? kFlagIdle : 0u) | (carryShadowHit ? kFlagShadowRayHit : 0u) | delta | (bounce & 0xFFu);
     if (newFlags != flags) pool.flags[tid] = newFlags;   // a live path's flags mostly stay as they are
     }
 }
@@ -270,16 +271,16 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         const float4 h4 = pool.hit[path];
         HitRecord hit;
         hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = pool.hitInst[path];
-        const float4 ro = pool.rayO[path], rd = pool.rayD[path];
+        const F3 rd = pool.rayD[path];
         const V3 dir = mk(rd.x, rd.y, rd.z);
         const uint4 r4 = pool.rng[path];
         Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
         float4 thr = pool.throughput[path];
-        float4 li = pool.li[path];
+        F3 li = pool.li[path];
         uint32_t flags = pool.flags[path];
         {
             // CONTROL's Li += light sampling result (:520-528), done here for live paths
-            const float4 lsr0 = pool.lsr[path];
+            const F3 lsr0 = pool.lsr[path];
             const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
             li.x = li.x + (!shadowHit ? lsr0.x : 0.0f);
             li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                 V3 radiance; float lightPdf;
                 evaluate_light<CAPS>(sc, lightIndex, it.triangleIndex, it.geometryNormal, dir, hit.t, fc->lightCount, &radiance, &lightPdf);
                 if (lightPdf > 0.0f) {
-                    const float weight = !(li.w != 0.0f) ? power_heuristic(thr.w, lightPdf) : 1.0f;
+                    const float weight = !(flags & kFlagDelta) ? power_heuristic(thr.w, lightPdf) : 1.0f;
                     L = L + T * radiance * weight;
                 }
             }
@@ -344,8 +345,8 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                     const float NdotWI = fabsf(dot(it.normal, wi));
                     T = T * bsdf * NdotWI / bsdfPdf;
                     const V3 o = offset_ray_origin(it.position, it.geometryNormal, wi);
-                    pool.rayO[path] = make_float4(o.x, o.y, o.z, inf());
-                    pool.rayD[path] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+                    pool.rayO[path] = F3{o.x, o.y, o.z};
+                    pool.rayD[path] = F3{wi.x, wi.y, wi.z};
                     flags = (flags & 0xFFFFFF00u) | ((bounce + 1) & 0xFFu);
                 } else {
                     flags |= kFlagTerminate;
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             }
             DCRT_MCLK(4);
             thr.w = bsdfPdf;
-            li.w = isDelta ? 1.0f : 0.0f;
+            flags = isDelta ? flags | kFlagDelta : flags & ~kFlagDelta;
             if (features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430
                 if (!terminate) pool.extOpacity[path] = next1(rng);
                 if (hasShadow) pool.shadowOpacity[path] = next1(rng);
@@ -367,8 +368,8 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         if (hasShadow) reinterpret_cast<float*>(&pool.shadowD[path])[3] = asf(flags);
         pool.rng[path] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
         pool.throughput[path] = make_float4(T.x, T.y, T.z, thr.w);
-        pool.li[path] = make_float4(L.x, L.y, L.z, li.w);
-        pool.lsr[path] = make_float4(lsr.x, lsr.y, lsr.z, 0.0f);
+        pool.li[path] = F3{L.x, L.y, L.z};
+        pool.lsr[path] = F3{lsr.x, lsr.y, lsr.z};
     }
     DCRT_MCLK(5);
     uint32_t es, ss;
@@ -582,7 +583,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
         sc, qm.prefix[kShards], fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) { return qentry(pool.extQueue, pool.size, qm, i); },
         [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
-            const float4 o = pool.rayO[path], d = pool.rayD[path];
+            const F3 o = pool.rayO[path], d = pool.rayD[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf());
             if (OPACITY) s.opacitySample = pool.extOpacity[path];
             return path;
@@ -661,8 +662,8 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     const uint32_t nExt = qe.prefix[kShards], nShadow = qs.prefix[kShards];
     const uint32_t* extQueue = sgpr_ptr(pool.extQueue);
     const uint32_t* shQueue = sgpr_ptr(pool.shadowQueue);
-    const float4* rayO = sgpr_ptr(pool.rayO);
-    const float4* rayD = sgpr_ptr(pool.rayD);
+    const float* rayO = sgpr_ptr((float*)pool.rayO);
+    const float* rayD = sgpr_ptr((float*)pool.rayD);
     const float4* shO = sgpr_ptr(pool.shadowO);
     const float4* shD = sgpr_ptr(pool.shadowD);
     TraversalStats st = {0u, 0u, 0u};
@@ -675,8 +676,11 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
         },
         [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
             const bool shadow = i >= nExt;
-            const float4 o = (shadow ? shO : rayO)[path];
-            const float4 d = (shadow ? shD : rayD)[path];
+            // one 16-B load for either kind: a shadow ray's float4, or an extension ray's 12-B
+            // F3 and the next entry's first word (unused; the arrays carry a spare entry)
+            const size_t at = (size_t)path * (shadow ? 4u : 3u);
+            const F4u o = *(const F4u*)((shadow ? (const float*)shO : rayO) + at);
+            const F4u d = *(const F4u*)((shadow ? (const float*)shD : rayD) + at);
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, shadow ? o.w : inf());
             s.anyHit = shadow;
             s.pathFlags = asu(d.w);

@@ -277,8 +277,8 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     }
     // WavefrontPathTracer.cpp:120-264 (SoA instead of AoS)
     const size_t P = poolSize;
-    CHECKED(DeviceAlloc(&pool.rayO, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.rayD, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.rayO, (size_t)P + 1, &poolAllocs));   // (+1: the cast kernel's 16-B reads of 12-B entries)
+    CHECKED(DeviceAlloc(&pool.rayD, (size_t)P + 1, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.hit, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.hitInst, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowO, P, &poolAllocs));
