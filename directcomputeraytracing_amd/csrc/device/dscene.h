@@ -271,6 +271,11 @@ struct TraversalStats {
     uint32_t nodes;   // iterationCounter (BVHAccel.inc.hlsl:121)
     uint32_t tris;    // triangle tests
     uint32_t blas;    // TLAS -> BLAS entries
+#ifdef DCRT_PHASE_CLOCKS
+    // diagnostic build: node visits served by the LDS scene cache; pushes onto a stack
+    // already 4 / 8 / 12 entries deep
+    uint32_t cached, deep4, deep8, deep12;
+#endif
 };
 
 struct TravState {
@@ -387,6 +392,11 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
 {
     if (INSTR) ++st.nodes;
     const uint32_t stride = stack_stride<ALL_CACHED>(shift);
+#ifdef DCRT_PHASE_CLOCKS
+    if (INSTR) {
+        st.cached += (ALL_CACHED || (s.node & 0x7FFFFFFFu) < sc.cachedNodes) ? 1u : 0u;
+    }
+#endif
     // the stack top (read only by a pop) is issued together with the node fetch: this
     // visit's push writes the row above it, so the two LDS round trips of a visit overlap
     const uint32_t top = stack_at(lds, s.sp);
@@ -422,6 +432,13 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     const bool pop = !hit && !empty;
     const bool done = !hit && empty;
     const bool restore = pop && (int)s.node < 0 && (int)top >= 0;    // BLAS -> TLAS: back to the world ray
+#ifdef DCRT_PHASE_CLOCKS
+    if (INSTR && descend) {
+        st.deep4 += s.sp >= 4u * stride ? 1u : 0u;
+        st.deep8 += s.sp >= 8u * stride ? 1u : 0u;
+        st.deep12 += s.sp >= 12u * stride ? 1u : 0u;
+    }
+#endif
     s.node = descend ? nearChild : (pop ? top : s.node);
     s.sp = descend ? s.sp + stride : (pop ? s.sp - stride : s.sp);
     // rare (about once per ray): a branch the wave skips when no lane restores; as

@@ -23,7 +23,7 @@ namespace dev {
 // MATERIAL: [8] loads + Li update, [9] HitInfoToIntersection, [10] emission, [11] NEE
 // (light sample, BSDF eval + pdf, shadow ray), [12] BSDF sample + new ray, [13] stores,
 // [14] queue appends, [15] items.
-__device__ unsigned long long g_phaseClk[16];
+__device__ unsigned long long g_phaseClk[24];
 #define DCRT_PHASE_INIT unsigned long long clk_[6] = {0, 0, 0, 0, 0, 0}; unsigned long long tP_ = __builtin_amdgcn_s_memtime()
 #define DCRT_PHASE(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); clk_[i] += t_ - tP_; tP_ = t_; } while (0)
 #define DCRT_PHASE_COUNT(i) (++clk_[i])
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
     scene_cache_load(sc, stackMem, block_shift());
     QueueMap qm;
     qmap(cnt, kQExt, &qm);
-    TraversalStats st = {0u, 0u, 0u};
+    TraversalStats st = {};
     persistent_trace<false, INSTR, OPACITY>(
         sc, qm.prefix[kShards], fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) { return qentry(pool.extQueue, pool.size, qm, i); },
@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
     QueueMap qm;
     qmap(cnt, kQShadow, &qm);
     const uint32_t n = qm.prefix[kShards];
-    TraversalStats st = {0u, 0u, 0u};
+    TraversalStats st = {};
     persistent_trace<true, INSTR, OPACITY>(
         sc, n, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) { return qentry(pool.shadowQueue, pool.size, qm, i); },
@@ -666,8 +666,8 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     const float* rayD = sgpr_ptr((float*)pool.rayD);
     const float4* shO = sgpr_ptr(pool.shadowO);
     const float4* shD = sgpr_ptr(pool.shadowD);
-    TraversalStats st = {0u, 0u, 0u};
-    TraversalStats stExt = {0u, 0u, 0u}, stShadow = {0u, 0u, 0u};
+    TraversalStats st = {};
+    TraversalStats stExt = {}, stShadow = {};
     persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
@@ -685,7 +685,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
             s.anyHit = shadow;
             s.pathFlags = asu(d.w);
             if (OPACITY) s.opacitySample = shadow ? pool.shadowOpacity[path] : pool.extOpacity[path];
-            if (INSTR) { st.nodes = 0u; st.tris = 0u; st.blas = 0u; }
+            if (INSTR) st = TraversalStats{};
             return path;
         },
         [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
@@ -699,10 +699,22 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
             if (INSTR) {
                 TraversalStats& dst = s.anyHit ? stShadow : stExt;
                 dst.nodes += st.nodes; dst.tris += st.tris; dst.blas += st.blas;
+#ifdef DCRT_PHASE_CLOCKS
+                dst.cached += st.cached; dst.deep4 += st.deep4; dst.deep8 += st.deep8; dst.deep12 += st.deep12;
+#endif
             }
         },
         st, DCRT_WAVE_TAG(g));
     if (INSTR) { flush_stats(stExt, instr); flush_stats(stShadow, instr + 3); }
+#ifdef DCRT_PHASE_CLOCKS
+    if (INSTR) {
+        const unsigned long long c = wave_sum(stExt.cached + stShadow.cached), d4 = wave_sum(stExt.deep4 + stShadow.deep4),
+                                 d8 = wave_sum(stExt.deep8 + stShadow.deep8), d12 = wave_sum(stExt.deep12 + stShadow.deep12);
+        if ((threadIdx.x & 63u) == 0) {
+            atomicAdd(&g_phaseClk[16], c); atomicAdd(&g_phaseClk[17], d4); atomicAdd(&g_phaseClk[18], d8); atomicAdd(&g_phaseClk[19], d12);
+        }
+    }
+#endif
     end_iteration(cnt, nextCnt, g, nShadow);
 }
 
@@ -718,7 +730,7 @@ __device__ __forceinline__ bool trace_full(const DeviceScene& sc, V3 o, V3 d, fl
     TravState s;
     trav_init(s, o, d, 0.0f, tMax, f2b);
     s.opacitySample = opacitySample;
-    TraversalStats st = {0u, 0u, 0u};
+    TraversalStats st = {};
     for (;;) {
         if (trav_visit<false>(sc, s, lds, shift, st)) break;
         if (s.parked && trav_leaf<ANY_HIT, false, OPACITY>(sc, s, watertight, lds, shift, st)) break;
@@ -866,7 +878,7 @@ __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const 
 {
     extern __shared__ uint32_t stackMem[];
     scene_cache_load(sc, stackMem, block_shift());
-    TraversalStats st = {0u, 0u, 0u};
+    TraversalStats st = {};
     persistent_trace<ANY, true, false>(
         sc, n, features, 16u, 32u, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) { return i; },

@@ -1394,7 +1394,7 @@ extern "C" DCRT_API int dcrt_debug_phase_clocks(dcrt_tracer* t, unsigned long lo
     TRACER_GUARD(t);
     HIPCHECK(hipStreamSynchronize(t->stream));
     HIPCHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phaseClk), sizeof(g_phaseClk)));
-    const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long zero[24] = {};
     HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phaseClk), zero, sizeof(zero)));
     return DCRT_OK;
 }

@@ -32,7 +32,7 @@ def main():
     tr.render_images(100, 2, filt)
     fn = tr._lib.dcrt_debug_phase_clocks
     fn.restype = C.c_int
-    out = np.zeros(16, np.uint64)
+    out = np.zeros(24, np.uint64)
     assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
     # node visits of the same 8 images (instrumented kernel), then the clocked run
     tr.set_instrumentation(True, False)
@@ -42,13 +42,15 @@ def main():
     st = tr.traversal_stats()
     tr.set_instrumentation(False, False)
     assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
+    diag = out[16:20].copy()
     tr.reset_stats()
     tr.render_images(0, images, filt)
     assert fn(tr._h, out.ctypes.data_as(C.c_void_p)) == 0
     c = tr.counters()
     visits = st["ext_node_visits"] + st["shadow_node_visits"]
     leaves = st["ext_triangle_tests"] + st["shadow_triangle_tests"] + st["ext_blas_entries"] + st["shadow_blas_entries"]
-    print(f"max bounce {bounces}: node visits {visits}, leaf events {leaves}")
+    print(f"max bounce {bounces}: node visits {visits}, leaf events {leaves}; from the LDS cache "
+          f"{100 * diag[0] / max(1, visits):.1f} %; pushes onto >= 4 / 8 / 12 entries {int(diag[1])} / {int(diag[2])} / {int(diag[3])}")
     tot = float(out[0] + out[1] + out[2])
     for i, name in enumerate(("hand-over + stores + set-up", "phase A (node visits)", "phase B (leaf work)")):
         print(f"{name:30s} {out[i] / 1e9:9.3f} Gcycles  {100 * out[i] / tot:5.1f} %")
