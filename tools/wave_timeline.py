@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-wave timeline of the EXT / SHADOW cast kernels (1 image, 1080p Cornell).
+"""Diagnostic: per-wave timeline of the cast kernels (1080p Cornell; argv: log2 pool size,
+images, optional .npz output for the raw stamps -- default 21 1; `24 8` is one batch of the bench's workload, one pipeline).
 
 Needs a library built with -DDCRT_WAVE_TIMELINE (gpu_ab/timeline.so, DCRT_LIB=...).
 For each iteration slot prints: waves, items, kernel span (first start .. last end),
@@ -20,12 +21,15 @@ def main():
     from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
     scene = Scene((1920, 1080))
     scenes.setup_cornell(scene, 1920, 1080, 8)
-    tr = WavefrontPathTracer(path_pool_size=1 << 21, iterations_per_render=16)
+    pool = int(sys.argv[1]) if len(sys.argv) > 1 else 21
+    images = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    tr = WavefrontPathTracer(path_pool_size=1 << pool, iterations_per_render=16)
     tr.on_scene_loaded(scene)
     filt = scene.filter_params()
     tr.clear_film()
-    tr.render_images(100, 1, filt)
-    tr.render_images(0, 1, filt)
+    if images == 1:
+        tr.render_images(100, 1, filt)
+    tr.render_images(0, images, filt)
     tr.synchronize()
     fn = tr._lib.dcrt_debug_wave_timeline
     fn.restype = C.c_int
@@ -33,6 +37,8 @@ def main():
     items = np.zeros((2, 16, 8192), np.uint32)
     rc = fn(tr._h, stamps.ctypes.data_as(C.c_void_p), items.ctypes.data_as(C.c_void_p))
     assert rc == 0, rc
+    if len(sys.argv) > 3:
+        np.savez_compressed(sys.argv[3], stamps=stamps, items=items)
     for k, name in enumerate(("EXT", "SHADOW")):
         for it in range(16):
             st = stamps[k, it]
