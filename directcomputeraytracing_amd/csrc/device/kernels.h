@@ -142,6 +142,16 @@ struct alignas(4) F4u {
     float x, y, z, w;
 };
 
+// Element i of a path-pool array through a 32-bit byte offset (every pool array is
+// < 4 GiB): the access then takes the array base in SGPRs plus one VGPR offset
+// (global_load v, v_off, s[base]) instead of a 64-bit VGPR address per array, which
+// MATERIAL otherwise keeps live from a path's loads to its stores
+template <typename T>
+DEV T& slot(T* base, uint32_t i)
+{
+    return *(T*)((char*)base + (uint64_t)(i * (uint32_t)sizeof(T)));
+}
+
 struct PathPool {
     F3* rayO;            // extension ray origin (tMax = inf, tMin = 0 implicit); size + 1 entries
     F3* rayD;            // extension ray direction; size + 1 entries (the cast kernel's 16-B reads)

@@ -268,24 +268,33 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
     if (active) {
         ++itemsDone;
         path = qentry(pool.materialQueue, pool.size, qm, i);
-        const float4 h4 = pool.hit[path];
+        const float4 h4 = slot(pool.hit, path);
         HitRecord hit;
-        hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = pool.hitInst[path];
-        const F3 rd = pool.rayD[path];
+        hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, path);
+        const F3 rd = slot(pool.rayD, path);
         const V3 dir = mk(rd.x, rd.y, rd.z);
-        const uint4 r4 = pool.rng[path];
+#ifndef DCRT_MAT_LATE_LOADS
+        const uint4 r4 = slot(pool.rng, path);
         Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
-        float4 thr = pool.throughput[path];
-        F3 li = pool.li[path];
-        uint32_t flags = pool.flags[path];
+        float4 thr = slot(pool.throughput, path);
+        F3 li = slot(pool.li, path);
+#endif
+        uint32_t flags = slot(pool.flags, path);
+#ifndef DCRT_MAT_LATE_LOADS
         {
             // CONTROL's Li += light sampling result (:520-528), done here for live paths
-            const F3 lsr0 = pool.lsr[path];
+            const F3 lsr0 = slot(pool.lsr, path);
             const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
             li.x = li.x + (!shadowHit ? lsr0.x : 0.0f);
             li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
             li.z = li.z + (!shadowHit ? lsr0.z : 0.0f);
         }
+#endif
+        // the slot index as a fresh value for the stores below: their addresses are then
+        // formed where they are used instead of being shared with the loads' and kept
+        // live in VGPR pairs across the whole shading code
+        uint32_t out = path;
+        asm volatile("" : "+v"(out));
         const uint32_t bounce = flags & 0xFFu;
         const uint32_t features = fc->features;
         const bool vndf = (features & DCRT_FEATURE_GGX_SAMPLE_VNDF) != 0;
@@ -296,13 +305,30 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         DCRT_MCLK(0);
         if (hasHit) hit_to_intersection<CAPS>(sc, hit, it);
         DCRT_MCLK(1);
+#ifdef DCRT_MAT_LATE_LOADS
+        float4 thr = slot(pool.throughput, path);
+        F3 li = slot(pool.li, path);
+        {
+            const F3 lsr0 = slot(pool.lsr, path);
+            const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
+            li.x = li.x + (!shadowHit ? lsr0.x : 0.0f);
+            li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
+            li.z = li.z + (!shadowHit ? lsr0.z : 0.0f);
+        }
+        const uint4 r4 = slot(pool.rng, path);
+        Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
+#endif
         V3 T = mk(thr.x, thr.y, thr.z);
         V3 L = mk(li.x, li.y, li.z);
         // Evaluate light :331-349
         {
             const uint32_t lightIndex = hasHit ? it.lightIndex : fc->envLightIndex;
             const bool visible = (features & DCRT_FEATURE_LIGHT_VISIBLE) != 0;
+#ifdef DCRT_X_NO_EVAL
+            if (false) {
+#else
             if (visible ? lightIndex != DCRT_LIGHT_INDEX_INVALID : (bounce > 0 && lightIndex != DCRT_LIGHT_INDEX_INVALID)) {
+#endif
                 V3 radiance; float lightPdf;
                 evaluate_light<CAPS>(sc, lightIndex, it.triangleIndex, it.geometryNormal, dir, hit.t, fc->lightCount, &radiance, &lightPdf);
                 if (lightPdf > 0.0f) {
@@ -319,7 +345,11 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         } else {
             const V3 wo = -dir;
             const BsdfFrame bf = bsdf_frame(sc, wo, it);
+#ifdef DCRT_X_NO_NEE
+            if (false) {
+#else
             if (fc->lightCount != 0) {
+#endif
                 const LightSample ls = sample_light<CAPS>(sc, it.position, fc->lightCount, rng);
                 if (any_pos(ls.radiance) && ls.pdf > 0.0f) {
                     const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, bf, it);
@@ -328,8 +358,8 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                     const float weight = ls.isDelta ? 1.0f : power_heuristic(ls.pdf, bsdfPdf);
                     lsr = T * ls.radiance * bsdf * NdotWI * weight / ls.pdf;
                     const V3 so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
-                    pool.shadowO[path] = make_float4(so.x, so.y, so.z, ls.distance);
-                    pool.shadowD[path] = make_float4(ls.wi.x, ls.wi.y, ls.wi.z, 0.0f);
+                    slot(pool.shadowO, out) = make_float4(so.x, so.y, so.z, ls.distance);
+                    slot(pool.shadowD, out) = make_float4(ls.wi.x, ls.wi.y, ls.wi.z, 0.0f);
                     hasShadow = true;
                 }
             }
@@ -340,13 +370,17 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                 const float sel = next1(rng);
                 const float sx = next1(rng), sy = next1(rng);
                 V3 wi, bsdf;
+#ifdef DCRT_X_NO_SAMPLE
+                wi = mk(sx, sy, sel); bsdf = wi; bsdfPdf = sx;
+#else
                 sample_bsdf(sc, vndf, bf, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
+#endif
                 if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
                     const float NdotWI = fabsf(dot(it.normal, wi));
                     T = T * bsdf * NdotWI / bsdfPdf;
                     const V3 o = offset_ray_origin(it.position, it.geometryNormal, wi);
-                    pool.rayO[path] = F3{o.x, o.y, o.z};
-                    pool.rayD[path] = F3{wi.x, wi.y, wi.z};
+                    slot(pool.rayO, out) = F3{o.x, o.y, o.z};
+                    slot(pool.rayD, out) = F3{wi.x, wi.y, wi.z};
                     flags = (flags & 0xFFFFFF00u) | ((bounce + 1) & 0xFFu);
                 } else {
                     flags |= kFlagTerminate;
@@ -357,26 +391,26 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             thr.w = bsdfPdf;
             flags = isDelta ? flags | kFlagDelta : flags & ~kFlagDelta;
             if (features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430
-                if (!terminate) pool.extOpacity[path] = next1(rng);
-                if (hasShadow) pool.shadowOpacity[path] = next1(rng);
+                if (!terminate) slot(pool.extOpacity, out) = next1(rng);
+                if (hasShadow) slot(pool.shadowOpacity, out) = next1(rng);
             }
         }
         if (!hasShadow) flags = flags & ~kFlagShadowRayHit;
-        pool.flags[path] = flags;
+        slot(pool.flags, out) = flags;
         // the shadow cast writes the path's flags with the occlusion bit (a plain store, no
         // read of the flags in front of it): it takes them from shadowD.w (tMin, unused: 0)
-        if (hasShadow) reinterpret_cast<float*>(&pool.shadowD[path])[3] = asf(flags);
-        pool.rng[path] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
-        pool.throughput[path] = make_float4(T.x, T.y, T.z, thr.w);
-        pool.li[path] = F3{L.x, L.y, L.z};
-        pool.lsr[path] = F3{lsr.x, lsr.y, lsr.z};
+        if (hasShadow) reinterpret_cast<float*>(&slot(pool.shadowD, out))[3] = asf(flags);
+        slot(pool.rng, out) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+        slot(pool.throughput, out) = make_float4(T.x, T.y, T.z, thr.w);
+        slot(pool.li, out) = F3{L.x, L.y, L.z};
+        slot(pool.lsr, out) = F3{lsr.x, lsr.y, lsr.z};
     }
     DCRT_MCLK(5);
     uint32_t es, ss;
     block_append2(active && !terminate, qctr(cnt, kQExt, shard), active && hasShadow, qctr(cnt, kQShadow, shard),
                   sm + (round & 1u) * 32u, &es, &ss);
-    if (active && !terminate) pool.extQueue[(size_t)shard * pool.size + es] = path;
-    if (active && hasShadow) pool.shadowQueue[(size_t)shard * pool.size + ss] = path;
+    if (active && !terminate) slot(pool.extQueue, shard * pool.size + es) = path;
+    if (active && hasShadow) slot(pool.shadowQueue, shard * pool.size + ss) = path;
     DCRT_MCLK(6);
     ++round;
     }
@@ -841,7 +875,11 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
                 V3 wi, bsdf;
                 float bsdfPdf = 0.0f;
                 bool isDelta = false;
+#ifdef DCRT_X_NO_SAMPLE
+                wi = mk(sx, sy, sel); bsdf = wi; bsdfPdf = sx;
+#else
                 sample_bsdf(sc, vndf, bf, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
+#endif
                 if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
                     const float NdotWI = fabsf(dot(it.normal, wi));
                     T = T * bsdf * NdotWI / bsdfPdf;
