@@ -273,14 +273,11 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, path);
         const F3 rd = slot(pool.rayD, path);
         const V3 dir = mk(rd.x, rd.y, rd.z);
-#ifndef DCRT_MAT_LATE_LOADS
         const uint4 r4 = slot(pool.rng, path);
         Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
         float4 thr = slot(pool.throughput, path);
         F3 li = slot(pool.li, path);
-#endif
         uint32_t flags = slot(pool.flags, path);
-#ifndef DCRT_MAT_LATE_LOADS
         {
             // CONTROL's Li += light sampling result (:520-528), done here for live paths
             const F3 lsr0 = slot(pool.lsr, path);
@@ -289,7 +286,6 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
             li.z = li.z + (!shadowHit ? lsr0.z : 0.0f);
         }
-#endif
         // the slot index as a fresh value for the stores below: their addresses are then
         // formed where they are used instead of being shared with the loads' and kept
         // live in VGPR pairs across the whole shading code
@@ -305,30 +301,13 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         DCRT_MCLK(0);
         if (hasHit) hit_to_intersection<CAPS>(sc, hit, it);
         DCRT_MCLK(1);
-#ifdef DCRT_MAT_LATE_LOADS
-        float4 thr = slot(pool.throughput, path);
-        F3 li = slot(pool.li, path);
-        {
-            const F3 lsr0 = slot(pool.lsr, path);
-            const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
-            li.x = li.x + (!shadowHit ? lsr0.x : 0.0f);
-            li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
-            li.z = li.z + (!shadowHit ? lsr0.z : 0.0f);
-        }
-        const uint4 r4 = slot(pool.rng, path);
-        Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
-#endif
         V3 T = mk(thr.x, thr.y, thr.z);
         V3 L = mk(li.x, li.y, li.z);
         // Evaluate light :331-349
         {
             const uint32_t lightIndex = hasHit ? it.lightIndex : fc->envLightIndex;
             const bool visible = (features & DCRT_FEATURE_LIGHT_VISIBLE) != 0;
-#ifdef DCRT_X_NO_EVAL
-            if (false) {
-#else
             if (visible ? lightIndex != DCRT_LIGHT_INDEX_INVALID : (bounce > 0 && lightIndex != DCRT_LIGHT_INDEX_INVALID)) {
-#endif
                 V3 radiance; float lightPdf;
                 evaluate_light<CAPS>(sc, lightIndex, it.triangleIndex, it.geometryNormal, dir, hit.t, fc->lightCount, &radiance, &lightPdf);
                 if (lightPdf > 0.0f) {
@@ -345,11 +324,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         } else {
             const V3 wo = -dir;
             const BsdfFrame bf = bsdf_frame(sc, wo, it);
-#ifdef DCRT_X_NO_NEE
-            if (false) {
-#else
             if (fc->lightCount != 0) {
-#endif
                 const LightSample ls = sample_light<CAPS>(sc, it.position, fc->lightCount, rng);
                 if (any_pos(ls.radiance) && ls.pdf > 0.0f) {
                     const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, bf, it);
@@ -370,11 +345,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                 const float sel = next1(rng);
                 const float sx = next1(rng), sy = next1(rng);
                 V3 wi, bsdf;
-#ifdef DCRT_X_NO_SAMPLE
-                wi = mk(sx, sy, sel); bsdf = wi; bsdfPdf = sx;
-#else
                 sample_bsdf(sc, vndf, bf, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
-#endif
                 if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
                     const float NdotWI = fabsf(dot(it.normal, wi));
                     T = T * bsdf * NdotWI / bsdfPdf;
@@ -875,11 +846,7 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
                 V3 wi, bsdf;
                 float bsdfPdf = 0.0f;
                 bool isDelta = false;
-#ifdef DCRT_X_NO_SAMPLE
-                wi = mk(sx, sy, sel); bsdf = wi; bsdfPdf = sx;
-#else
                 sample_bsdf(sc, vndf, bf, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
-#endif
                 if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
                     const float NdotWI = fabsf(dot(it.normal, wi));
                     T = T * bsdf * NdotWI / bsdfPdf;
