@@ -30,9 +30,18 @@ constexpr uint32_t kControlBlock = DCRT_CONTROL_BLOCK;  // CONTROL workgroup (th
 constexpr uint32_t kShards = 8;
 constexpr uint32_t kShardStride = 64;                  // uint32 words (256 B)
 constexpr uint32_t kQExt = 0, kQShadow = 1, kQMaterial = 2, kQueues = 3;
+// Material-queue counter shards (CONTROL appends once per workgroup, only MATERIAL reads
+// the queue). 16 / 32 shards cut CONTROL by 10 % on one pipeline (178 -> 161 us) but the
+// two-pipeline bench lost 1.5-3 % (2.74-2.81 vs 2.79-2.85 ms/spp, tools/ab_libs.sh, three
+// passes): MATERIAL's longer shard-prefix lookup. Each shard holds matCap entries.
+#ifndef DCRT_MAT_SHARDS
+#define DCRT_MAT_SHARDS 8
+#endif
+constexpr uint32_t kMatShards = DCRT_MAT_SHARDS;
+constexpr uint32_t kCounterWords = 2 * kShards + kMatShards;   // ext, shadow, then material shards
 
 struct Counters {        // one set per iteration parity
-    uint32_t w[kQueues * kShards * kShardStride];
+    uint32_t w[kCounterWords * kShardStride];
 };
 struct Globals {
     uint32_t nextBlock[kShards * kShardStride];        // per-shard pixel-block cursors
@@ -60,20 +69,24 @@ DEV uint32_t qtotal(const Counters* c, uint32_t q)
     for (uint32_t s = 0; s < kShards; ++s) t += qctr_load(c, q, s);
     return t;
 }
-// Concatenated view of the shards of one queue: item i -> (shard, offset).
-struct QueueMap {
-    uint32_t prefix[kShards + 1];
+// Concatenated view of the N shards of one queue: item i -> (shard, offset).
+template <uint32_t N = kShards>
+struct QueueMapN {
+    uint32_t prefix[N + 1];
 };
-DEV void qmap(const Counters* c, uint32_t q, QueueMap* m)
+using QueueMap = QueueMapN<kShards>;
+template <uint32_t N>
+DEV void qmap(const Counters* c, uint32_t q, QueueMapN<N>* m)
 {
     m->prefix[0] = 0;
-    for (uint32_t s = 0; s < kShards; ++s) m->prefix[s + 1] = m->prefix[s] + qctr_load(c, q, s);
+    for (uint32_t s = 0; s < N; ++s) m->prefix[s + 1] = m->prefix[s] + qctr_load(c, q, s);
 }
-DEV uint32_t qentry(const uint32_t* queue, uint32_t cap, const QueueMap& m, uint32_t i)
+template <uint32_t N>
+DEV uint32_t qentry(const uint32_t* queue, uint32_t cap, const QueueMapN<N>& m, uint32_t i)
 {
     uint32_t s = 0, base = 0;                 // static indices only: no scratch for the map
 #pragma unroll
-    for (uint32_t k = 1; k < kShards; ++k) {
+    for (uint32_t k = 1; k < N; ++k) {
         const bool ge = i >= m.prefix[k];
         s += ge ? 1u : 0u;
         base = ge ? m.prefix[k] : base;
@@ -170,8 +183,9 @@ struct PathPool {
     float* shadowOpacity;      //                      g_ShadowRayOpacitySamples
     uint32_t* extQueue;        // kShards x size entries each
     uint32_t* shadowQueue;
-    uint32_t* materialQueue;
+    uint32_t* materialQueue;   // kMatShards x matCap entries
     uint32_t size;
+    uint32_t matCap;           // entries per material-queue shard
 };
 
 // Sample textures (m_SamplePositionTexture / m_SampleValueTexture) for every image of a

@@ -192,8 +192,9 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     if (!staticFill && waveIdle && lane == 0)
         want = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shardBlocks;
     uint32_t mslot, bslot;
-    block_append2(!idle, qctr(cnt, kQMaterial, shard), want, cursor, sm, &mslot, &bslot);
-    if (!idle) pool.materialQueue[(size_t)shard * pool.size + mslot] = tid;
+    const uint32_t mshard = blockIdx.x % kMatShards;
+    block_append2(!idle, qctr(cnt, kQMaterial, mshard), want, cursor, sm, &mslot, &bslot);
+    if (!idle) slot(pool.materialQueue, mshard * pool.matCap + mslot) = tid;
     uint32_t claimed = 0;
     bool got = false;
     if (staticFill) {
@@ -253,9 +254,9 @@ template <uint32_t CAPS>
 __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt)
 {
     __shared__ uint32_t sm[64];
-    QueueMap qm;
+    QueueMapN<kMatShards> qm;
     qmap(cnt, kQMaterial, &qm);
-    const uint32_t count = qm.prefix[kShards];
+    const uint32_t count = qm.prefix[kMatShards];
     const uint32_t shard = blockIdx.x % kShards;
     DCRT_MCLK_INIT;
     uint32_t itemsDone = 0;
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
     uint32_t path = 0;
     if (active) {
         ++itemsDone;
-        path = qentry(pool.materialQueue, pool.size, qm, i);
+        path = qentry(pool.materialQueue, pool.matCap, qm, i);
         const float4 h4 = slot(pool.hit, path);
         HitRecord hit;
         hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, path);
@@ -607,7 +608,9 @@ __device__ __forceinline__ void end_iteration(const Counters* cnt, Counters* nex
 {
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
-            const uint32_t ext = qtotal(cnt, kQExt), material = qtotal(cnt, kQMaterial);
+            uint32_t material = 0;
+            for (uint32_t sh = 0; sh < kMatShards; ++sh) material += qctr_load(cnt, kQMaterial, sh);
+            const uint32_t ext = qtotal(cnt, kQExt);
             g->extRays += ext;
             g->shadowRays += shadowRays;
             g->iterations += 1ull;
@@ -615,7 +618,7 @@ __device__ __forceinline__ void end_iteration(const Counters* cnt, Counters* nex
             // IsImageComplete (WavefrontPathTracer.cpp:508-523), exact and on the device
             g->imageComplete = (material == 0u && ext == 0u && !g->stopped) ? 1u : 0u;
         }
-        if (threadIdx.x < kQueues * kShards) nextCnt->w[threadIdx.x * kShardStride] = 0u;
+        if (threadIdx.x < kCounterWords) nextCnt->w[threadIdx.x * kShardStride] = 0u;
     }
 }
 

@@ -294,7 +294,13 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.shadowOpacity, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.extQueue, (size_t)P * kShards, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowQueue, (size_t)P * kShards, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.materialQueue, (size_t)P * kShards, &poolAllocs));
+    {
+        // CONTROL workgroup b appends its live slots to material shard b % kMatShards
+        const uint64_t G = std::min<uint32_t>(poolSize / kControlBlock, kControlMaxBlocks);
+        const uint64_t rounds = (P + G * kControlBlock - 1) / (G * kControlBlock);
+        pool.matCap = (uint32_t)(((G + kMatShards - 1) / kMatShards) * rounds * kControlBlock);
+    }
+    CHECKED(DeviceAlloc(&pool.materialQueue, (size_t)pool.matCap * kMatShards, &poolAllocs));
     pool.size = poolSize;
     CHECKED(DeviceAlloc(&dFrame, 1, &poolAllocs));
     CHECKED(DeviceAlloc(&dCounters, 2, &poolAllocs));
@@ -833,10 +839,8 @@ int dcrt_tracer::ReadCompletion(bool* complete)
     HIPCHECK(hipMemcpyAsync(hCounters, dCounters + last, sizeof(Counters), hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipStreamSynchronize(stream));
     uint32_t material = 0, ext = 0;
-    for (uint32_t sh = 0; sh < kShards; ++sh) {
-        material += hCounters->w[(kQMaterial * kShards + sh) * kShardStride];
-        ext += hCounters->w[(kQExt * kShards + sh) * kShardStride];
-    }
+    for (uint32_t sh = 0; sh < kMatShards; ++sh) material += hCounters->w[(kQMaterial * kShards + sh) * kShardStride];
+    for (uint32_t sh = 0; sh < kShards; ++sh) ext += hCounters->w[(kQExt * kShards + sh) * kShardStride];
     *complete = material == 0 && ext == 0;
     return DCRT_OK;
 }
