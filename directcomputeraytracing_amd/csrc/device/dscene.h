@@ -151,7 +151,9 @@ struct Shear {
     float sx, sy, sz;
     float ox, oy, oz;     // the ray origin permuted, (o[kx], o[ky], o[kz]) (rotated-triangle test)
 };
-DEV Shear make_shear(V3 d)   // BVHAccel.inc.hlsl:72-83
+// inv = (1/d.x, 1/d.y, 1/d.z) as the slab test already holds it: the shear's 1/d[kz] is
+// the same IEEE quotient, so it is selected instead of divided again at every leaf
+DEV Shear make_shear(V3 d, V3 inv)   // BVHAccel.inc.hlsl:72-83
 {
     Shear s;
     const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
@@ -160,17 +162,16 @@ DEV Shear make_shear(V3 d)   // BVHAccel.inc.hlsl:72-83
     int x = z + 1; x = x == 3 ? 0 : x;
     int y = x + 1; y = y == 3 ? 0 : y;
     s.kx = x; s.ky = y; s.kz = z;
-    const float dz = comp(d, z);
-    const float invZ = 1.0f / dz;
+    const float invZ = comp(inv, z);
     s.sx = -comp(d, x) * invZ;
     s.sy = -comp(d, y) * invZ;
     s.sz = invZ;
     s.ox = 0.0f; s.oy = 0.0f; s.oz = 0.0f;
     return s;
 }
-DEV Shear make_shear_rot(V3 d, V3 o)
+DEV Shear make_shear_rot(V3 d, V3 o, V3 inv)
 {
-    Shear s = make_shear(d);
+    Shear s = make_shear(d, inv);
     s.ox = comp(o, s.kx); s.oy = comp(o, s.ky); s.oz = comp(o, s.kz);
     return s;
 }
@@ -504,7 +505,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
     // the shear of the current space, recomputed at every leaf instead of kept across
     // visits: fewer live registers (the cache-only kernel fits 7 waves/SIMD in 72 VGPRs:
     // 3.03 -> 2.96 ms/spp; coffee / lamp configs -1 to -2 %)
-    if (watertight) s.sh = ALL_CACHED ? make_shear_rot(s.ld, s.lo) : make_shear(s.ld);
+    if (watertight) s.sh = ALL_CACHED ? make_shear_rot(s.ld, s.lo, s.inv) : make_shear(s.ld, s.inv);
     // one triangle test: false = go on, true = the ray is finished (any-hit)
     auto test = [&](uint32_t p) __attribute__((always_inline)) {
         if (INSTR) ++st.tris;
