@@ -423,7 +423,9 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     const bool descend = hit && !leaf;
     // near/far by the split axis' direction sign (one bit of the space's sign mask);
     // children keep the BLAS bit of the packed node reference
-    const bool neg = ((s.negMask >> (misc & 0x3u)) & 1u) != 0u;
+    // (v_bfe takes its offset from the low 5 bits of misc: the split axis for an interior
+    // node; for a leaf, whose neg is unused, a bit of negMask above bit 3, i.e. 0)
+    const bool neg = __builtin_amdgcn_ubfe(s.negMask, misc, 1u) != 0u;
     const uint32_t next = s.node + 1u;
     const uint32_t rightRef = right | (s.node & 0x80000000u);
     const uint32_t nearChild = neg ? rightRef : next;
