@@ -194,7 +194,9 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     uint32_t mslot, bslot;
     const uint32_t mshard = blockIdx.x % kMatShards;
     block_append2(!idle, qctr(cnt, kQMaterial, mshard), want, cursor, sm, &mslot, &bslot);
-    if (!idle) slot(pool.materialQueue, mshard * pool.matCap + mslot) = tid;
+    // (bit 31: the path's first MATERIAL pass, whose Li, light sampling result and
+    // throughput are the NEW_PATH constants and are not stored or loaded)
+    if (!idle) slot(pool.materialQueue, mshard * pool.matCap + mslot) = tid | (bounce == 0u ? 0x80000000u : 0u);
     uint32_t claimed = 0;
     bool got = false;
     if (staticFill) {
@@ -220,12 +222,12 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) pool.extOpacity[tid] = next1(rng);   // :223-226
             pool.pixel[tid] = image * (film.width * film.height) + py * film.width + px;
             pool.pixelSample[tid] = make_float2(psx, psy);
-            pool.lsr[tid] = F3{0.0f, 0.0f, 0.0f};
             pool.rng[tid] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
             pool.rayO[tid] = F3{o.x, o.y, o.z};
             pool.rayD[tid] = F3{d.x, d.y, d.z};
-            pool.li[tid] = F3{0.0f, 0.0f, 0.0f};   // isDelta = true: kFlagDelta below
-            pool.throughput[tid] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+            // Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0 are implicit: the path's
+            // first MATERIAL pass takes them as constants (material-queue bit 31); isDelta =
+            // true: kFlagDelta below
             newPath = true;
             idle = false;
             bounce = 0;
@@ -268,7 +270,9 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
     uint32_t path = 0;
     if (active) {
         ++itemsDone;
-        path = qentry(pool.materialQueue, pool.matCap, qm, i);
+        const uint32_t entry = qentry(pool.materialQueue, pool.matCap, qm, i);
+        path = entry & 0x7FFFFFFFu;
+        const bool first = (entry >> 31) != 0u;   // NEW_PATH's constants, not loaded
         const float4 h4 = slot(pool.hit, path);
         HitRecord hit;
         hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, path);
@@ -276,12 +280,12 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         const V3 dir = mk(rd.x, rd.y, rd.z);
         const uint4 r4 = slot(pool.rng, path);
         Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
-        float4 thr = slot(pool.throughput, path);
-        F3 li = slot(pool.li, path);
+        float4 thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : slot(pool.throughput, path);
+        F3 li = first ? F3{0.0f, 0.0f, 0.0f} : slot(pool.li, path);
         uint32_t flags = slot(pool.flags, path);
         {
             // CONTROL's Li += light sampling result (:520-528), done here for live paths
-            const F3 lsr0 = slot(pool.lsr, path);
+            const F3 lsr0 = first ? F3{0.0f, 0.0f, 0.0f} : slot(pool.lsr, path);
             const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
             li.x = li.x + (!shadowHit ? lsr0.x : 0.0f);
             li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
