@@ -253,7 +253,8 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
 // CAPS: the scene capabilities this variant is compiled for (kCapAll = any scene; see
 // kCapOpaqueDelta in dscene.h and dcrt_tracer::UploadScene).
 template <uint32_t CAPS>
-__global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt)
+__global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
+                                                                             Film film)
 {
     __shared__ uint32_t sm[64];
     QueueMapN<kMatShards> qm;
@@ -372,14 +373,26 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             }
         }
         if (!hasShadow) flags = flags & ~kFlagShadowRayHit;
-        slot(pool.flags, out) = flags;
-        // the shadow cast writes the path's flags with the occlusion bit (a plain store, no
-        // read of the flags in front of it): it takes them from shadowD.w (tMin, unused: 0)
-        if (hasShadow) reinterpret_cast<float*>(&slot(pool.shadowD, out))[3] = asf(flags);
-        slot(pool.rng, out) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
-        slot(pool.throughput, out) = make_float4(T.x, T.y, T.z, thr.w);
-        slot(pool.li, out) = F3{L.x, L.y, L.z};
-        slot(pool.lsr, out) = F3{lsr.x, lsr.y, lsr.z};
+        if (terminate && !hasShadow) {
+            // The path ends here with no shadow ray pending: all CONTROL would still do is
+            // Li += light sampling result (0: the same bits as L + 0.0f) and WriteSample
+            // (RayTracingCommon.inc.hlsl:118-122), so both happen here and the slot goes
+            // idle at once (CONTROL reads nothing for it; no path state is stored)
+            const size_t p = slot(pool.pixel, out);
+            film.samplePosition[p] = slot(pool.pixelSample, out);
+            film.sampleValue[p] = make_float4(L.x + 0.0f, L.y + 0.0f, L.z + 0.0f, 0.0f);
+            if (film.debugRng) film.debugRng[p] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+            slot(pool.flags, out) = kFlagIdle;
+        } else {
+            slot(pool.flags, out) = flags;
+            // the shadow cast writes the path's flags with the occlusion bit (a plain store, no
+            // read of the flags in front of it): it takes them from shadowD.w (tMin, unused: 0)
+            if (hasShadow) reinterpret_cast<float*>(&slot(pool.shadowD, out))[3] = asf(flags);
+            slot(pool.rng, out) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+            slot(pool.throughput, out) = make_float4(T.x, T.y, T.z, thr.w);
+            slot(pool.li, out) = F3{L.x, L.y, L.z};
+            slot(pool.lsr, out) = F3{lsr.x, lsr.y, lsr.z};
+        }
     }
     DCRT_MCLK(5);
     uint32_t es, ss;

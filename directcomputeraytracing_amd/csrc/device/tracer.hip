@@ -734,7 +734,7 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     hipLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, pool, film, (const FrameConstants*)dFrame, cnt,
                        dGlobals, (uint32_t)(film.debugRng != nullptr));
     auto material = materialCaps == kCapOpaqueDelta ? material_kernel<kCapOpaqueDelta> : material_kernel<kCapAll>;
-    hipLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt);
+    hipLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt, film);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timed) {
         while (events.size() < eventsUsed + 2) {
