@@ -200,6 +200,14 @@ struct Film {
     uint32_t width, height, rowCount;
 };
 
+// Where MATERIAL writes the samples of the paths it ends (a device copy of the Film's
+// sample pointers: read only on that path, so they hold no SGPRs across the shading code)
+struct SampleOut {
+    float2* samplePosition;
+    float4* sampleValue;
+    uint4* debugRng;
+};
+
 // Pixel of lane `lane` in claimed block `block` of the batch: image, then 8-row group,
 // then 8-column block. False for lanes outside the film or past the last rendered row.
 DEV bool block_pixel(const FrameConstants& fc, const Film& film, uint32_t block, uint32_t lane, uint32_t* px, uint32_t* py,

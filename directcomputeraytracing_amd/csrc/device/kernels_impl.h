@@ -254,7 +254,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
 // kCapOpaqueDelta in dscene.h and dcrt_tracer::UploadScene).
 template <uint32_t CAPS>
 __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
-                                                                             Film film)
+                                                                             const SampleOut* sampleOut)
 {
     __shared__ uint32_t sm[64];
     QueueMapN<kMatShards> qm;
@@ -378,10 +378,11 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             // Li += light sampling result (0: the same bits as L + 0.0f) and WriteSample
             // (RayTracingCommon.inc.hlsl:118-122), so both happen here and the slot goes
             // idle at once (CONTROL reads nothing for it; no path state is stored)
-            const size_t p = slot(pool.pixel, out);
-            film.samplePosition[p] = slot(pool.pixelSample, out);
-            film.sampleValue[p] = make_float4(L.x + 0.0f, L.y + 0.0f, L.z + 0.0f, 0.0f);
-            if (film.debugRng) film.debugRng[p] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+            const uint32_t p = slot(pool.pixel, out);
+            const SampleOut so = *sampleOut;
+            slot(so.samplePosition, p) = slot(pool.pixelSample, out);
+            slot(so.sampleValue, p) = make_float4(L.x + 0.0f, L.y + 0.0f, L.z + 0.0f, 0.0f);
+            if (so.debugRng) slot(so.debugRng, p) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
             slot(pool.flags, out) = kFlagIdle;
         } else {
             slot(pool.flags, out) = flags;

@@ -159,6 +159,8 @@ struct dcrt_tracer {
     FrameConstants* dFrame = nullptr;
     Counters* dCounters = nullptr;     // [2]
     Globals* dGlobals = nullptr;
+    SampleOut* dSampleOut = nullptr;   // MATERIAL's copy of the sample pointers (EnsureSamples)
+    SampleOut hSampleOut = {};
     unsigned long long* dInstr = nullptr;   // [8]
     Counters* hCounters = nullptr;     // pinned [2]
 
@@ -303,6 +305,7 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.materialQueue, (size_t)pool.matCap * kMatShards, &poolAllocs));
     pool.size = poolSize;
     CHECKED(DeviceAlloc(&dFrame, 1, &poolAllocs));
+    CHECKED(DeviceAlloc(&dSampleOut, 1, &poolAllocs));
     CHECKED(DeviceAlloc(&dCounters, 2, &poolAllocs));
     CHECKED(DeviceAlloc(&dGlobals, 1, &poolAllocs));
     CHECKED(DeviceAlloc(&dInstr, 8, &poolAllocs));
@@ -576,6 +579,9 @@ int dcrt_tracer::EnsureSamples(uint32_t images)
     HIPCHECK(hipMemsetAsync(film.samplePosition, 0, n * sizeof(float2), stream));
     HIPCHECK(hipMemsetAsync(film.sampleValue, 0, n * sizeof(float4), stream));
     if (film.debugRng) HIPCHECK(hipMemsetAsync(film.debugRng, 0, n * sizeof(uint4), stream));
+    hSampleOut = SampleOut{film.samplePosition, film.sampleValue, film.debugRng};
+    HIPCHECK(hipMemcpyAsync(dSampleOut, &hSampleOut, sizeof(SampleOut), hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
     sampleImages = images;
     return DCRT_OK;
 }
@@ -734,7 +740,8 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     hipLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, pool, film, (const FrameConstants*)dFrame, cnt,
                        dGlobals, (uint32_t)(film.debugRng != nullptr));
     auto material = materialCaps == kCapOpaqueDelta ? material_kernel<kCapOpaqueDelta> : material_kernel<kCapAll>;
-    hipLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt, film);
+    hipLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
+                       (const SampleOut*)dSampleOut);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timed) {
         while (events.size() < eventsUsed + 2) {
