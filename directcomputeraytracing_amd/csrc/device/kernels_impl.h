@@ -1014,6 +1014,9 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
         const int x0 = (int)(tile % tilesX) * kFilmTile, y0 = (int)(tile / tilesX) * kFilmTile;
         const uint32_t px = (uint32_t)x0 + (threadIdx.x % kFilmTile), py = (uint32_t)y0 + (threadIdx.x / kFilmTile);
         const bool mine = px < W && py < H && !(film.rowOwned && !film.rowOwned[py]);
+        // a partitioned film's tiles without an owned pixel stage and convolve nothing
+        // (at N ranks that is (N-1)/N of the tiles)
+        if (film.rowOwned && !__syncthreads_or(mine)) continue;
         int xs = 0, xe = -1, ys = 0, ye = -1;
         float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (mine) {
