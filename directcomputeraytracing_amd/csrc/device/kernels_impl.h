@@ -267,8 +267,10 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
     const bool active = i < count;
-    bool terminate = false, hasShadow = false;
-    uint32_t path = 0;
+    bool terminate = false, hasShadow = false, ends = false;
+    uint32_t path = 0, pix = 0;
+    float2 pixSample = make_float2(0.0f, 0.0f);
+    float4 sample = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (active) {
         ++itemsDone;
         const uint32_t entry = qentry(pool.materialQueue, pool.matCap, qm, i);
@@ -373,16 +375,19 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             }
         }
         if (!hasShadow) flags = flags & ~kFlagShadowRayHit;
-        if (terminate && !hasShadow) {
+        ends = terminate && !hasShadow;
+        if (ends) {
             // The path ends here with no shadow ray pending: all CONTROL would still do is
             // Li += light sampling result (0: the same bits as L + 0.0f) and WriteSample
-            // (RayTracingCommon.inc.hlsl:118-122), so both happen here and the slot goes
-            // idle at once (CONTROL reads nothing for it; no path state is stored)
-            const uint32_t p = slot(pool.pixel, out);
+            // (RayTracingCommon.inc.hlsl:118-122), so both happen in this pass and the slot
+            // goes idle at once (CONTROL reads nothing for it; no path state is stored). The
+            // pixel is loaded here and the sample stored after the queue appends, whose
+            // atomic round trip hides the load.
+            pix = slot(pool.pixel, out);
+            pixSample = slot(pool.pixelSample, out);
+            sample = make_float4(L.x + 0.0f, L.y + 0.0f, L.z + 0.0f, 0.0f);
             const SampleOut so = *sampleOut;
-            slot(so.samplePosition, p) = slot(pool.pixelSample, out);
-            slot(so.sampleValue, p) = make_float4(L.x + 0.0f, L.y + 0.0f, L.z + 0.0f, 0.0f);
-            if (so.debugRng) slot(so.debugRng, p) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+            if (so.debugRng) slot(so.debugRng, pix) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
             slot(pool.flags, out) = kFlagIdle;
         } else {
             slot(pool.flags, out) = flags;
@@ -401,6 +406,11 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                   sm + (round & 1u) * 32u, &es, &ss);
     if (active && !terminate) slot(pool.extQueue, shard * pool.size + es) = path;
     if (active && hasShadow) slot(pool.shadowQueue, shard * pool.size + ss) = path;
+    if (ends) {
+        const SampleOut so = *sampleOut;
+        slot(so.samplePosition, pix) = pixSample;
+        slot(so.sampleValue, pix) = sample;
+    }
     DCRT_MCLK(6);
     ++round;
     }
