@@ -29,16 +29,17 @@ constexpr uint32_t kControlBlock = DCRT_CONTROL_BLOCK;  // CONTROL workgroup (th
 // iteration; eight words spread that over eight memory-side atomic units.
 constexpr uint32_t kShards = 8;
 constexpr uint32_t kShardStride = 64;                  // uint32 words (256 B)
-constexpr uint32_t kQExt = 0, kQShadow = 1, kQMaterial = 2, kQueues = 3;
-// Material-queue counter shards (CONTROL appends once per workgroup, only MATERIAL reads
-// the queue). 16 / 32 shards cut CONTROL by 10 % on one pipeline (178 -> 161 us) but the
-// two-pipeline bench lost 1.5-3 % (2.74-2.81 vs 2.79-2.85 ms/spp, tools/ab_libs.sh, three
-// passes): MATERIAL's longer shard-prefix lookup. Each shard holds matCap entries.
-#ifndef DCRT_MAT_SHARDS
-#define DCRT_MAT_SHARDS 8
+constexpr uint32_t kQExt = 0, kQShadow = 1, kQFinish = 2, kQueues = 3;
+// Finish-queue counter shards: MATERIAL lists the paths it ends with a shadow ray still
+// pending (the next CONTROL pass completes them). Each shard holds finCap entries.
+#ifndef DCRT_FIN_SHARDS
+#define DCRT_FIN_SHARDS 8
 #endif
-constexpr uint32_t kMatShards = DCRT_MAT_SHARDS;
-constexpr uint32_t kCounterWords = 2 * kShards + kMatShards;   // ext, shadow, then material shards
+constexpr uint32_t kFinShards = DCRT_FIN_SHARDS;
+constexpr uint32_t kCounterWords = 2 * kShards + kFinShards;   // ext, shadow, then finish shards
+// Extension-queue entry bit: the path's first MATERIAL pass follows (set by NEW_PATH), whose
+// Li, light sampling result and throughput are the NEW_PATH constants, not stored or loaded
+constexpr uint32_t kEntryFirst = 0x80000000u;
 
 struct Counters {        // one set per iteration parity
     uint32_t w[kCounterWords * kShardStride];
@@ -48,7 +49,9 @@ struct Globals {
     uint32_t totalBlocks;
     uint32_t stackOverflow;
     // device-side image sequencing (RenderImages): no host round trip between images
-    uint32_t imageComplete;   // SHADOW: this iteration's CONTROL found every path idle and nothing to claim
+    uint32_t imageComplete;   // SHADOW: every path idle after this iteration and nothing was claimed
+    uint32_t poolIdle;        // the same, ignoring `stopped` (Render's IsImageComplete)
+    uint32_t prevLive;        // paths live after the previous iteration (extension + finish queues)
     uint32_t stopped;         // all requested images are done: CONTROL claims nothing more
     uint32_t imagesDone, imageTarget, seedBase;
     uint32_t batchImages;     // images path-traced together in the current batch (image index in [0, batchImages))
@@ -181,11 +184,17 @@ struct PathPool {
     uint32_t* flags;
     float* extOpacity;         // ALLOW_ANYHIT_SHADER: g_ExtensionRayOpacitySamples
     float* shadowOpacity;      //                      g_ShadowRayOpacitySamples
-    uint32_t* extQueue;        // kShards x size entries each
+    // Queues (kShards x size entries each). The extension and finish queues alternate by
+    // iteration parity: `extQueue` / `finQueue` are this iteration's (appended to),
+    // `extPrev` / `finPrev` the previous iteration's (MATERIAL / CONTROL work lists);
+    // the host sets the four pointers per launch.
+    uint32_t* extQueue;
+    const uint32_t* extPrev;
     uint32_t* shadowQueue;
-    uint32_t* materialQueue;   // kMatShards x matCap entries
+    uint32_t* finQueue;        // kFinShards x finCap entries
+    const uint32_t* finPrev;
     uint32_t size;
-    uint32_t matCap;           // entries per material-queue shard
+    uint32_t finCap;           // entries per finish-queue shard
 };
 
 // Sample textures (m_SamplePositionTexture / m_SampleValueTexture) for every image of a

@@ -105,6 +105,8 @@ __global__ void set_idle_kernel(PathPool pool, Counters* counters, Globals* g, u
         g->batchImages = 1u;
         g->batchCap = 1u;
         g->imageComplete = 0u;
+        g->poolIdle = 0u;
+        g->prevLive = 0u;
         g->stopped = 0u;
         g->imagesDone = 0u;
         g->imageTarget = 1u;
@@ -150,59 +152,70 @@ __global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32
 }
 
 // ---- CONTROL (+ NEW_PATH) -------------------------------------------------------
+// Live paths never pass through CONTROL: MATERIAL takes them from the previous
+// iteration's extension queue and ends the paths it can (no shadow ray pending) itself.
+// CONTROL (1) completes the paths MATERIAL ended with a shadow ray pending (listed in
+// the previous iteration's finish queue): Li += light sampling result unless the shadow
+// ray hit (:520-528) and WriteSample; (2) while its shard has pixel blocks to hand out,
+// scans the slots for fully idle waves, which claim the next 8x8 block and start its
+// paths (NEW_PATH). With every block claimed (the batch's first pass claims all of
+// them) a pass is the finish list only, not a read of every slot's flags.
 __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, Film film, const FrameConstants* fc, Counters* cnt,
-                                                       Globals* g, uint32_t debugRng)
+                                                       const Counters* prev, Globals* g, uint32_t debugRng)
 {
     __shared__ uint32_t sm[64];
     if (g->stopped) return;                    // RenderImages finished: nothing live, nothing to claim
+    {
+        QueueMapN<kFinShards> fm;
+        qmap(prev, kQFinish, &fm);
+        const uint32_t nFin = fm.prefix[kFinShards];
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nFin; i += gridDim.x * blockDim.x) {
+            const uint32_t path = qentry(pool.finPrev, pool.finCap, fm, i);
+            const bool shadowHit = (slot(pool.flags, path) & kFlagShadowRayHit) != 0;
+            F3 li = slot(pool.li, path);
+            const F3 lsr = slot(pool.lsr, path);
+            li.x = li.x + (!shadowHit ? lsr.x : 0.0f);
+            li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
+            li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
+            const uint32_t p = slot(pool.pixel, path);
+            slot(film.samplePosition, p) = slot(pool.pixelSample, path);
+            slot(film.sampleValue, p) = make_float4(li.x, li.y, li.z, 0.0f);
+            if (debugRng) slot(film.debugRng, p) = slot(pool.rng, path);
+            // last, after stores that consumed the loads: another workgroup's scan may see the
+            // slot idle from here on and start a new path in it
+            slot(pool.flags, path) = kFlagIdle;
+        }
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t shard = blockIdx.x % kShards;
     uint32_t* cursor = &g->nextBlock[shard * kShardStride];
     // pixel blocks of this shard: shard, shard + kShards, ...
     const uint32_t shardBlocks = g->totalBlocks > shard ? (g->totalBlocks - shard + kShards - 1) / kShards : 0u;
     const bool staticFill = g->staticFill != 0u;   // (the grid then covers the pool exactly once)
+    if (!staticFill) {
+        // (one read for the workgroup: the scan below holds barriers, so the exit must be uniform)
+        __shared__ uint32_t exhausted;
+        if (threadIdx.x == 0) exhausted = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= shardBlocks;
+        __syncthreads();
+        if (exhausted) return;
+    }
     for (uint32_t base = blockIdx.x * blockDim.x; base < pool.size; base += gridDim.x * blockDim.x) {
     const uint32_t tid = base + threadIdx.x;
-    const uint32_t flags = pool.flags[tid];
-    bool idle = (flags & kFlagIdle) != 0;
-    const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
-    const bool terminate = (flags & kFlagTerminate) != 0;
-    uint32_t bounce = flags & 0xFFu;
-    // Li += light sampling result unless the shadow ray hit (:520-528). For a live path
-    // MATERIAL does this addition as its first step (same operands, same bits), so the
-    // path's Li is read and written once per iteration; the shadow-hit bit is carried.
-    if (!idle && terminate) {
-        F3 li = pool.li[tid];
-        const F3 lsr = pool.lsr[tid];
-        li.x = li.x + (!shadowHit ? lsr.x : 0.0f);
-        li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
-        li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
-        const size_t p = pool.pixel[tid];
-        film.samplePosition[p] = pool.pixelSample[tid];
-        film.sampleValue[p] = make_float4(li.x, li.y, li.z, 0.0f);
-        if (debugRng) film.debugRng[p] = pool.rng[tid];
-        idle = true;
-    }
-    const bool carryShadowHit = !idle && shadowHit;
-    // A fully idle wave claims the next 8x8 block (one atomic per workgroup, in the same
-    // barrier round as the material-queue append); at a batch start (all slots idle,
-    // cursors preset) wave j of the shard takes block j outright.
+    const bool idle = (pool.flags[tid] & kFlagIdle) != 0;
+    // A fully idle wave claims the next 8x8 block (one atomic per workgroup); at a batch
+    // start (all slots idle, cursors preset) wave j of the shard takes block j outright.
     const bool waveIdle = __ballot(!idle) == 0ull;
-    bool want = false;
-    if (!staticFill && waveIdle && lane == 0)
-        want = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shardBlocks;
-    uint32_t mslot, bslot;
-    const uint32_t mshard = blockIdx.x % kMatShards;
-    block_append2(!idle, qctr(cnt, kQMaterial, mshard), want, cursor, sm, &mslot, &bslot);
-    // (bit 31: the path's first MATERIAL pass, whose Li, light sampling result and
-    // throughput are the NEW_PATH constants and are not stored or loaded)
-    if (!idle) slot(pool.materialQueue, mshard * pool.matCap + mslot) = tid | (bounce == 0u ? 0x80000000u : 0u);
     uint32_t claimed = 0;
     bool got = false;
     if (staticFill) {
         claimed = (blockIdx.x / kShards) * (blockDim.x >> 6) + (threadIdx.x >> 6);
         got = waveIdle && claimed < shardBlocks;
     } else {
+        bool want = false;
+        if (waveIdle && lane == 0)
+            want = __hip_atomic_load(cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < shardBlocks;
+        uint32_t bslot, unused;
+        block_append2(false, cursor, want, cursor, sm, &unused, &bslot);
         claimed = (uint32_t)__shfl((int)bslot, 0, 64);
         got = __shfl((int)want, 0, 64) != 0 && claimed < shardBlocks;
     }
@@ -226,21 +239,16 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             pool.rayO[tid] = F3{o.x, o.y, o.z};
             pool.rayD[tid] = F3{d.x, d.y, d.z};
             // Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0 are implicit: the path's
-            // first MATERIAL pass takes them as constants (material-queue bit 31); isDelta =
-            // true: kFlagDelta below
+            // first MATERIAL pass takes them as constants (kEntryFirst); isDelta = true, bounce 0
+            pool.flags[tid] = kFlagDelta;
             newPath = true;
-            idle = false;
-            bounce = 0;
         }
     }
     // (the other half of sm: the next round's first append reuses the first half only
     // after every thread has passed this append's barriers)
     uint32_t eslot, unused;
     block_append2(newPath, qctr(cnt, kQExt, shard), false, qctr(cnt, kQExt, shard), sm + 32, &eslot, &unused);
-    if (newPath) pool.extQueue[(size_t)shard * pool.size + eslot] = tid;
-    const uint32_t delta = newPath ? kFlagDelta : (!idle ? flags & kFlagDelta : 0u);
-    const uint32_t newFlags = (idle ? kFlagIdle : 0u) | (carryShadowHit ? kFlagShadowRayHit : 0u) | delta | (bounce & 0xFFu);
-    if (newFlags != flags) pool.flags[tid] = newFlags;   // a live path's flags mostly stay as they are
+    if (newPath) pool.extQueue[(size_t)shard * pool.size + eslot] = tid | kEntryFirst;
     }
 }
 
@@ -254,13 +262,15 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
 // kCapOpaqueDelta in dscene.h and dcrt_tracer::UploadScene).
 template <uint32_t CAPS>
 __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
-                                                                             const SampleOut* sampleOut)
+                                                                             const Counters* prev, const SampleOut* sampleOut)
 {
     __shared__ uint32_t sm[64];
-    QueueMapN<kMatShards> qm;
-    qmap(cnt, kQMaterial, &qm);
-    const uint32_t count = qm.prefix[kMatShards];
+    // the work list: the previous iteration's extension queue (its rays have been cast)
+    QueueMap qm;
+    qmap(prev, kQExt, &qm);
+    const uint32_t count = qm.prefix[kShards];
     const uint32_t shard = blockIdx.x % kShards;
+    const uint32_t fshard = blockIdx.x % kFinShards;
     DCRT_MCLK_INIT;
     uint32_t itemsDone = 0;
     uint32_t round = 0;   // grid-stride round: alternates block_append2's sm halves
@@ -273,9 +283,9 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
     float4 sample = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (active) {
         ++itemsDone;
-        const uint32_t entry = qentry(pool.materialQueue, pool.matCap, qm, i);
-        path = entry & 0x7FFFFFFFu;
-        const bool first = (entry >> 31) != 0u;   // NEW_PATH's constants, not loaded
+        const uint32_t entry = qentry(pool.extPrev, pool.size, qm, i);
+        path = entry & ~kEntryFirst;
+        const bool first = (entry & kEntryFirst) != 0u;   // NEW_PATH's constants, not loaded
         const float4 h4 = slot(pool.hit, path);
         HitRecord hit;
         hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, path);
@@ -406,6 +416,18 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
                   sm + (round & 1u) * 32u, &es, &ss);
     if (active && !terminate) slot(pool.extQueue, shard * pool.size + es) = path;
     if (active && hasShadow) slot(pool.shadowQueue, shard * pool.size + ss) = path;
+    {
+        // paths ended with a shadow ray pending: the next CONTROL pass completes them (rare
+        // enough for one atomic per wave that has any)
+        const bool fin = active && terminate && hasShadow;
+        const unsigned long long fm = __ballot(fin);
+        if (fm != 0ull) {
+            uint32_t fb = 0;
+            if ((threadIdx.x & 63u) == 0) fb = atomicAdd(qctr(cnt, kQFinish, fshard), (uint32_t)__popcll(fm));
+            fb = (uint32_t)__shfl((int)fb, 0, 64) + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+            if (fin) slot(pool.finQueue, fshard * pool.finCap + fb) = path;
+        }
+    }
     if (ends) {
         const SampleOut so = *sampleOut;
         slot(so.samplePosition, pix) = pixSample;
@@ -615,7 +637,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
     TraversalStats st = {};
     persistent_trace<false, INSTR, OPACITY>(
         sc, qm.prefix[kShards], fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
-        [&](uint32_t i) __attribute__((always_inline)) { return qentry(pool.extQueue, pool.size, qm, i); },
+        [&](uint32_t i) __attribute__((always_inline)) { return qentry(pool.extQueue, pool.size, qm, i) & ~kEntryFirst; },
         [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
             const F3 o = pool.rayO[path], d = pool.rayD[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf());
@@ -636,15 +658,20 @@ __device__ __forceinline__ void end_iteration(const Counters* cnt, Counters* nex
 {
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
-            uint32_t material = 0;
-            for (uint32_t sh = 0; sh < kMatShards; ++sh) material += qctr_load(cnt, kQMaterial, sh);
+            uint32_t fin = 0;
+            for (uint32_t sh = 0; sh < kFinShards; ++sh) fin += qctr_load(cnt, kQFinish, sh);
             const uint32_t ext = qtotal(cnt, kQExt);
             g->extRays += ext;
             g->shadowRays += shadowRays;
             g->iterations += 1ull;
             g->staticFill = 0u;   // only a batch's first CONTROL pass claims statically
-            // IsImageComplete (WavefrontPathTracer.cpp:508-523), exact and on the device
-            g->imageComplete = (material == 0u && ext == 0u && !g->stopped) ? 1u : 0u;
+            // IsImageComplete (WavefrontPathTracer.cpp:508-523), exact and on the device: no
+            // path was live entering this iteration (so CONTROL's scan saw every slot idle)
+            // and none was started
+            const bool idle = g->prevLive == 0u && ext == 0u;
+            g->poolIdle = idle ? 1u : 0u;
+            g->imageComplete = (idle && !g->stopped) ? 1u : 0u;
+            g->prevLive = ext + fin;
         }
         if (threadIdx.x < kCounterWords) nextCnt->w[threadIdx.x * kShardStride] = 0u;
     }
@@ -708,7 +735,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
             const bool shadow = i >= nExt;
-            return qentry(shadow ? shQueue : extQueue, pool.size, shadow ? qs : qe, shadow ? i - nExt : i);
+            return qentry(shadow ? shQueue : extQueue, pool.size, shadow ? qs : qe, shadow ? i - nExt : i) & ~kEntryFirst;
         },
         [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
             const bool shadow = i >= nExt;

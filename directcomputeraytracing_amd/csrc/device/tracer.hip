@@ -134,7 +134,9 @@ struct dcrt_tracer {
     uint64_t imagesCompleted = 0;                // since the last ResetStats (counters())
 
     std::vector<void*> poolAllocs, sceneAllocs, filmAllocs, sampleAllocs, rowAllocs;
-    PathPool pool{};
+    PathPool pool{};                   // (queue pointers set per launch: LaunchIteration)
+    uint32_t* extQueues = nullptr;     // 2 parities x kShards x poolSize
+    uint32_t* finQueues = nullptr;     // 2 parities x kFinShards x pool.finCap
     DeviceScene scene{};
     bool hasScene = false;
     uint32_t castBlock = 256;
@@ -294,15 +296,17 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.extOpacity, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowOpacity, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.extQueue, (size_t)P * kShards, &poolAllocs));
+    // the extension and finish queues: one per iteration parity (extQueues / finQueues)
+    CHECKED(DeviceAlloc(&extQueues, (size_t)P * kShards * 2, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowQueue, (size_t)P * kShards, &poolAllocs));
     {
-        // CONTROL workgroup b appends its live slots to material shard b % kMatShards
-        const uint64_t G = std::min<uint32_t>(poolSize / kControlBlock, kControlMaxBlocks);
-        const uint64_t rounds = (P + G * kControlBlock - 1) / (G * kControlBlock);
-        pool.matCap = (uint32_t)(((G + kMatShards - 1) / kMatShards) * rounds * kControlBlock);
+        // MATERIAL workgroup b appends the paths it ends with a shadow ray pending to finish
+        // shard b % kFinShards
+        const uint64_t G = std::min<uint32_t>((poolSize + kMaterialBlock - 1) / kMaterialBlock, kMaterialMaxBlocks);
+        const uint64_t rounds = (P + G * kMaterialBlock - 1) / (G * kMaterialBlock);
+        pool.finCap = (uint32_t)(((G + kFinShards - 1) / kFinShards) * rounds * kMaterialBlock);
     }
-    CHECKED(DeviceAlloc(&pool.materialQueue, (size_t)pool.matCap * kMatShards, &poolAllocs));
+    CHECKED(DeviceAlloc(&finQueues, (size_t)pool.finCap * kFinShards * 2, &poolAllocs));
     pool.size = poolSize;
     CHECKED(DeviceAlloc(&dFrame, 1, &poolAllocs));
     CHECKED(DeviceAlloc(&dSampleOut, 1, &poolAllocs));
@@ -729,7 +733,12 @@ int dcrt_tracer::BeginImage()
 int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
 {
     Counters* cnt = dCounters + par;
-    Counters* next = dCounters + (par ^ 1u);
+    Counters* next = dCounters + (par ^ 1u);   // (the previous iteration's; the casts clear them for the next)
+    PathPool pool = this->pool;
+    pool.extQueue = extQueues + (size_t)par * kShards * poolSize;
+    pool.extPrev = extQueues + (size_t)(par ^ 1u) * kShards * poolSize;
+    pool.finQueue = finQueues + (size_t)par * kFinShards * pool.finCap;
+    pool.finPrev = finQueues + (size_t)(par ^ 1u) * kFinShards * pool.finCap;
     // CONTROL and MATERIAL get one workgroup per 256 slots (their grid-stride loops then run
     // once): the hardware dispatcher balances them, where a capped grid leaves a partial
     // second round of workgroups (occupancy 7 and 3 waves/SIMD, not 8) as a tail.
@@ -738,10 +747,10 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     const bool opacity = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) != 0;
     const uint32_t castGrid = CastGrid(castBlock, opacity);
     hipLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, pool, film, (const FrameConstants*)dFrame, cnt,
-                       dGlobals, (uint32_t)(film.debugRng != nullptr));
+                       (const Counters*)next, dGlobals, (uint32_t)(film.debugRng != nullptr));
     auto material = materialCaps == kCapOpaqueDelta ? material_kernel<kCapOpaqueDelta> : material_kernel<kCapAll>;
     hipLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
-                       (const SampleOut*)dSampleOut);
+                       (const Counters*)next, (const SampleOut*)dSampleOut);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timed) {
         while (events.size() < eventsUsed + 2) {
@@ -838,17 +847,14 @@ int dcrt_tracer::RunIterations(uint32_t n)
     return DCRT_OK;
 }
 
-// IsImageComplete (WavefrontPathTracer.cpp:508-523): the material and new-path
-// queues of the last CONTROL pass were both empty. Here exact, not 2 frames late.
+// IsImageComplete (WavefrontPathTracer.cpp:508-523): no path was live entering the last
+// iteration and none was started (Globals::poolIdle). Here exact, not 2 frames late.
 int dcrt_tracer::ReadCompletion(bool* complete)
 {
-    const uint32_t last = parity ^ 1u;
-    HIPCHECK(hipMemcpyAsync(hCounters, dCounters + last, sizeof(Counters), hipMemcpyDeviceToHost, stream));
+    uint32_t* h = (uint32_t*)hCounters;   // (pinned staging)
+    HIPCHECK(hipMemcpyAsync(h, &dGlobals->poolIdle, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipStreamSynchronize(stream));
-    uint32_t material = 0, ext = 0;
-    for (uint32_t sh = 0; sh < kMatShards; ++sh) material += hCounters->w[(kQMaterial * kShards + sh) * kShardStride];
-    for (uint32_t sh = 0; sh < kShards; ++sh) ext += hCounters->w[(kQExt * kShards + sh) * kShardStride];
-    *complete = material == 0 && ext == 0;
+    *complete = *h != 0;
     return DCRT_OK;
 }
 
