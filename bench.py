@@ -34,6 +34,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, /opt/skills/guides/MI355X_MICROAR
 EXT_RAY_BYTES = 4 + 32 + 20    # queue index + SRay + SRayHit
 NODE_BYTES, TRI_BYTES, BLAS_BYTES = 32, 48, 56
 SHADOW_RAY_BYTES = 4 + 32 + 4 + 4
+CONTROL_BYTES, MATERIAL_BYTES, NEW_PATH_BYTES = 92, 600, 88   # per path-iteration / new path
+FILM_BYTES_BASE, FILM_BYTES_PER_TAP = 32, 24                  # SampleConvolution: 24 B per window tap + 32
 
 
 def parse():
@@ -306,6 +308,15 @@ def main():
     # measured HBM traffic of the same cast launches: a committed rocprofv3 PMC summary of
     # THIS workload (tools/profile.sh + tools/pmc_traffic.py record the workload they profiled),
     # never a profile of another image count, pool or scene
+    # whole-pipeline roofline ("and for the whole pipeline"): the reference's
+    # algorithmic bytes of every stage for the timed images (cast terms as above, CONTROL +
+    # MATERIAL per path-iteration = per extension ray, NEW_PATH per new path, the film pass
+    # per pixel x image), from the roofline leg's counts of the same images, over the timed
+    # region's wall time (max over ranks), per GPU
+    film_bytes = FILM_BYTES_BASE + FILM_BYTES_PER_TAP * (2 * int(filt.radius + 0.5) + 1) ** 2
+    pipe_bytes_R = (ext_bytes + shadow_bytes + (CONTROL_BYTES + MATERIAL_BYTES) * cr["extension_rays"]
+                    + NEW_PATH_BYTES * cr["new_paths"] + film_bytes * args.width * args.height * R / world)
+    pipe_achieved = pipe_bytes_R * (images / R) / elapsed / 1e9
     workload_key = {"config": args.config, "resolution": [args.width, args.height], "images": R,
                     "path_pool": args.pool, "world": world}
     traffic, traffic_src = None, "no committed PMC profile of this workload"
@@ -364,6 +375,12 @@ def main():
                      "per_shadow_ray": {"nodes": st["shadow_node_visits"] / max(1, cr["shadow_rays"]),
                                         "tris": st["shadow_triangle_tests"] / max(1, cr["shadow_rays"]),
                                         "blas": st["shadow_blas_entries"] / max(1, cr["shadow_rays"])}},
+        "pipeline_roofline": {"bound": "hbm", "achieved": round(pipe_achieved, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(pipe_achieved / HBM_PEAK_GBS, 4),
+                              "bytes_per_spp": int(pipe_bytes_R / R),
+                              "basis": "per GPU: algorithmic bytes of cast + CONTROL (92 B) + MATERIAL (600 B) per "
+                                       "path-iteration + NEW_PATH (88 B) per new path + film pass per pixel-image "
+                                       "(SURVEY 8(d)) over the timed region's wall time"},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
