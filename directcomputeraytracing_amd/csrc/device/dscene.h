@@ -202,7 +202,9 @@ DEV bool tri_watertight(V3 o, const Shear& sh, float tMin, float tMax, V3 v0, V3
     *t = tScaled * invDet;
     *u = e1 * invDet;
     *v = e2 * invDet;
-    *backface = (fsign(sh.sz) * det) < 0.0f;
+    // fsign(sz) * det < 0 (the reference's form) as a sign-bit test: the two differ only
+    // for det = +-0 or NaN, where the test below rejects the hit and `backface` is unused
+    *backface = sh.sz != 0.0f && (int)(asu(sh.sz) ^ asu(det)) < 0;
     return det != 0.0f && *t >= tMin && *t < tMax;
 }
 
@@ -212,7 +214,8 @@ DEV bool tri_watertight_rot(const Shear& sh, float tMin, float tMax, float4 q0, 
                             float* t, float* u, float* v, bool* backface)
 {
     *t = 0.0f; *u = 0.0f; *v = 0.0f; *backface = false;
-    if (q0.w != 0.0f) return false;   // degenerate
+    // (the degenerate flag q0.w is tested with the edge signs below, not first: an early
+    // exit on it made the three vertex reads wait for a separate read of q0.w)
     float p0x = q0.x - sh.ox, p0y = q0.y - sh.oy, p0z = q0.z - sh.oz;
     float p1x = q1.x - sh.ox, p1y = q1.y - sh.oy, p1z = q1.z - sh.oz;
     float p2x = q2.x - sh.ox, p2y = q2.y - sh.oy, p2z = q2.z - sh.oz;
@@ -222,7 +225,7 @@ DEV bool tri_watertight_rot(const Shear& sh, float tMin, float tMax, float4 q0, 
     const float e0 = p1x * p2y - p2x * p1y;
     const float e1 = p2x * p0y - p0x * p2y;
     const float e2 = p0x * p1y - p1x * p0y;
-    if ((e0 < 0.0f || e1 < 0.0f || e2 < 0.0f) && (e0 > 0.0f || e1 > 0.0f || e2 > 0.0f)) return false;
+    if (q0.w != 0.0f || ((e0 < 0.0f || e1 < 0.0f || e2 < 0.0f) && (e0 > 0.0f || e1 > 0.0f || e2 > 0.0f))) return false;
     const float det = e0 + e1 + e2;
     p0z = p0z * sh.sz; p1z = p1z * sh.sz; p2z = p2z * sh.sz;
     const float tScaled = e0 * p0z + e1 * p1z + e2 * p2z;
@@ -230,7 +233,9 @@ DEV bool tri_watertight_rot(const Shear& sh, float tMin, float tMax, float4 q0, 
     *t = tScaled * invDet;
     *u = e1 * invDet;
     *v = e2 * invDet;
-    *backface = (fsign(sh.sz) * det) < 0.0f;
+    // fsign(sz) * det < 0 (the reference's form) as a sign-bit test: the two differ only
+    // for det = +-0 or NaN, where the test below rejects the hit and `backface` is unused
+    *backface = sh.sz != 0.0f && (int)(asu(sh.sz) ^ asu(det)) < 0;
     return det != 0.0f && *t >= tMin && *t < tMax;
 }
 
@@ -513,12 +518,18 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         if (INSTR) ++st.tris;
         float t, u, v; bool bf, h;
         if (ALL_CACHED && watertight) {
-            const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u + p * kRotTriFloat4 + (uint32_t)s.sh.kz * 3u;
-            h = tri_watertight_rot(s.sh, s.tMin, s.tMax, c[0], c[1], c[2], &t, &u, &v, &bf);
+            // (24-bit multiply: a full-rate v_mul_u32_u24 instead of the quarter-rate v_mul_lo_u32)
+            const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u +
+                              __umul24(p, kRotTriFloat4) + __umul24((uint32_t)s.sh.kz, 3u);
+            const float4 q0 = c[0], q1 = c[1], q2 = c[2];
+            // all three vertex reads issued before the degenerate / edge-sign exit (one LDS
+            // round trip, not a read of q0 first and of q1, q2 behind the branch)
+            asm volatile("" :: "v"(q0.w), "v"(q1.x), "v"(q2.x));
+            h = tri_watertight_rot(s.sh, s.tMin, s.tMax, q0, q1, q2, &t, &u, &v, &bf);
         } else {
             float4 q0, q1, q2;
             if (ALL_CACHED) {
-                const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u + p * kRotTriFloat4 + 6u;
+                const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u + __umul24(p, kRotTriFloat4) + 6u;
                 q0 = c[0]; q1 = c[1]; q2 = c[2];   // permutation z = 2 is the identity
             } else if (p < sc.cachedTris) {
                 const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u;

@@ -281,6 +281,8 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
     uint32_t path = 0, pix = 0;
     float2 pixSample = make_float2(0.0f, 0.0f);
     float4 sample = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float2* outPos = nullptr;
+    float4* outVal = nullptr;
     if (active) {
         ++itemsDone;
         const uint32_t entry = qentry(pool.extPrev, pool.size, qm, i);
@@ -396,7 +398,11 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
             pix = slot(pool.pixel, out);
             pixSample = slot(pool.pixelSample, out);
             sample = make_float4(L.x + 0.0f, L.y + 0.0f, L.z + 0.0f, 0.0f);
+            // the sample pointers are read here too, not after the appends: read there (behind
+            // the barriers and the atomic) they were one more round trip at the wave's end
             const SampleOut so = *sampleOut;
+            outPos = so.samplePosition;
+            outVal = so.sampleValue;
             if (so.debugRng) slot(so.debugRng, pix) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
             slot(pool.flags, out) = kFlagIdle;
         } else {
@@ -429,9 +435,8 @@ __global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(P
         }
     }
     if (ends) {
-        const SampleOut so = *sampleOut;
-        slot(so.samplePosition, pix) = pixSample;
-        slot(so.sampleValue, pix) = sample;
+        slot(outPos, pix) = pixSample;
+        slot(outVal, pix) = sample;
     }
     DCRT_MCLK(6);
     ++round;
