@@ -143,7 +143,7 @@ def main():
         workload = f"{desc}, {{spp}} spp ({world} spp/step, film stripes across {world} GPU(s)), wavefront"
     args.pool = args.pool or scenes.default_pool(args.width, args.height)
     filt = scene.filter_params()
-    from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
+    from directcomputeraytracing_amd.partition import halo_for_radius, pipeline_pool, render_rows, stream_partition
     halo = max(1, halo_for_radius(filt.radius, args.height))
 
     def make_tracer(pool, part):
@@ -162,7 +162,10 @@ def main():
     tracers = []
     for s_ in range(K):
         part = stream_partition(args.height, world, rank, K, s_, args.stripe) if (K > 1 or world > 1) else None
-        tracers.append(make_tracer(args.pool // K, part))
+        # (a pool just short of a whole number of batches grows by <= 5 %: one drain less)
+        rows = len(render_rows(args.height, *part, halo)) if part is not None else args.height
+        pool = pipeline_pool(args.pool // K, rows, args.width, args.steps * world) if not args.image_batch else args.pool // K
+        tracers.append(make_tracer(pool, part))
     tracer = tracers[0]
 
     def render_all(first, count):

@@ -423,9 +423,9 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     const bool hit = ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a, b);
     const uint32_t misc = asu(b.w);
     const uint32_t right = asu(b.z);
-    // leaf: TLAS-leaf bit (4) or a primitive count (bits 3 and up)
-    const bool leaf = misc > 3u;
-    const bool descend = hit && !leaf;
+    // leaf: TLAS-leaf bit (4) or a primitive count (bits 3 and up); parked = hit && leaf
+    // is formed as hit ^ descend below (a mask operation, not a second compare of misc)
+    const bool descend = hit & (misc < 4u);
     // near/far by the split axis' direction sign (one bit of the space's sign mask);
     // children keep the BLAS bit of the packed node reference
     // (v_bfe takes its offset from the low 5 bits of misc: the split axis for an interior
@@ -457,7 +457,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
         s.negMask = neg_mask(s.d, s.negMask);
     }
-    s.parked = hit && leaf;
+    s.parked = hit ^ descend;
     if (!ALL_CACHED) {   // (ALL_CACHED: phase B reads them from the LDS copy of the node)
         s.leafRef = right;
         s.leafMisc = misc;

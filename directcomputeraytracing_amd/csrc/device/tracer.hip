@@ -601,7 +601,9 @@ uint32_t dcrt_tracer::AutoBatch(uint32_t count) const
 {
     uint32_t b = batchImages;
     if (b == 0) {
-        const uint64_t pixels = std::max<uint64_t>(1, (uint64_t)rowCount * filmW);
+        // the slots an image takes: whole 8x8 pixel blocks (a wave each), partial bands and
+        // columns included, so a batch that "fits" never waits for slots to free up
+        const uint64_t pixels = std::max<uint64_t>(1, (uint64_t)bandCount * kBlockH * ((filmW + kBlockW - 1) / kBlockW) * kBlockW);
         b = (uint32_t)std::min<uint64_t>(kMaxImageBatch, std::max<uint64_t>(1, poolSize / pixels));
         // equal batches: as many batches as the cap needs, each as large as the others (a
         // small last batch would pay a whole drain for a sparse wavefront)

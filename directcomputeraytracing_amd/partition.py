@@ -60,6 +60,21 @@ def stream_partition(height: int, world_size: int, rank: int, streams: int, stre
     return v, stream * world_size + rank, max(1, round(height / (v * k)))
 
 
+def pipeline_pool(pool: int, rows: int, width: int, images: int, max_batch: int = 64, slack: float = 0.08) -> int:
+    """Path-pool slots for one pipeline rendering `images` images of `rows` x `width` pixels.
+
+    dcrt_tracer::AutoBatch cuts a render into equal batches of as many images as the pool
+    holds (at most `max_batch`), and every batch ends in a drain. When the pool falls just
+    short of a whole number of batches (an N = 8 rank's stripes plus halo: 62.4 shares of a
+    2^23 pool, i.e. 5 batches of 256 shares instead of 4) the pool grows by up to `slack`
+    so the render needs one batch less; otherwise it is returned unchanged. An image takes
+    whole 8x8 pixel blocks of slots (partial bands and columns included), as AutoBatch counts."""
+    px = max(1, -(-rows // BLOCK_H) * BLOCK_H * -(-width // 8) * 8)
+    batches = max(-(-images // max_batch), -(-int(images * px) // int(pool * (1.0 + slack))))
+    need = -(-images // batches) * px
+    return max(pool, -(-need // 256) * 256)
+
+
 def halo_for_radius(radius: float, height: int = 65535) -> int:
     """Rows of support beyond a pixel row that SampleConvolution gathers (SampleConvolution.hlsl:77-81),
     in the kernel's float32 arithmetic over the film's rows (dcrt_tracer FilterSupportRows): floor(r + 0.5),
