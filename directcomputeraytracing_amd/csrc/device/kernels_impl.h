@@ -253,6 +253,9 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
 }
 
 // ---- MATERIAL -----------------------------------------------------------------------
+#ifndef DCRT_MATERIAL_BLOCK
+#define DCRT_MATERIAL_BLOCK 256
+#endif
 #ifdef DCRT_MATERIAL_WAVES_PER_EU
 #define DCRT_MATERIAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(DCRT_MATERIAL_WAVES_PER_EU, 8)))
 #else
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
 // CAPS: the scene capabilities this variant is compiled for (kCapAll = any scene; see
 // kCapOpaqueDelta in dscene.h and dcrt_tracer::UploadScene).
 template <uint32_t CAPS>
-__global__ __launch_bounds__(256) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
+__global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
                                                                              const Counters* prev, const SampleOut* sampleOut)
 {
     __shared__ uint32_t sm[64];

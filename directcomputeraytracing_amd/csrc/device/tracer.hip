@@ -45,7 +45,10 @@ namespace {
 constexpr uint32_t kDefaultPoolSize = 1u << 20;      // 2^20 slots: 16 waves x 256 CUs x 256 (MI355X)
 constexpr uint32_t kDefaultIterations = 8;
 constexpr uint32_t kMaxImageBatch = 64;               // images in flight per RenderImages batch (sample textures: 24 B/px each)
-constexpr uint32_t kMaterialBlock = 256;
+#ifndef DCRT_MATERIAL_BLOCK
+#define DCRT_MATERIAL_BLOCK 256
+#endif
+constexpr uint32_t kMaterialBlock = DCRT_MATERIAL_BLOCK;   // MATERIAL workgroup (one queue-append atomic each)
 constexpr uint32_t kMaxPersistentBlocks = 256 * 8;   // CUs x resident workgroups
 #ifndef DCRT_CONTROL_MAX_BLOCKS
 #define DCRT_CONTROL_MAX_BLOCKS 0xFFFFFFFFu
