@@ -76,6 +76,34 @@ def test_stream_partition_covers_film_once():
                 assert cover.min() == 1 and cover.max() == 1
 
 
+def test_pipeline_pool_sizes_whole_batches():
+    """bench.py's per-pipeline pool: unchanged at N = 1 (8 half-film shares fit 2^23
+    slots), grown by at most 8 % where that saves a batch (N = 2 / 4 / 8 ranks' stripes
+    plus halo at 8x8-block granularity), and the grown pool holds whole batches."""
+    from directcomputeraytracing_amd.partition import pipeline_pool, render_rows, stream_partition
+    W, H, base = 1920, 1080, 1 << 23
+
+    def slots(rows):   # AutoBatch: whole 8x8 blocks
+        return -(-rows // 8) * 8 * -(-W // 8) * 8
+
+    for world in (1, 2, 4, 8):
+        images = 64 * world
+        for s in (0, 1):
+            w, v, sh = stream_partition(H, world, 0, 2, s, 64)
+            rows = len(render_rows(H, w, v, sh, 1))
+            pool = pipeline_pool(base, rows, W, images)
+            assert base <= pool <= base * 1.08 and pool % 256 == 0
+            per = slots(rows)
+            batch = min(64, pool // per)
+            batches = -(-images // batch)
+            assert batches <= -(-images // min(64, base // per))          # never more batches
+            assert -(-images // batches) * per <= pool                     # equal batches fit
+            if world == 1:
+                assert pool == base
+            if world == 8:
+                assert batches == images // 64                             # 4 batches of 64, not 5
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
