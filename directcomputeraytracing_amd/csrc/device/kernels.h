@@ -168,6 +168,16 @@ DEV T& slot(T* base, uint32_t i)
     return *(T*)((char*)base + (uint64_t)(i * (uint32_t)sizeof(T)));
 }
 
+// The state only CONTROL and MATERIAL touch, one 64-B record per slot (one whole 64-B
+// memory sector per path instead of a 12- or 16-B piece of four arrays' sectors):
+// xoshiro state, throughput + bsdfPdf, Li and the light sampling result.
+struct PathState {
+    uint4 rng;
+    float4 thr;      // T.xyz, bsdfPdf
+    float4 liLsr;    // Li.xyz (isDelta: kFlagDelta in flags), lsr.x
+    float4 lsr2;     // lsr.y, lsr.z, -, -
+};
+
 struct PathPool {
     F3* rayO;            // extension ray origin (tMax = inf, tMin = 0 implicit); size + 1 entries
     F3* rayD;            // extension ray direction; size + 1 entries (the cast kernel's 16-B reads)
@@ -177,10 +187,7 @@ struct PathPool {
     float4* shadowD;
     uint32_t* pixel;     // sample index: image * W*H + y * W + x
     float2* pixelSample;
-    uint4* rng;
-    F3* lsr;             // light sampling result
-    float4* throughput;  // T.xyz, bsdfPdf
-    F3* li;              // Li (isDelta: kFlagDelta in flags)
+    PathState* state;    // rng, throughput, Li, light sampling result
     uint32_t* flags;
     float* extOpacity;         // ALLOW_ANYHIT_SHADER: g_ExtensionRayOpacitySamples
     float* shadowOpacity;      //                      g_ShadowRayOpacitySamples

@@ -172,15 +172,17 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nFin; i += gridDim.x * blockDim.x) {
             const uint32_t path = qentry(pool.finPrev, pool.finCap, fm, i);
             const bool shadowHit = (slot(pool.flags, path) & kFlagShadowRayHit) != 0;
-            F3 li = slot(pool.li, path);
-            const F3 lsr = slot(pool.lsr, path);
+            const PathState& ps = slot(pool.state, path);
+            const float4 l4 = ps.liLsr, l2 = ps.lsr2;
+            F3 li{l4.x, l4.y, l4.z};
+            const F3 lsr{l4.w, l2.x, l2.y};
             li.x = li.x + (!shadowHit ? lsr.x : 0.0f);
             li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
             li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
             const uint32_t p = slot(pool.pixel, path);
             slot(film.samplePosition, p) = slot(pool.pixelSample, path);
             slot(film.sampleValue, p) = make_float4(li.x, li.y, li.z, 0.0f);
-            if (debugRng) slot(film.debugRng, p) = slot(pool.rng, path);
+            if (debugRng) slot(film.debugRng, p) = ps.rng;
             // last, after stores that consumed the loads: another workgroup's scan may see the
             // slot idle from here on and start a new path in it
             slot(pool.flags, path) = kFlagIdle;
@@ -235,11 +237,12 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) pool.extOpacity[tid] = next1(rng);   // :223-226
             pool.pixel[tid] = image * (film.width * film.height) + py * film.width + px;
             pool.pixelSample[tid] = make_float2(psx, psy);
-            pool.rng[tid] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+            slot(pool.state, tid).rng = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
             pool.rayO[tid] = F3{o.x, o.y, o.z};
             pool.rayD[tid] = F3{d.x, d.y, d.z};
             // Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0 are implicit: the path's
             // first MATERIAL pass takes them as constants (kEntryFirst); isDelta = true, bounce 0
+            // (writing them into the state record too measured the same: 2.687 vs 2.682 ms/spp)
             pool.flags[tid] = kFlagDelta;
             newPath = true;
         }
@@ -296,14 +299,17 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, path);
         const F3 rd = slot(pool.rayD, path);
         const V3 dir = mk(rd.x, rd.y, rd.z);
-        const uint4 r4 = slot(pool.rng, path);
+        const PathState& ps = slot(pool.state, path);
+        const uint4 r4 = ps.rng;
         Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
-        float4 thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : slot(pool.throughput, path);
-        F3 li = first ? F3{0.0f, 0.0f, 0.0f} : slot(pool.li, path);
+        float4 thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : ps.thr;
+        const float4 l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ps.liLsr;
+        const float4 l2 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ps.lsr2;
+        F3 li{l4.x, l4.y, l4.z};
         uint32_t flags = slot(pool.flags, path);
         {
             // CONTROL's Li += light sampling result (:520-528), done here for live paths
-            const F3 lsr0 = first ? F3{0.0f, 0.0f, 0.0f} : slot(pool.lsr, path);
+            const F3 lsr0{l4.w, l2.x, l2.y};
             const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
             li.x = li.x + (!shadowHit ? lsr0.x : 0.0f);
             li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
@@ -413,10 +419,11 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
             // the shadow cast writes the path's flags with the occlusion bit (a plain store, no
             // read of the flags in front of it): it takes them from shadowD.w (tMin, unused: 0)
             if (hasShadow) reinterpret_cast<float*>(&slot(pool.shadowD, out))[3] = asf(flags);
-            slot(pool.rng, out) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
-            slot(pool.throughput, out) = make_float4(T.x, T.y, T.z, thr.w);
-            slot(pool.li, out) = F3{L.x, L.y, L.z};
-            slot(pool.lsr, out) = F3{lsr.x, lsr.y, lsr.z};
+            PathState& po = slot(pool.state, out);
+            po.rng = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+            po.thr = make_float4(T.x, T.y, T.z, thr.w);
+            po.liLsr = make_float4(L.x, L.y, L.z, lsr.x);
+            po.lsr2 = make_float4(lsr.y, lsr.z, 0.0f, 0.0f);
         }
     }
     DCRT_MCLK(5);

@@ -292,10 +292,7 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.shadowD, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.pixel, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.pixelSample, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.rng, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.lsr, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.throughput, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.li, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.state, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.extOpacity, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowOpacity, P, &poolAllocs));
