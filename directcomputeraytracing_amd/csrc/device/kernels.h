@@ -188,6 +188,8 @@ struct PathPool {
     uint32_t* pixel;     // sample index: image * W*H + y * W + x
     float2* pixelSample;
     PathState* state;    // rng, throughput, Li, light sampling result
+    uint4* rngNew;       // a new path's rng, as CONTROL wrote it (dense 16-B writes; its
+                         // first MATERIAL pass reads it here, later passes from `state`)
     uint32_t* flags;
     float* extOpacity;         // ALLOW_ANYHIT_SHADER: g_ExtensionRayOpacitySamples
     float* shadowOpacity;      //                      g_ShadowRayOpacitySamples

@@ -237,7 +237,9 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) pool.extOpacity[tid] = next1(rng);   // :223-226
             pool.pixel[tid] = image * (film.width * film.height) + py * film.width + px;
             pool.pixelSample[tid] = make_float2(psx, psy);
-            slot(pool.state, tid).rng = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+            // (into its own dense array: a 16-B piece of each 64-B state record was a partly
+            // written sector per path)
+            pool.rngNew[tid] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
             pool.rayO[tid] = F3{o.x, o.y, o.z};
             pool.rayD[tid] = F3{d.x, d.y, d.z};
             // Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0 are implicit: the path's
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         const F3 rd = slot(pool.rayD, path);
         const V3 dir = mk(rd.x, rd.y, rd.z);
         const PathState& ps = slot(pool.state, path);
-        const uint4 r4 = ps.rng;
+        const uint4 r4 = first ? slot(pool.rngNew, path) : ps.rng;
         Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
         float4 thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : ps.thr;
         const float4 l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ps.liLsr;

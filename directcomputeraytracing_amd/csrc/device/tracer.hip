@@ -293,6 +293,7 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.pixel, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.pixelSample, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.state, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.rngNew, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.extOpacity, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowOpacity, P, &poolAllocs));
