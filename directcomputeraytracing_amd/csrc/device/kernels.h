@@ -181,6 +181,10 @@ struct PathState {
 struct PathPool {
     F3* rayO;            // extension ray origin (tMax = inf, tMin = 0 implicit); size + 1 entries
     F3* rayD;            // extension ray direction; size + 1 entries (the cast kernel's 16-B reads)
+    // the extension cast's result, indexed by the ray's item in the extension queue (its
+    // index in the shards' prefix order, the same for the cast and the next MATERIAL pass),
+    // not by path slot: written and read densely, and MATERIAL loads it beside the queue
+    // entry instead of behind it
     float4* hit;         // t, u, v, asfloat(triangle | backface << 31)
     uint32_t* hitInst;
     float4* shadowO;

@@ -296,9 +296,9 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         const uint32_t entry = qentry(pool.extPrev, pool.size, qm, i);
         path = entry & ~kEntryFirst;
         const bool first = (entry & kEntryFirst) != 0u;   // NEW_PATH's constants, not loaded
-        const float4 h4 = slot(pool.hit, path);
+        const float4 h4 = slot(pool.hit, i);
         HitRecord hit;
-        hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, path);
+        hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, i);
         const F3 rd = slot(pool.rayD, path);
         const V3 dir = mk(rd.x, rd.y, rd.z);
         const PathState& ps = slot(pool.state, path);
@@ -659,11 +659,11 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
             const F3 o = pool.rayO[path], d = pool.rayD[path];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf());
             if (OPACITY) s.opacitySample = pool.extOpacity[path];
-            return path;
+            return i;   // the result goes to the ray's queue item
         },
-        [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
-            pool.hit[path] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
-            pool.hitInst[path] = s.found ? s.hit.inst : 0u;
+        [&](uint32_t item, const TravState& s) __attribute__((always_inline)) {
+            pool.hit[item] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
+            pool.hitInst[item] = s.found ? s.hit.inst : 0u;
         },
         st, DCRT_WAVE_TAG(g));
     if (INSTR) flush_stats(st, instr);
@@ -766,15 +766,15 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
             s.pathFlags = asu(d.w);
             if (OPACITY) s.opacitySample = shadow ? pool.shadowOpacity[path] : pool.extOpacity[path];
             if (INSTR) st = TraversalStats{};
-            return path;
+            return shadow ? path : i;   // an extension ray's result goes to its queue item
         },
-        [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
+        [&](uint32_t item, const TravState& s) __attribute__((always_inline)) {
             if (s.anyHit) {
                 // the path's flags as MATERIAL wrote them (carried in shadowD.w): a plain store
-                pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (s.pathFlags & ~kFlagShadowRayHit);
+                pool.flags[item] = (s.found ? kFlagShadowRayHit : 0u) | (s.pathFlags & ~kFlagShadowRayHit);
             } else {
-                pool.hit[path] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
-                pool.hitInst[path] = s.found ? s.hit.inst : 0u;
+                pool.hit[item] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
+                pool.hitInst[item] = s.found ? s.hit.inst : 0u;
             }
             if (INSTR) {
                 TraversalStats& dst = s.anyHit ? stShadow : stExt;
