@@ -97,6 +97,24 @@ DEV uint32_t qentry(const uint32_t* queue, uint32_t cap, const QueueMapN<N>& m, 
     return queue[(size_t)s * cap + (i - base)];
 }
 
+// Position of item i of the concatenated shards: s * cap + (i - prefix[s]).
+template <uint32_t N>
+DEV uint32_t qpos(uint32_t cap, const QueueMapN<N>& m, uint32_t i)
+{
+    uint32_t s = 0, base = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < N; ++k) {
+        const bool ge = i >= m.prefix[k];
+        s += ge ? 1u : 0u;
+        base = ge ? m.prefix[k] : base;
+    }
+    return s * cap + (i - base);
+}
+// Extension-ray record `q` (q = shard * recCap + entry) through a 32-bit byte offset (one
+// parity's records stay below 4 GiB: dcrt_tracer::Create checks it)
+DEV float4* ext_rec(float4* recs, uint32_t q) { return (float4*)((char*)recs + (uint64_t)(q * 32u)); }
+DEV const float4* ext_rec(const float4* recs, uint32_t q) { return (const float4*)((const char*)recs + (uint64_t)(q * 32u)); }
+
 // Per-image constants, read from HBM so a captured graph can be replayed for
 // every frame seed (SNewPathConstants / SMaterialConstants / SControlConstants).
 struct FrameConstants {
@@ -179,8 +197,6 @@ struct PathState {
 };
 
 struct PathPool {
-    F3* rayO;            // extension ray origin (tMax = inf, tMin = 0 implicit); size + 1 entries
-    F3* rayD;            // extension ray direction; size + 1 entries (the cast kernel's 16-B reads)
     // the extension cast's result, indexed by the ray's item in the extension queue (its
     // index in the shards' prefix order, the same for the cast and the next MATERIAL pass),
     // not by path slot: written and read densely, and MATERIAL loads it beside the queue
@@ -201,12 +217,18 @@ struct PathPool {
     // iteration parity: `extQueue` / `finQueue` are this iteration's (appended to),
     // `extPrev` / `finPrev` the previous iteration's (MATERIAL / CONTROL work lists);
     // the host sets the four pointers per launch.
-    uint32_t* extQueue;
-    const uint32_t* extPrev;
+    // Extension rays travel IN the extension queue: entry e of shard s is a 32-B record at
+    // 2 * (s * recCap + e) float4s, (origin, 0) and (direction, asfloat(path slot |
+    // kEntryFirst)); tMax = inf, tMin = 0 implicit. Its producer (CONTROL, MATERIAL) writes
+    // it densely at its queue position, the cast reads it there without an index load, and
+    // the next MATERIAL pass takes the path and the incoming direction from one 16-B load.
+    float4* extRec;
+    const float4* extPrevRec;
     uint32_t* shadowQueue;
     uint32_t* finQueue;        // kFinShards x finCap entries
     const uint32_t* finPrev;
     uint32_t size;
+    uint32_t recCap;           // entries per extension-queue shard
     uint32_t finCap;           // entries per finish-queue shard
 };
 

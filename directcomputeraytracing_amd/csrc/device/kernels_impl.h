@@ -223,6 +223,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     }
     const uint32_t block = shard + claimed * kShards;
     bool newPath = false;
+    V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 0.0f);
     if (got) {
         uint32_t px = 0, py = 0, image = 0;
         if (block_pixel(*fc, film, block, lane, &px, &py, &image)) {
@@ -232,7 +233,6 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             const float fsx = (psx + (float)px) / (float)fc->resolution[0];
             const float fsy = (psy + (float)py) / (float)fc->resolution[1];
             const float a0 = next1(rng), a1 = next1(rng), a2 = next1(rng);
-            V3 o, d;
             generate_ray(*fc, fsx, fsy, a0, a1, a2, &o, &d);
             if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) pool.extOpacity[tid] = next1(rng);   // :223-226
             pool.pixel[tid] = image * (film.width * film.height) + py * film.width + px;
@@ -240,8 +240,6 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             // (into its own dense array: a 16-B piece of each 64-B state record was a partly
             // written sector per path)
             pool.rngNew[tid] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
-            pool.rayO[tid] = F3{o.x, o.y, o.z};
-            pool.rayD[tid] = F3{d.x, d.y, d.z};
             // Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0 are implicit: the path's
             // first MATERIAL pass takes them as constants (kEntryFirst); isDelta = true, bounce 0
             // (writing them into the state record too measured the same: 2.687 vs 2.682 ms/spp)
@@ -253,7 +251,11 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     // after every thread has passed this append's barriers)
     uint32_t eslot, unused;
     block_append2(newPath, qctr(cnt, kQExt, shard), false, qctr(cnt, kQExt, shard), sm + 32, &eslot, &unused);
-    if (newPath) pool.extQueue[(size_t)shard * pool.size + eslot] = tid | kEntryFirst;
+    if (newPath) {
+        float4* r = ext_rec(pool.extRec, shard * pool.recCap + eslot);
+        r[0] = make_float4(o.x, o.y, o.z, 0.0f);
+        r[1] = make_float4(d.x, d.y, d.z, asf(tid | kEntryFirst));
+    }
     }
 }
 
@@ -291,15 +293,18 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     float4 sample = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float2* outPos = nullptr;
     float4* outVal = nullptr;
+    V3 nO = mk(0.0f, 0.0f, 0.0f), nD = mk(0.0f, 0.0f, 0.0f);   // the next extension ray
     if (active) {
         ++itemsDone;
-        const uint32_t entry = qentry(pool.extPrev, pool.size, qm, i);
+        // the ray's record in the previous iteration's extension queue: its direction and
+        // the path slot (the hit record is at item i, independent of it)
+        const float4 rd = ext_rec(pool.extPrevRec, qpos(pool.recCap, qm, i))[1];
+        const uint32_t entry = asu(rd.w);
         path = entry & ~kEntryFirst;
         const bool first = (entry & kEntryFirst) != 0u;   // NEW_PATH's constants, not loaded
         const float4 h4 = slot(pool.hit, i);
         HitRecord hit;
         hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, i);
-        const F3 rd = slot(pool.rayD, path);
         const V3 dir = mk(rd.x, rd.y, rd.z);
         const PathState& ps = slot(pool.state, path);
         const uint4 r4 = first ? slot(pool.rngNew, path) : ps.rng;
@@ -380,9 +385,8 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
                 if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
                     const float NdotWI = fabsf(dot(it.normal, wi));
                     T = T * bsdf * NdotWI / bsdfPdf;
-                    const V3 o = offset_ray_origin(it.position, it.geometryNormal, wi);
-                    slot(pool.rayO, out) = F3{o.x, o.y, o.z};
-                    slot(pool.rayD, out) = F3{wi.x, wi.y, wi.z};
+                    nO = offset_ray_origin(it.position, it.geometryNormal, wi);
+                    nD = wi;   // (written into the extension queue after the append)
                     flags = (flags & 0xFFFFFF00u) | ((bounce + 1) & 0xFFu);
                 } else {
                     flags |= kFlagTerminate;
@@ -432,7 +436,11 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     uint32_t es, ss;
     block_append2(active && !terminate, qctr(cnt, kQExt, shard), active && hasShadow, qctr(cnt, kQShadow, shard),
                   sm + (round & 1u) * 32u, &es, &ss);
-    if (active && !terminate) slot(pool.extQueue, shard * pool.size + es) = path;
+    if (active && !terminate) {
+        float4* r = ext_rec(pool.extRec, shard * pool.recCap + es);
+        r[0] = make_float4(nO.x, nO.y, nO.z, 0.0f);
+        r[1] = make_float4(nD.x, nD.y, nD.z, asf(path));
+    }
     if (active && hasShadow) slot(pool.shadowQueue, shard * pool.size + ss) = path;
     {
         // paths ended with a shadow ray pending: the next CONTROL pass completes them (rare
@@ -654,11 +662,12 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
     TraversalStats st = {};
     persistent_trace<false, INSTR, OPACITY>(
         sc, qm.prefix[kShards], fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
-        [&](uint32_t i) __attribute__((always_inline)) { return qentry(pool.extQueue, pool.size, qm, i) & ~kEntryFirst; },
-        [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
-            const F3 o = pool.rayO[path], d = pool.rayD[path];
+        [&](uint32_t i) __attribute__((always_inline)) { return qpos(pool.recCap, qm, i); },
+        [&](uint32_t i, uint32_t q, TravState& s) __attribute__((always_inline)) {
+            const float4* r = ext_rec((const float4*)pool.extRec, q);
+            const float4 o = r[0], d = r[1];
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, inf());
-            if (OPACITY) s.opacitySample = pool.extOpacity[path];
+            if (OPACITY) s.opacitySample = pool.extOpacity[asu(d.w) & ~kEntryFirst];
             return i;   // the result goes to the ray's queue item
         },
         [&](uint32_t item, const TravState& s) __attribute__((always_inline)) {
@@ -740,10 +749,8 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     qmap(cnt, kQExt, &qe);
     qmap(cnt, kQShadow, &qs);
     const uint32_t nExt = qe.prefix[kShards], nShadow = qs.prefix[kShards];
-    const uint32_t* extQueue = sgpr_ptr(pool.extQueue);
     const uint32_t* shQueue = sgpr_ptr(pool.shadowQueue);
-    const float* rayO = sgpr_ptr((float*)pool.rayO);
-    const float* rayD = sgpr_ptr((float*)pool.rayD);
+    const float4* extRec = sgpr_ptr((const float4*)pool.extRec);
     const float4* shO = sgpr_ptr(pool.shadowO);
     const float4* shD = sgpr_ptr(pool.shadowD);
     TraversalStats st = {};
@@ -751,16 +758,18 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
-            const bool shadow = i >= nExt;
-            return qentry(shadow ? shQueue : extQueue, pool.size, shadow ? qs : qe, shadow ? i - nExt : i) & ~kEntryFirst;
+            // a shadow ray: its path slot (queue entry); an extension ray: its record's
+            // position in the queue (no load)
+            return i >= nExt ? qentry(shQueue, pool.size, qs, i - nExt) : qpos(pool.recCap, qe, i);
         },
-        [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
+        [&](uint32_t i, uint32_t v, TravState& s) __attribute__((always_inline)) {
             const bool shadow = i >= nExt;
-            // one 16-B load for either kind: a shadow ray's float4, or an extension ray's 12-B
-            // F3 and the next entry's first word (unused; the arrays carry a spare entry)
-            const size_t at = (size_t)path * (shadow ? 4u : 3u);
-            const F4u o = *(const F4u*)((shadow ? (const float*)shO : rayO) + at);
-            const F4u d = *(const F4u*)((shadow ? (const float*)shD : rayD) + at);
+            // a shadow ray's two float4 (slot v), or the extension ray's 32-B record (position v),
+            // through 32-bit byte offsets (the records stay below 4 GiB: dcrt_tracer::Create)
+            const uint32_t off = shadow ? v * 16u : v * 32u;
+            const float4 o = *(const float4*)((const char*)(shadow ? shO : extRec) + (uint64_t)off);
+            const float4 d = *(const float4*)((const char*)(shadow ? shD : extRec) + (uint64_t)(shadow ? off : off + 16u));
+            const uint32_t path = shadow ? v : asu(d.w) & ~kEntryFirst;
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, shadow ? o.w : inf());
             s.anyHit = shadow;
             s.pathFlags = asu(d.w);

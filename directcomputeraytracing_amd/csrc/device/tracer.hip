@@ -138,7 +138,7 @@ struct dcrt_tracer {
 
     std::vector<void*> poolAllocs, sceneAllocs, filmAllocs, sampleAllocs, rowAllocs;
     PathPool pool{};                   // (queue pointers set per launch: LaunchIteration)
-    uint32_t* extQueues = nullptr;     // 2 parities x kShards x poolSize
+    float4* extRecs = nullptr;         // 2 parities x kShards x recCap extension-ray records (2 float4)
     uint32_t* finQueues = nullptr;     // 2 parities x kFinShards x pool.finCap
     DeviceScene scene{};
     bool hasScene = false;
@@ -284,8 +284,6 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     }
     // WavefrontPathTracer.cpp:120-264 (SoA instead of AoS)
     const size_t P = poolSize;
-    CHECKED(DeviceAlloc(&pool.rayO, (size_t)P + 1, &poolAllocs));   // (+1: the cast kernel's 16-B reads of 12-B entries)
-    CHECKED(DeviceAlloc(&pool.rayD, (size_t)P + 1, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.hit, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.hitInst, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowO, P, &poolAllocs));
@@ -297,8 +295,20 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.extOpacity, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowOpacity, P, &poolAllocs));
-    // the extension and finish queues: one per iteration parity (extQueues / finQueues)
-    CHECKED(DeviceAlloc(&extQueues, (size_t)P * kShards * 2, &poolAllocs));
+    // the extension and finish queues: one per iteration parity (extRecs / finQueues). An
+    // extension-queue shard s receives the new paths of CONTROL's workgroups b = s mod
+    // kShards and the continuing paths of MATERIAL's (one 256-slot / 256-item round each when
+    // their grids cover the pool): at most 2 ceil(G / kShards) 256 entries; a capped grid
+    // (several rounds) falls back to the whole pool per shard.
+    {
+        const uint32_t G = (poolSize + 255u) / 256u;
+        const bool oneRound = std::min<uint32_t>(poolSize / kControlBlock, kControlMaxBlocks) * kControlBlock >= poolSize &&
+                              std::min<uint32_t>(G, kMaterialMaxBlocks) * kMaterialBlock >= poolSize && kControlBlock == 256u &&
+                              kMaterialBlock == 256u;
+        pool.recCap = oneRound ? std::min<uint32_t>(poolSize, 2u * ((G + kShards - 1) / kShards) * 256u) : poolSize;
+    }
+    if ((uint64_t)pool.recCap * kShards * 32u > 0xFFFFFFFFull) { SetLastError("path pool too large for the extension-queue records"); return DCRT_E_LIMIT; }
+    CHECKED(DeviceAlloc(&extRecs, (size_t)pool.recCap * kShards * 2 * 2, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowQueue, (size_t)P * kShards, &poolAllocs));
     {
         // MATERIAL workgroup b appends the paths it ends with a shadow ray pending to finish
@@ -738,8 +748,8 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     Counters* cnt = dCounters + par;
     Counters* next = dCounters + (par ^ 1u);   // (the previous iteration's; the casts clear them for the next)
     PathPool pool = this->pool;
-    pool.extQueue = extQueues + (size_t)par * kShards * poolSize;
-    pool.extPrev = extQueues + (size_t)(par ^ 1u) * kShards * poolSize;
+    pool.extRec = extRecs + (size_t)par * kShards * pool.recCap * 2;
+    pool.extPrevRec = extRecs + (size_t)(par ^ 1u) * kShards * pool.recCap * 2;
     pool.finQueue = finQueues + (size_t)par * kFinShards * pool.finCap;
     pool.finPrev = finQueues + (size_t)(par ^ 1u) * kFinShards * pool.finCap;
     // CONTROL and MATERIAL get one workgroup per 256 slots (their grid-stride loops then run
