@@ -203,8 +203,10 @@ struct PathPool {
     // entry instead of behind it
     float4* hit;         // t, u, v, asfloat(triangle | backface << 31)
     uint32_t* hitInst;
-    float4* shadowO;
-    float4* shadowD;
+    // Shadow rays, like the extension rays, travel in their queue: entry e of shard s has
+    // a 32-B record at 2 * (s * recCap + e) float4s, (origin, tMax) and (direction, the
+    // path's flags as MATERIAL left them), beside its path slot in shadowQueue[s * recCap + e]
+    float4* shRec;
     uint32_t* pixel;     // sample index: image * W*H + y * W + x
     float2* pixelSample;
     PathState* state;    // rng, throughput, Li, light sampling result

@@ -294,6 +294,9 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     float2* outPos = nullptr;
     float4* outVal = nullptr;
     V3 nO = mk(0.0f, 0.0f, 0.0f), nD = mk(0.0f, 0.0f, 0.0f);   // the next extension ray
+    float4 sO = make_float4(0.0f, 0.0f, 0.0f, 0.0f);            // the shadow ray (origin, tMax)
+    V3 sD = mk(0.0f, 0.0f, 0.0f);
+    uint32_t sFlags = 0;
     if (active) {
         ++itemsDone;
         // the ray's record in the previous iteration's extension queue: its direction and
@@ -369,8 +372,8 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
                     const float weight = ls.isDelta ? 1.0f : power_heuristic(ls.pdf, bsdfPdf);
                     lsr = T * ls.radiance * bsdf * NdotWI * weight / ls.pdf;
                     const V3 so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
-                    slot(pool.shadowO, out) = make_float4(so.x, so.y, so.z, ls.distance);
-                    slot(pool.shadowD, out) = make_float4(ls.wi.x, ls.wi.y, ls.wi.z, 0.0f);
+                    sO = make_float4(so.x, so.y, so.z, ls.distance);   // (written into the shadow
+                    sD = ls.wi;                                         //  queue after the append)
                     hasShadow = true;
                 }
             }
@@ -422,9 +425,9 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
             slot(pool.flags, out) = kFlagIdle;
         } else {
             slot(pool.flags, out) = flags;
-            // the shadow cast writes the path's flags with the occlusion bit (a plain store, no
-            // read of the flags in front of it): it takes them from shadowD.w (tMin, unused: 0)
-            if (hasShadow) reinterpret_cast<float*>(&slot(pool.shadowD, out))[3] = asf(flags);
+            // (the shadow cast writes the path's flags with the occlusion bit — a plain store,
+            // no read of the flags in front of it — taking them from the shadow ray's record)
+            sFlags = flags;
             PathState& po = slot(pool.state, out);
             po.rng = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
             po.thr = make_float4(T.x, T.y, T.z, thr.w);
@@ -441,7 +444,13 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         r[0] = make_float4(nO.x, nO.y, nO.z, 0.0f);
         r[1] = make_float4(nD.x, nD.y, nD.z, asf(path));
     }
-    if (active && hasShadow) slot(pool.shadowQueue, shard * pool.size + ss) = path;
+    if (active && hasShadow) {
+        const uint32_t q = shard * pool.recCap + ss;
+        float4* r = ext_rec(pool.shRec, q);
+        r[0] = sO;
+        r[1] = make_float4(sD.x, sD.y, sD.z, asf(sFlags));
+        slot(pool.shadowQueue, q) = path;
+    }
     {
         // paths ended with a shadow ray pending: the next CONTROL pass completes them (rare
         // enough for one atomic per wave that has any)
@@ -715,9 +724,11 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
     TraversalStats st = {};
     persistent_trace<true, INSTR, OPACITY>(
         sc, n, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
-        [&](uint32_t i) __attribute__((always_inline)) { return qentry(pool.shadowQueue, pool.size, qm, i); },
-        [&](uint32_t i, uint32_t path, TravState& s) __attribute__((always_inline)) {
-            const float4 o = pool.shadowO[path], d = pool.shadowD[path];
+        [&](uint32_t i) __attribute__((always_inline)) { return qpos(pool.recCap, qm, i); },
+        [&](uint32_t i, uint32_t q, TravState& s) __attribute__((always_inline)) {
+            const float4* r = ext_rec((const float4*)pool.shRec, q);
+            const float4 o = r[0], d = r[1];
+            const uint32_t path = slot(pool.shadowQueue, q);
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, o.w);
             s.pathFlags = asu(d.w);
             if (OPACITY) s.opacitySample = pool.shadowOpacity[path];
@@ -751,25 +762,22 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     const uint32_t nExt = qe.prefix[kShards], nShadow = qs.prefix[kShards];
     const uint32_t* shQueue = sgpr_ptr(pool.shadowQueue);
     const float4* extRec = sgpr_ptr((const float4*)pool.extRec);
-    const float4* shO = sgpr_ptr(pool.shadowO);
-    const float4* shD = sgpr_ptr(pool.shadowD);
+    const float4* shRec = sgpr_ptr((const float4*)pool.shRec);
     TraversalStats st = {};
     TraversalStats stExt = {}, stShadow = {};
     persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
-            // a shadow ray: its path slot (queue entry); an extension ray: its record's
-            // position in the queue (no load)
-            return i >= nExt ? qentry(shQueue, pool.size, qs, i - nExt) : qpos(pool.recCap, qe, i);
+            // either kind: its record's position in its queue (no load)
+            return i >= nExt ? qpos(pool.recCap, qs, i - nExt) : qpos(pool.recCap, qe, i);
         },
         [&](uint32_t i, uint32_t v, TravState& s) __attribute__((always_inline)) {
             const bool shadow = i >= nExt;
-            // a shadow ray's two float4 (slot v), or the extension ray's 32-B record (position v),
-            // through 32-bit byte offsets (the records stay below 4 GiB: dcrt_tracer::Create)
-            const uint32_t off = shadow ? v * 16u : v * 32u;
-            const float4 o = *(const float4*)((const char*)(shadow ? shO : extRec) + (uint64_t)off);
-            const float4 d = *(const float4*)((const char*)(shadow ? shD : extRec) + (uint64_t)(shadow ? off : off + 16u));
-            const uint32_t path = shadow ? v : asu(d.w) & ~kEntryFirst;
+            // the ray's 32-B record at its queue position v (32-bit byte offsets: the records
+            // stay below 4 GiB, dcrt_tracer::Create); a shadow ray's path slot beside it
+            const float4* r = ext_rec(shadow ? shRec : extRec, v);
+            const float4 o = r[0], d = r[1];
+            const uint32_t path = shadow ? slot(shQueue, v) : asu(d.w) & ~kEntryFirst;
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, shadow ? o.w : inf());
             s.anyHit = shadow;
             s.pathFlags = asu(d.w);

@@ -286,8 +286,6 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     const size_t P = poolSize;
     CHECKED(DeviceAlloc(&pool.hit, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.hitInst, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.shadowO, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.shadowD, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.pixel, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.pixelSample, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.state, P, &poolAllocs));
@@ -309,7 +307,10 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     }
     if ((uint64_t)pool.recCap * kShards * 32u > 0xFFFFFFFFull) { SetLastError("path pool too large for the extension-queue records"); return DCRT_E_LIMIT; }
     CHECKED(DeviceAlloc(&extRecs, (size_t)pool.recCap * kShards * 2 * 2, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.shadowQueue, (size_t)P * kShards, &poolAllocs));
+    // the shadow queue (filled and cast within one iteration): records + path slots
+    CHECKED(DeviceAlloc(&pool.shRec, (size_t)pool.recCap * kShards * 2, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.shadowQueue, (size_t)pool.recCap * kShards, &poolAllocs));
+
     {
         // MATERIAL workgroup b appends the paths it ends with a shadow ray pending to finish
         // shard b % kFinShards
