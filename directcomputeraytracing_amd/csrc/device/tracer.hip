@@ -305,7 +305,8 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
                               kMaterialBlock == 256u;
         pool.recCap = oneRound ? std::min<uint32_t>(poolSize, 2u * ((G + kShards - 1) / kShards) * 256u) : poolSize;
     }
-    if ((uint64_t)pool.recCap * kShards * 32u > 0xFFFFFFFFull) { SetLastError("path pool too large for the extension-queue records"); return DCRT_E_LIMIT; }
+    // (32-bit byte offsets address one parity's records: at most 2^32 bytes, e.g. 2^26 slots)
+    if ((uint64_t)pool.recCap * kShards * 32u > (1ull << 32)) { SetLastError("path pool too large for the extension-queue records"); return DCRT_E_LIMIT; }
     CHECKED(DeviceAlloc(&extRecs, (size_t)pool.recCap * kShards * 2 * 2, &poolAllocs));
     // the shadow queue (filled and cast within one iteration): records + path slots
     CHECKED(DeviceAlloc(&pool.shRec, (size_t)pool.recCap * kShards * 2, &poolAllocs));
