@@ -550,11 +550,9 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
     // (24-bit multiply: a 32-bit a * b + c becomes v_mad_u64_u32 with an arbitrary VGPR as
     // the unused high addend, which made the refill wait for the window's pending load)
     auto itemIndex = [&](uint32_t k) { return (waveId + __umul24(k / kInterleave, waves)) * kInterleave + k % kInterleave; };
-    // Prefetch window: lane L holds `ahead` = lookup() of the wave's item k = L (mod 64)
-    // in [cursor, cursor + 64), loaded one refill or more before a lane takes it, so a
-    // refill waits for the ray loads only, not for the queue read in front of them.
-    uint32_t ahead = 0;
-    if (lane < end && itemIndex(lane) < n) ahead = lookup(itemIndex(lane));
+    // lookup(i) is arithmetic only (a ray's record position in its queue): a refill waits for
+    // the ray loads alone (the earlier 4-B queue entries needed a prefetch window of lookups
+    // one refill ahead, a bpermute and a register)
     TravState s;
     // lane state, one integer (per-lane bools cost mask <-> register conversions per step):
     // kIdle no ray; kRun visiting nodes; kPark at a leaf (phase B work pending); kFin ray
@@ -575,11 +573,8 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         const uint32_t nNeed = (uint32_t)__popcll(need);
         const bool refill = nNeed >= kRefillLanes && cursor < end;
         const uint32_t k = cursor + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-        uint32_t path = 0;
-        if (refill) path = (uint32_t)__shfl((int)ahead, (int)(k & 63u), 64);   // every lane: a full-wave bpermute
-        // Finished rays are written here, after the window read and just before the ray
-        // loads: stores count in vmcnt too, so written earlier they would make the window
-        // read wait for their acknowledgement, and the ray loads then wait once more.
+        // Finished rays are written here, just before the ray loads (stores count in vmcnt
+        // too: the loads are then not queued behind older stores' acknowledgements twice).
         if (ls == kFin) {
             emit(item, s);
             ls = kIdle;
@@ -587,16 +582,11 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         if (refill) {
             const uint32_t idx = itemIndex(k);
             if (free && k < end && idx < n) {
-                item = fetch(idx, path, s);
+                item = fetch(idx, lookup(idx), s);
                 if (!f2b) s.negMask = 0u;
                 ls = kRun;
             }
-            const uint32_t used = min(nNeed, end - cursor);
-            // this lane's window item cursor + ((L - cursor) mod 64) was taken: look up the one 64 later
-            const uint32_t off = (lane - cursor) & 63u;
-            const uint32_t k2 = cursor + off + 64u;
-            if (off < used && k2 < end && itemIndex(k2) < n) ahead = lookup(itemIndex(k2));
-            cursor += used;
+            cursor += min(nNeed, end - cursor);
         }
         DCRT_PHASE(0);
         if (__ballot(ls != kIdle) == 0ull) break;
