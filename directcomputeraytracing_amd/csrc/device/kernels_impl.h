@@ -85,6 +85,32 @@ __device__ __forceinline__ void block_append2(bool pa, uint32_t* ca, bool pb, ui
     *rb = sm[31] + sm[16 + wave] + xb;
 }
 
+// Three appends at once (MATERIAL: extension, shadow and finish queues): as block_append2,
+// threads 0 / 1 / 2 issue the three atomics together. sm needs 48 words per call (callers
+// alternate two halves of 96).
+__device__ __forceinline__ void block_append3(bool pa, uint32_t* ca, bool pb, uint32_t* cb, bool pc, uint32_t* cc, uint32_t* sm,
+                                              uint32_t* ra, uint32_t* rb, uint32_t* rc)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t waves = blockDim.x >> 6;
+    const unsigned long long ma = __ballot(pa), mb = __ballot(pb), mc = __ballot(pc);
+    const uint32_t xa = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
+    const uint32_t xb = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+    const uint32_t xc = __builtin_amdgcn_mbcnt_hi((uint32_t)(mc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mc, 0u));
+    if (lane == 0) { sm[wave] = (uint32_t)__popcll(ma); sm[16 + wave] = (uint32_t)__popcll(mb); sm[32 + wave] = (uint32_t)__popcll(mc); }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint32_t* q = sm + threadIdx.x * 16;
+        uint32_t total = 0;
+        for (uint32_t w = 0; w < waves; ++w) { const uint32_t c = q[w]; q[w] = total; total += c; }
+        q[15] = total ? atomicAdd(threadIdx.x == 0 ? ca : (threadIdx.x == 1 ? cb : cc), total) : 0u;
+    }
+    __syncthreads();
+    *ra = sm[15] + sm[wave] + xa;
+    *rb = sm[31] + sm[16 + wave] + xb;
+    *rc = sm[47] + sm[32 + wave] + xc;
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(uint32_t v)
 {
     unsigned long long s = v;
@@ -274,7 +300,7 @@ template <uint32_t CAPS>
 __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
                                                                              const Counters* prev, const SampleOut* sampleOut)
 {
-    __shared__ uint32_t sm[64];
+    __shared__ uint32_t sm[96];
     // the work list: the previous iteration's extension queue (its rays have been cast)
     QueueMap qm;
     qmap(prev, kQExt, &qm);
@@ -437,8 +463,11 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     }
     DCRT_MCLK(5);
     uint32_t es, ss;
-    block_append2(active && !terminate, qctr(cnt, kQExt, shard), active && hasShadow, qctr(cnt, kQShadow, shard),
-                  sm + (round & 1u) * 32u, &es, &ss);
+    // (paths ended with a shadow ray pending: the next CONTROL pass completes them)
+    const bool fin = active && terminate && hasShadow;
+    uint32_t fb;
+    block_append3(active && !terminate, qctr(cnt, kQExt, shard), active && hasShadow, qctr(cnt, kQShadow, shard),
+                  fin, qctr(cnt, kQFinish, fshard), sm + (round & 1u) * 48u, &es, &ss, &fb);
     if (active && !terminate) {
         float4* r = ext_rec(pool.extRec, shard * pool.recCap + es);
         r[0] = make_float4(nO.x, nO.y, nO.z, 0.0f);
@@ -451,18 +480,7 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         r[1] = make_float4(sD.x, sD.y, sD.z, asf(sFlags));
         slot(pool.shadowQueue, q) = path;
     }
-    {
-        // paths ended with a shadow ray pending: the next CONTROL pass completes them (rare
-        // enough for one atomic per wave that has any)
-        const bool fin = active && terminate && hasShadow;
-        const unsigned long long fm = __ballot(fin);
-        if (fm != 0ull) {
-            uint32_t fb = 0;
-            if ((threadIdx.x & 63u) == 0) fb = atomicAdd(qctr(cnt, kQFinish, fshard), (uint32_t)__popcll(fm));
-            fb = (uint32_t)__shfl((int)fb, 0, 64) + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-            if (fin) slot(pool.finQueue, fshard * pool.finCap + fb) = path;
-        }
-    }
+    if (fin) slot(pool.finQueue, fshard * pool.finCap + fb) = path;
     if (ends) {
         slot(outPos, pix) = pixSample;
         slot(outVal, pix) = sample;
