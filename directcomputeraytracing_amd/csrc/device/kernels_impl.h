@@ -289,11 +289,15 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
 #ifndef DCRT_MATERIAL_BLOCK
 #define DCRT_MATERIAL_BLOCK 256
 #endif
-#ifdef DCRT_MATERIAL_WAVES_PER_EU
-#define DCRT_MATERIAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(DCRT_MATERIAL_WAVES_PER_EU, 8)))
-#else
-#define DCRT_MATERIAL_OCCUPANCY
+// The any-scene MATERIAL variant is held to 5 waves/SIMD (<= 96 VGPRs; 117 and 4 waves
+// unbounded): it then spills 3 VGPRs and still gains, coffee 3.12 -> 3.02, lamp 7.78 ->
+// 7.62 ms/spp (three / two A/B passes). The scene-specialised variants reach 5 waves by
+// themselves (95 VGPRs); held to 5 the compiler schedules them into 91 and the Cornell
+// bench loses 2 % (2.393 -> 2.447, four passes), so they are left unbounded.
+#ifndef DCRT_MATERIAL_WAVES_PER_EU
+#define DCRT_MATERIAL_WAVES_PER_EU 5
 #endif
+#define DCRT_MATERIAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(CAPS == kCapAll ? DCRT_MATERIAL_WAVES_PER_EU : 1, 8)))
 // CAPS: the scene capabilities this variant is compiled for (kCapAll = any scene; see
 // kCapOpaqueDelta in dscene.h and dcrt_tracer::UploadScene).
 template <uint32_t CAPS>
