@@ -130,6 +130,18 @@ class TraversalStats(C.Structure):
                 ("shadow_blas_entries", C.c_uint64), ("ext_launches", C.c_uint64), ("ext_kernel_ms", C.c_double)]
 
 
+class ObjMesh(C.Structure):
+    _fields_ = [("vertices", C.POINTER(Vertex)), ("vertex_count", C.c_uint32), ("indices", C.POINTER(C.c_uint32)),
+                ("material_ids", C.POINTER(C.c_uint32)), ("triangle_count", C.c_uint32)]
+
+
+class ObjMaterial(C.Structure):
+    _fields_ = [("albedo", C.c_float * 3), ("ior", C.c_float), ("roughness", C.c_float), ("opacity", C.c_float),
+                ("albedo_texture_index", C.c_int32), ("opacity_texture_index", C.c_int32)]
+
+
+OBJ_SCENE_LAYOUT = 1
+
 # Every symbol include/dcrt.h declares: (name, restype, argtypes)
 _P = C.c_void_p
 _I = C.c_int
@@ -162,6 +174,12 @@ SIGNATURES = [
     ("dcrt_bvh_build_blas", _I, [C.POINTER(Vertex), C.POINTER(C.c_uint32), _U, C.POINTER(BVHNode),
                                  C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    ("dcrt_obj_load", _I, [C.c_char_p, _U, _U, C.POINTER(_P)]),
+    ("dcrt_obj_mesh_count", _I, [_P, C.POINTER(C.c_uint32)]),
+    ("dcrt_obj_get_mesh", _I, [_P, _U, C.POINTER(ObjMesh)]),
+    ("dcrt_obj_material_count", _I, [_P, C.POINTER(C.c_uint32)]),
+    ("dcrt_obj_get_material", _I, [_P, _U, C.POINTER(ObjMaterial)]),
+    ("dcrt_obj_free", None, [_P]),
     ("dcrt_tracer_create", _I, [C.POINTER(TracerConfig), C.POINTER(_P)]),
     ("dcrt_tracer_destroy", None, [_P]),
     ("dcrt_tracer_upload_scene", _I, [_P, C.POINTER(FlatScene)]),

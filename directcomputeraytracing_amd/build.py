@@ -136,6 +136,21 @@ def build_oracle(force: bool = False) -> Path:
     return ORACLE_LIB
 
 
+REFERENCE = Path(os.environ.get("DCRT_REFERENCE", "/root/reference"))
+
+
+def build_reference_checkers() -> Path | None:
+    """TEST INFRASTRUCTURE: when the reference sources are present (the build container,
+    never the GPU box), compile its own OBJ dependencies -- tinyobjloader + MikkTSpace,
+    unmodified, from where they lie -- with our load-flow harness into
+    oracle/_ref/librefobj.so (oracle/ref_obj/Makefile). tests/test_obj_pin.py uses it."""
+    if not (REFERENCE / "tinyobjloader" / "tiny_obj_loader.h").exists():
+        return None
+    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR / "ref_obj"), f"REF={REFERENCE}"], check=True,
+                   stdout=subprocess.DEVNULL)
+    return ORACLE_DIR / "_ref" / "librefobj.so"
+
+
 if __name__ == "__main__":
     print(build_native(force="--force" in sys.argv, verbose=True))
     print(build_oracle(force="--force" in sys.argv))

@@ -4,6 +4,7 @@
 #include <cstring>
 #include <vector>
 #include <exception>
+#include <memory>
 #include <string>
 
 #include "../../../include/dcrt.h"
@@ -265,6 +266,93 @@ DCRT_API int dcrt_bvh_build_blas(const dcrt_vertex* vertices, const uint32_t* in
     return DCRT_OK;
     DCRT_GUARD_END
 }
+
+// ---- OBJ meshes before the BVH build (WavefrontOBJLoading.cpp:155-263,374-465)
+struct dcrt_obj_meshes {
+    std::vector<dcrt::Mesh> meshes;
+    std::vector<dcrt::SMaterial> materials;
+};
+
+DCRT_API int dcrt_obj_load(const char* path, uint32_t flags, uint32_t material_index_base, dcrt_obj_meshes** out)
+{
+    if (!path || !out) return DCRT_E_INVALID_ARG;
+    DCRT_GUARD_BEGIN
+    std::unique_ptr<dcrt_obj_meshes> r(new dcrt_obj_meshes());
+    dcrt::ObjData data;
+    std::string err;
+    if (!dcrt::ParseObjFile(path, &data, &err)) {
+        SetLastError(err);
+        return DCRT_E_IO;
+    }
+    dcrt::SMeshProcessingParams params;
+    params.changeWindingOrder = true;
+    params.flipTexcoordV = true;
+    if (flags & DCRT_OBJ_SCENE_LAYOUT) {
+        params.applyTransform = true;
+        params.transform.m[0][0] = -1.0f;
+        for (size_t s = 0; s < data.shapes.size(); ++s) {
+            r->meshes.emplace_back();
+            params.materialIndexBase = material_index_base;
+            if (!dcrt::CreateMeshFromObjData(data, &data.shapes[s], 1, params, &r->meshes.back())) {
+                SetLastError("mesh creation failed");
+                return DCRT_E_IO;
+            }
+        }
+    } else {
+        params.materialIndexBase = material_index_base;
+        r->meshes.emplace_back();
+        if (!dcrt::CreateMeshFromObjData(data, data.shapes.data(), (uint32_t)data.shapes.size(), params, &r->meshes.back())) {
+            SetLastError("mesh creation failed");
+            return DCRT_E_IO;
+        }
+    }
+    std::vector<std::string> textureNames;
+    dcrt::TranslateObjMaterials(data, 0, &r->materials, &textureNames);
+    *out = r.release();
+    return DCRT_OK;
+    DCRT_GUARD_END
+}
+
+DCRT_API int dcrt_obj_mesh_count(const dcrt_obj_meshes* m, uint32_t* out)
+{
+    if (!m || !out) return DCRT_E_INVALID_ARG;
+    *out = (uint32_t)m->meshes.size();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_obj_get_mesh(const dcrt_obj_meshes* m, uint32_t index, dcrt_obj_mesh* out)
+{
+    if (!m || !out || index >= m->meshes.size()) return DCRT_E_INVALID_ARG;
+    const dcrt::Mesh& mesh = m->meshes[index];
+    out->vertices = mesh.vertices.data();
+    out->vertex_count = (uint32_t)mesh.vertices.size();
+    out->indices = mesh.indices.data();
+    out->material_ids = mesh.materialIds.data();
+    out->triangle_count = mesh.GetTriangleCount();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_obj_material_count(const dcrt_obj_meshes* m, uint32_t* out)
+{
+    if (!m || !out) return DCRT_E_INVALID_ARG;
+    *out = (uint32_t)m->materials.size();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_obj_get_material(const dcrt_obj_meshes* m, uint32_t index, dcrt_obj_material* out)
+{
+    if (!m || !out || index >= m->materials.size()) return DCRT_E_INVALID_ARG;
+    const dcrt::SMaterial& s = m->materials[index];
+    out->albedo[0] = s.albedo.x; out->albedo[1] = s.albedo.y; out->albedo[2] = s.albedo.z;
+    out->ior = s.ior.x;
+    out->roughness = s.roughness;
+    out->opacity = s.opacity;
+    out->albedo_texture_index = s.albedoTextureIndex;
+    out->opacity_texture_index = s.opacityTextureIndex;
+    return DCRT_OK;
+}
+
+DCRT_API void dcrt_obj_free(dcrt_obj_meshes* m) { delete m; }
 
 }  // extern "C"
 

@@ -1,11 +1,13 @@
 // obj_loader.cpp -- Wavefront OBJ/MTL loading for CScene
-// (Source/WavefrontOBJLoading.cpp:155-465). The parser reproduces the
-// tinyobjloader behaviours the reference depends on (shape split on g/o,
-// per-face material ids, ear-clipping triangulation that reduces to a fan on
-// convex polygons, MTL defaults). Tangents are generated per corner from the UV
-// parameterisation and averaged over corners that share (v, vn, vt) -- a
-// MikkTSpace-compatible result for planar, consistently mapped faces (MikkTSpace
-// itself is not re-derived: parity unpinned).
+// (Source/WavefrontOBJLoading.cpp:155-465). The reference parses with tinyobjloader
+// (/root/reference/tinyobjloader/tiny_obj_loader.h, LoadObj with triangulation) and
+// generates tangents with MikkTSpace; both are parity-defining (vertex bits, vertex
+// order, triangle order), so this parser restates the tinyobjloader behaviours the
+// loader depends on -- its digit-by-digit number parsing, line/token rules, shape
+// splitting on g/o/usemtl, ear-clipping triangulation and MTL defaults -- and
+// tangent_space.cpp restates genTangSpaceDefault. tests/test_obj_pin.py checks the
+// result bit for bit against the unmodified reference libraries built test-side
+// (oracle/ref_obj/).
 #include "scene.h"
 
 #include <cmath>
@@ -20,30 +22,153 @@
 namespace dcrt {
 namespace {
 
-std::string Trim(const std::string& s)
+inline bool Blank(char c) { return c == ' ' || c == '\t'; }
+inline bool LineEnd(char c) { return c == '\r' || c == '\n' || c == '\0'; }
+inline bool Digit(char c) { return (unsigned)(c - '0') < 10u; }
+
+// One line with tinyobjloader's safeGetline rules: "\n", "\r\n" and a lone "\r" end a
+// line (tiny_obj_loader.h:730-762).
+bool NextLine(std::istream& in, std::string* line)
 {
-    size_t b = s.find_first_not_of(" \t\r\n"), e = s.find_last_not_of(" \t\r\n");
-    return b == std::string::npos ? std::string() : s.substr(b, e - b + 1);
+    line->clear();
+    std::streambuf* sb = in.rdbuf();
+    if (sb->sgetc() == EOF) return false;
+    for (;;) {
+        const int c = sb->sbumpc();
+        if (c == '\n' || c == EOF) return true;
+        if (c == '\r') {
+            if (sb->sgetc() == '\n') sb->sbumpc();
+            return true;
+        }
+        line->push_back((char)c);
+    }
 }
 
-// "v", "v/vt", "v//vn", "v/vt/vn"; 1-based, negative = relative (tinyobj parseTriple)
-bool ParseCorner(const std::string& tok, int vcount, int vncount, int vtcount, ObjIndex* out)
+// tryParseDouble (tiny_obj_loader.h:836-960): the integer digits accumulate as m*10 + d,
+// fraction digit k adds d * 10^-k (a table for k < 8, pow beyond), an exponent e scales
+// by ldexp(m * 5^e, e). Not correctly rounded, so it is restated rather than strtod.
+bool ObjReal(const char* s, const char* end, double* out)
 {
-    int vals[3] = { 0, 0, 0 };
-    bool has[3] = { false, false, false };
-    size_t pos = 0;
-    for (int k = 0; k < 3 && pos <= tok.size(); ++k) {
-        size_t slash = tok.find('/', pos);
-        std::string part = tok.substr(pos, slash == std::string::npos ? std::string::npos : slash - pos);
-        if (!part.empty()) { vals[k] = std::atoi(part.c_str()); has[k] = true; }
-        if (slash == std::string::npos) break;
-        pos = slash + 1;
+    if (s >= end) return false;
+    static const double kFrac[8] = { 1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001 };
+    double m = 0.0;
+    int e10 = 0, digits = 0;
+    char sign = '+', expSign = '+';
+    const char* c = s;
+    bool leadingDot = false;
+    if (*c == '+' || *c == '-') {
+        sign = *c++;
+        leadingDot = c != end && *c == '.';
+    } else if (*c == '.') {
+        leadingDot = true;
+    } else if (!Digit(*c)) {
+        return false;
     }
-    auto fix = [](int idx, int n) { return idx > 0 ? idx - 1 : (idx < 0 ? n + idx : -1); };
-    if (!has[0] || vals[0] == 0) return false;
-    out->v = fix(vals[0], vcount);
-    out->vt = has[1] ? fix(vals[1], vtcount) : -1;
-    out->vn = has[2] ? fix(vals[2], vncount) : -1;
+    bool more = c != end;
+    if (!leadingDot) {
+        while (more && Digit(*c)) {
+            m *= 10;
+            m += (int)(*c - '0');
+            ++c; ++digits;
+            more = c != end;
+        }
+        if (digits == 0) return false;
+    }
+    if (more) {
+        bool exponent = false;
+        if (*c == '.') {
+            ++c;
+            int k = 1;
+            more = c != end;
+            while (more && Digit(*c)) {
+                m += (int)(*c - '0') * (k < 8 ? kFrac[k] : std::pow(10.0, -k));
+                ++k; ++c;
+                more = c != end;
+            }
+            exponent = more && (*c == 'e' || *c == 'E');
+        } else {
+            exponent = *c == 'e' || *c == 'E';
+        }
+        if (exponent) {
+            ++c;
+            more = c != end;
+            if (more && (*c == '+' || *c == '-')) expSign = *c++;
+            else if (!Digit(*c)) return false;
+            digits = 0;
+            more = c != end;
+            while (more && Digit(*c)) {
+                e10 *= 10;
+                e10 += (int)(*c - '0');
+                ++c; ++digits;
+                more = c != end;
+            }
+            e10 *= expSign == '+' ? 1 : -1;
+            if (digits == 0) return false;
+        }
+    }
+    *out = (sign == '+' ? 1 : -1) * (e10 ? std::ldexp(m * std::pow(5.0, e10), e10) : m);
+    return true;
+}
+
+// parseReal: one blank-delimited token, the default when it does not parse
+float TakeReal(const char** tok, double dflt = 0.0, bool* parsed = nullptr)
+{
+    *tok += std::strspn(*tok, " \t");
+    const char* end = *tok + std::strcspn(*tok, " \t\r");
+    double v = dflt;
+    const bool ok = ObjReal(*tok, end, &v);
+    if (parsed) *parsed = ok;
+    *tok = end;
+    return (float)v;
+}
+
+int TakeInt(const char** tok)
+{
+    *tok += std::strspn(*tok, " \t");
+    const int v = std::atoi(*tok);
+    *tok += std::strcspn(*tok, " \t\r");
+    return v;
+}
+
+std::string TakeWord(const char** tok)
+{
+    *tok += std::strspn(*tok, " \t");
+    const size_t n = std::strcspn(*tok, " \t\r");
+    std::string w(*tok, n);
+    *tok += n;
+    return w;
+}
+
+// 1-based, negative = relative to the elements so far, 0 = error (fixIndex)
+bool FixIndex(int idx, int n, int* out)
+{
+    if (idx > 0) { *out = idx - 1; return true; }
+    if (idx < 0) { *out = n + idx; return true; }
+    return false;
+}
+
+// "v", "v/vt", "v//vn", "v/vt/vn" (parseTriple)
+bool TakeCorner(const char** tok, int nv, int nvn, int nvt, ObjIndex* out)
+{
+    ObjIndex r;
+    if (!FixIndex(std::atoi(*tok), nv, &r.v)) return false;
+    *tok += std::strcspn(*tok, "/ \t\r");
+    if (**tok != '/') { *out = r; return true; }
+    ++*tok;
+    if (**tok == '/') {
+        ++*tok;
+        if (!FixIndex(std::atoi(*tok), nvn, &r.vn)) return false;
+        *tok += std::strcspn(*tok, "/ \t\r");
+        *out = r;
+        return true;
+    }
+    if (!FixIndex(std::atoi(*tok), nvt, &r.vt)) return false;
+    *tok += std::strcspn(*tok, "/ \t\r");
+    if (**tok != '/') { *out = r; return true; }
+    ++*tok;
+    if (!FixIndex(std::atoi(*tok), nvn, &r.vn)) return false;
+    *tok += std::strcspn(*tok, "/ \t\r");
+    *out = r;
     return true;
 }
 
@@ -55,18 +180,21 @@ bool PointInTriangle(const float* vx, const float* vy, float tx, float ty)   // 
     return c;
 }
 
-// Ear clipping as tinyobjloader's exportGroupsToShape (fan order on convex faces).
+// Ear clipping as tinyobjloader's exportGroupsToShape (tiny_obj_loader.h:1365-1598): a fan
+// on convex faces; corners whose vertex index is out of range read as (0, 0).
 void Triangulate(const std::vector<ObjIndex>& face, const std::vector<float>& v, int materialId, ObjShape* shape)
 {
     const size_t n = face.size();
     if (n < 3) return;
-    auto P = [&](const ObjIndex& i, int axis) { return (size_t)i.v * 3 + axis < v.size() ? v[(size_t)i.v * 3 + axis] : 0.0f; };
+    auto valid = [&](const ObjIndex& i, size_t axis) { return (size_t)i.v * 3 + axis < v.size(); };
+    auto P = [&](const ObjIndex& i, size_t axis) { return v[(size_t)i.v * 3 + axis]; };
     size_t axes[2] = { 1, 2 };
     for (size_t k = 0; k < n; ++k) {
         const ObjIndex& a = face[k % n]; const ObjIndex& b = face[(k + 1) % n]; const ObjIndex& c = face[(k + 2) % n];
-        float e0x = P(b, 0) - P(a, 0), e0y = P(b, 1) - P(a, 1), e0z = P(b, 2) - P(a, 2);
-        float e1x = P(c, 0) - P(b, 0), e1y = P(c, 1) - P(b, 1), e1z = P(c, 2) - P(b, 2);
-        float cx = std::fabs(e0y * e1z - e0z * e1y), cy = std::fabs(e0z * e1x - e0x * e1z), cz = std::fabs(e0x * e1y - e0y * e1x);
+        if (!valid(a, 2) || !valid(b, 2) || !valid(c, 2)) continue;
+        const float e0x = P(b, 0) - P(a, 0), e0y = P(b, 1) - P(a, 1), e0z = P(b, 2) - P(a, 2);
+        const float e1x = P(c, 0) - P(b, 0), e1y = P(c, 1) - P(b, 1), e1z = P(c, 2) - P(b, 2);
+        const float cx = std::fabs(e0y * e1z - e0z * e1y), cy = std::fabs(e0z * e1x - e0x * e1z), cz = std::fabs(e0x * e1y - e0y * e1x);
         const float eps = 1.1920929e-07f;
         if (cx > eps || cy > eps || cz > eps) {
             if (!(cx > cy && cx > cz)) { axes[0] = 0; if (cz > cx && cz > cy) axes[1] = 1; }
@@ -76,7 +204,8 @@ void Triangulate(const std::vector<ObjIndex>& face, const std::vector<float>& v,
     float area = 0.0f;
     for (size_t k = 0; k < n; ++k) {
         const ObjIndex& a = face[k % n]; const ObjIndex& b = face[(k + 1) % n];
-        area += (P(a, (int)axes[0]) * P(b, (int)axes[1]) - P(a, (int)axes[1]) * P(b, (int)axes[0])) * 0.5f;
+        if (!valid(a, axes[0]) || !valid(a, axes[1]) || !valid(b, axes[0]) || !valid(b, axes[1])) continue;
+        area += (P(a, axes[0]) * P(b, axes[1]) - P(a, axes[1]) * P(b, axes[0])) * 0.5f;
     }
     std::vector<ObjIndex> rem = face;
     size_t guess = 0, remainingIterations = rem.size(), previous = rem.size();
@@ -92,66 +221,104 @@ void Triangulate(const std::vector<ObjIndex>& face, const std::vector<float>& v,
         ObjIndex ind[3]; float vx[3], vy[3];
         for (int k = 0; k < 3; ++k) {
             ind[k] = rem[(guess + k) % np];
-            vx[k] = P(ind[k], (int)axes[0]); vy[k] = P(ind[k], (int)axes[1]);
+            const bool ok = valid(ind[k], axes[0]) && valid(ind[k], axes[1]);
+            vx[k] = ok ? P(ind[k], axes[0]) : 0.0f;
+            vy[k] = ok ? P(ind[k], axes[1]) : 0.0f;
         }
-        float e0x = vx[1] - vx[0], e0y = vy[1] - vy[0], e1x = vx[2] - vx[1], e1y = vy[2] - vy[1];
-        float cross = e0x * e1y - e0y * e1x;
+        const float e0x = vx[1] - vx[0], e0y = vy[1] - vy[0], e1x = vx[2] - vx[1], e1y = vy[2] - vy[1];
+        const float cross = e0x * e1y - e0y * e1x;
         if (cross * area < 0.0f) { guess += 1; continue; }
         bool overlap = false;
         for (size_t o = 3; o < np; ++o) {
             const ObjIndex& oi = rem[(guess + o) % np];
-            if (PointInTriangle(vx, vy, P(oi, (int)axes[0]), P(oi, (int)axes[1]))) { overlap = true; break; }
+            if (!valid(oi, axes[0]) || !valid(oi, axes[1])) continue;
+            if (PointInTriangle(vx, vy, P(oi, axes[0]), P(oi, axes[1]))) { overlap = true; break; }
         }
         if (overlap) { guess += 1; continue; }
         emit(ind[0], ind[1], ind[2]);
-        size_t removed = (guess + 1) % np;
-        rem.erase(rem.begin() + (long)removed);
+        rem.erase(rem.begin() + (long)((guess + 1) % np));
     }
     if (rem.size() == 3) emit(rem[0], rem[1], rem[2]);
 }
 
-bool ParseMtl(const std::string& path, std::vector<ObjMaterial>* mats, std::map<std::string, int>* index)
+// ParseTextureNameAndOption (tiny_obj_loader.h:1186-1270): options are skipped, the
+// texture name is the rest of the line
+bool TakeTextureName(const char* tok, std::string* name)
 {
-    std::ifstream in(path);
-    if (!in) return false;
+    bool found = false;
+    auto opt = [&](const char* o) {
+        const size_t n = std::strlen(o);
+        return std::strncmp(tok, o, n) == 0 && Blank(tok[n]);
+    };
+    while (!LineEnd(*tok)) {
+        tok += std::strspn(tok, " \t");
+        if (opt("-blendu") || opt("-blendv")) { tok += 8; tok += std::strspn(tok, " \t"); tok += std::strcspn(tok, " \t\r"); }
+        else if (opt("-clamp")) { tok += 7; tok += std::strspn(tok, " \t"); tok += std::strcspn(tok, " \t\r"); }
+        else if (opt("-boost")) { tok += 7; TakeReal(&tok, 1.0); }
+        else if (opt("-bm")) { tok += 4; TakeReal(&tok, 1.0); }
+        else if (opt("-o") || opt("-s") || opt("-t")) { tok += 3; TakeReal(&tok); TakeReal(&tok); TakeReal(&tok); }
+        else if (opt("-type")) { tok += 5; tok += std::strspn(tok, " \t"); tok += std::strcspn(tok, " \t\r"); }
+        else if (opt("-texres")) { tok += 7; TakeInt(&tok); }
+        else if (opt("-imfchan")) { tok += 9; tok += std::strspn(tok, " \t"); tok += std::strcspn(tok, " \t\r"); }
+        else if (opt("-mm")) { tok += 4; TakeReal(&tok); TakeReal(&tok); }
+        else if (opt("-colorspace")) { tok += 12; TakeWord(&tok); }
+        else { *name = tok; tok += name->size(); found = true; }
+    }
+    return found;
+}
+
+// LoadMtl (tiny_obj_loader.h:1688-2077), the fields the OBJ material translation reads
+// (WavefrontOBJLoading.cpp:305-338): Kd, Ni, Pr, d / Tr, map_Kd, map_d. A material is
+// flushed at the next newmtl when it has a name, and always at the end of the file.
+void ParseMtl(std::istream& in, std::vector<ObjMaterial>* mats, std::map<std::string, int>* index)
+{
+    ObjMaterial cur;
+    bool hasD = false, hasTr = false, hasKd = false;
     std::string line;
-    ObjMaterial* cur = nullptr;
-    bool hasD = false;
-    while (std::getline(in, line)) {
-        std::istringstream ss(line);
-        std::string tag;
-        ss >> tag;
-        if (tag == "newmtl") {
-            std::string name = Trim(line.substr(line.find("newmtl") + 6));
-            mats->emplace_back();
-            cur = &mats->back();
-            cur->name = name;
-            (*index)[name] = (int)mats->size() - 1;
-            hasD = false;
-        } else if (!cur) {
-            continue;
-        } else if (tag == "Kd") {
-            double r = 0, g = 0, b = 0; ss >> r >> g >> b;
-            cur->diffuse[0] = (float)r; cur->diffuse[1] = (float)g; cur->diffuse[2] = (float)b;
-        } else if (tag == "Ni") {
-            double x = 1; ss >> x; cur->ior = (float)x;
-        } else if (tag == "Pr") {
-            double x = 0; ss >> x; cur->roughness = (float)x;
-        } else if (tag == "d") {
-            double x = 1; ss >> x; cur->dissolve = (float)x; hasD = true;
-        } else if (tag == "Tr") {
-            double x = 0; ss >> x; if (!hasD) cur->dissolve = 1.0f - (float)x;
-        } else if (tag == "map_Kd") {
-            std::string rest = Trim(line.substr(line.find("map_Kd") + 6));
-            size_t sp = rest.find_last_of(" \t");
-            cur->diffuseTexname = sp == std::string::npos ? rest : rest.substr(sp + 1);
-        } else if (tag == "map_d") {
-            std::string rest = Trim(line.substr(line.find("map_d") + 5));
-            size_t sp = rest.find_last_of(" \t");
-            cur->alphaTexname = sp == std::string::npos ? rest : rest.substr(sp + 1);
+    auto flush = [&]() {
+        index->insert({ cur.name, (int)mats->size() });
+        mats->push_back(cur);
+    };
+    while (NextLine(in, &line)) {
+        line = line.substr(0, line.find_last_not_of(" \t") + 1);
+        if (!line.empty() && line.back() == '\n') line.pop_back();
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        const char* tok = line.c_str();
+        tok += std::strspn(tok, " \t");
+        if (tok[0] == '\0' || tok[0] == '#') continue;
+        if (std::strncmp(tok, "newmtl", 6) == 0 && Blank(tok[6])) {
+            if (!cur.name.empty()) flush();
+            cur = ObjMaterial();
+            hasD = hasTr = false;
+            cur.name = tok + 7;
+        } else if (tok[0] == 'K' && tok[1] == 'd' && Blank(tok[2])) {
+            tok += 2;
+            for (int k = 0; k < 3; ++k) cur.diffuse[k] = TakeReal(&tok);
+            hasKd = true;
+        } else if (tok[0] == 'N' && tok[1] == 'i' && Blank(tok[2])) {
+            tok += 2;
+            cur.ior = TakeReal(&tok);
+        } else if (tok[0] == 'd' && Blank(tok[1])) {
+            tok += 1;
+            cur.dissolve = TakeReal(&tok);
+            hasD = true;
+        } else if (tok[0] == 'T' && tok[1] == 'r' && Blank(tok[2])) {
+            tok += 2;
+            if (!hasD) cur.dissolve = 1.0f - TakeReal(&tok);
+            hasTr = true;
+        } else if (tok[0] == 'P' && tok[1] == 'r' && Blank(tok[2])) {
+            tok += 2;
+            cur.roughness = TakeReal(&tok);
+        } else if (std::strncmp(tok, "map_Kd", 6) == 0 && Blank(tok[6])) {
+            TakeTextureName(tok + 7, &cur.diffuseTexname);
+            if (!hasKd) cur.diffuse[0] = cur.diffuse[1] = cur.diffuse[2] = 0.6f;
+        } else if (std::strncmp(tok, "map_d", 5) == 0 && Blank(tok[5])) {
+            cur.alphaTexname = tok + 6;
+            TakeTextureName(tok + 6, &cur.alphaTexname);
         }
     }
-    return true;
+    (void)hasTr;
+    flush();
 }
 
 struct CornerKey {
@@ -172,123 +339,158 @@ struct CornerKeyHash {
         return h;
     }
 };
-struct IndexTripleHash {
-    size_t operator()(const std::tuple<int, int, int>& t) const
-    {
-        return std::hash<int>()(std::get<0>(t)) * 73856093u ^ std::hash<int>()(std::get<1>(t)) * 19349663u ^ std::hash<int>()(std::get<2>(t)) * 83492791u;
-    }
-};
 
-// Per-corner tangents for one shape (stand-in for genTangSpaceDefault, WavefrontOBJLoading.cpp:147-153).
-void GenerateTangents(const ObjData& d, const ObjShape& s, bool flipV, std::vector<Float3>* out)
+// Tangents for one shape's triangles through MikkTSpace's interface view of the mesh
+// (WavefrontOBJLoading.cpp:102-153): raw OBJ positions and normals, uv with the V flip,
+// a missing uv reads (0, 0).
+bool ShapeTangents(const ObjData& d, const ObjShape& s, bool flipV, std::vector<Float3>* out)
 {
-    const size_t faces = s.indices.size() / 3;
-    out->assign(faces * 3, Float3(0.0f, 0.0f, 0.0f));
-    std::vector<Float3> faceTangent(faces);
-    auto pos = [&](const ObjIndex& i) { return Float3(d.positions[(size_t)i.v * 3], d.positions[(size_t)i.v * 3 + 1], d.positions[(size_t)i.v * 3 + 2]); };
-    auto uv = [&](const ObjIndex& i) {
-        Float2 t{ 0.0f, 0.0f };
-        if (i.vt >= 0) { t.x = d.texcoords[(size_t)i.vt * 2]; t.y = d.texcoords[(size_t)i.vt * 2 + 1]; if (flipV) t.y = 1.0f - t.y; }
-        return t;
-    };
-    for (size_t f = 0; f < faces; ++f) {
-        const ObjIndex& a = s.indices[f * 3]; const ObjIndex& b = s.indices[f * 3 + 1]; const ObjIndex& c = s.indices[f * 3 + 2];
-        const Float3 e1 = pos(b) - pos(a), e2 = pos(c) - pos(a);
-        const Float2 ta = uv(a), tb = uv(b), tc = uv(c);
-        const float du1 = tb.x - ta.x, dv1 = tb.y - ta.y, du2 = tc.x - ta.x, dv2 = tc.y - ta.y;
-        const float r = du1 * dv2 - du2 * dv1;
-        faceTangent[f] = r != 0.0f ? (e1 * dv2 - e2 * dv1) * (1.0f / r) : Float3(0.0f, 0.0f, 0.0f);
+    const size_t corners = s.indices.size();
+    std::vector<Float3> pos(corners), nrm(corners), uvw(corners);
+    for (size_t c = 0; c < corners; ++c) {
+        const ObjIndex& i = s.indices[c];
+        pos[c] = Float3(d.positions[(size_t)i.v * 3], d.positions[(size_t)i.v * 3 + 1], d.positions[(size_t)i.v * 3 + 2]);
+        nrm[c] = Float3(d.normals[(size_t)i.vn * 3], d.normals[(size_t)i.vn * 3 + 1], d.normals[(size_t)i.vn * 3 + 2]);
+        float u = 0.0f, v = 0.0f;
+        if (i.vt != -1) {
+            u = d.texcoords[(size_t)i.vt * 2];
+            v = d.texcoords[(size_t)i.vt * 2 + 1];
+            if (flipV) v = 1.0f - v;
+        }
+        uvw[c] = Float3(u, v, 1.0f);
     }
-    std::unordered_map<std::tuple<int, int, int>, Float3, IndexTripleHash> acc;
-    for (size_t f = 0; f < faces; ++f)
-        for (int k = 0; k < 3; ++k) {
-            const ObjIndex& i = s.indices[f * 3 + k];
-            Float3& t = acc[std::make_tuple(i.v, i.vn, i.vt)];
-            t = t + faceTangent[f];
-        }
-    for (size_t f = 0; f < faces; ++f)
-        for (int k = 0; k < 3; ++k) {
-            const ObjIndex& i = s.indices[f * 3 + k];
-            Float3 t = acc[std::make_tuple(i.v, i.vn, i.vt)];
-            Float3 n(0.0f, 0.0f, 0.0f);
-            if (i.vn >= 0) n = Float3(d.normals[(size_t)i.vn * 3], d.normals[(size_t)i.vn * 3 + 1], d.normals[(size_t)i.vn * 3 + 2]);
-            const float nl = Length(n);
-            if (nl > 0.0f) { n = n * (1.0f / nl); t = t - n * Dot(t, n); }
-            const float tl = Length(t);
-            (*out)[f * 3 + k] = tl > 0.0f ? t * (1.0f / tl) : Float3(0.0f, 0.0f, 0.0f);
-        }
+    return GenerateMikkTangents(pos, nrm, uvw, out);
 }
 
 }  // namespace
 
 bool ParseObjFile(const std::string& path, ObjData* out, std::string* err)
 {
-    std::ifstream in(path);
+    std::ifstream in(path, std::ios::binary);
     if (!in) { if (err) *err = "cannot open " + path; return false; }
-    const std::string dir = path.find_last_of('/') == std::string::npos ? std::string(".") : path.substr(0, path.find_last_of('/'));
+    // MTL search path: the OBJ's directory (WavefrontOBJLoading.cpp:412), '/' appended
+    std::string baseDir = path.find_last_of('/') == std::string::npos ? std::string() : path.substr(0, path.find_last_of('/'));
+    if (!baseDir.empty() && baseDir.back() != '/') baseDir += '/';
     std::map<std::string, int> materialMap;
     ObjShape shape;
     std::string name;
     int material = -1;
     std::vector<std::vector<ObjIndex>> faces;   // current prim group
     std::vector<int> faceMaterials;
-    auto exportGroup = [&]() {
-        for (size_t i = 0; i < faces.size(); ++i) Triangulate(faces[i], out->positions, faceMaterials[i], &shape);
-        bool had = !faces.empty();
-        faces.clear(); faceMaterials.clear();
+    size_t otherPrims = 0;                      // l / p elements of the current prim group
+    bool shapeHasOther = false;                 // the shape holds exported l / p elements
+    auto exportGroup = [&]() {                  // exportGroupsToShape: false for an empty group
+        if (faces.empty() && otherPrims == 0) return false;
         shape.name = name;
-        return had;
+        shapeHasOther = shapeHasOther || otherPrims != 0;
+        for (size_t i = 0; i < faces.size(); ++i) Triangulate(faces[i], out->positions, faceMaterials[i], &shape);
+        return true;
     };
+    auto clearGroup = [&]() { faces.clear(); faceMaterials.clear(); otherPrims = 0; };
     std::string line;
-    while (std::getline(in, line)) {
+    while (NextLine(in, &line)) {
+        if (!line.empty() && line.back() == '\n') line.pop_back();
         if (!line.empty() && line.back() == '\r') line.pop_back();
-        std::istringstream ss(line);
-        std::string tag;
-        if (!(ss >> tag)) continue;
-        if (tag == "v") {
-            double x = 0, y = 0, z = 0; ss >> x >> y >> z;
-            out->positions.push_back((float)x); out->positions.push_back((float)y); out->positions.push_back((float)z);
-        } else if (tag == "vn") {
-            double x = 0, y = 0, z = 0; ss >> x >> y >> z;
-            out->normals.push_back((float)x); out->normals.push_back((float)y); out->normals.push_back((float)z);
-        } else if (tag == "vt") {
-            double x = 0, y = 0; ss >> x >> y;
-            out->texcoords.push_back((float)x); out->texcoords.push_back((float)y);
-        } else if (tag == "f") {
-            std::vector<ObjIndex> face;
-            std::string tok;
-            while (ss >> tok) {
+        const char* tok = line.c_str();
+        tok += std::strspn(tok, " \t");
+        if (tok[0] == '\0' || tok[0] == '#') continue;
+        const int nv = (int)(out->positions.size() / 3), nvn = (int)(out->normals.size() / 3), nvt = (int)(out->texcoords.size() / 2);
+        if (tok[0] == 'v' && Blank(tok[1])) {
+            tok += 2;
+            for (int k = 0; k < 3; ++k) out->positions.push_back(TakeReal(&tok));
+            continue;
+        }
+        if (tok[0] == 'v' && tok[1] == 'n' && Blank(tok[2])) {
+            tok += 3;
+            for (int k = 0; k < 3; ++k) out->normals.push_back(TakeReal(&tok));
+            continue;
+        }
+        if (tok[0] == 'v' && tok[1] == 't' && Blank(tok[2])) {
+            tok += 3;
+            for (int k = 0; k < 2; ++k) out->texcoords.push_back(TakeReal(&tok));
+            continue;
+        }
+        if ((tok[0] == 'l' || tok[0] == 'p') && Blank(tok[1])) {
+            tok += 2;
+            while (!LineEnd(tok[0])) {
                 ObjIndex idx;
-                if (!ParseCorner(tok, (int)out->positions.size() / 3, (int)out->normals.size() / 3, (int)out->texcoords.size() / 2, &idx)) {
+                if (!TakeCorner(&tok, nv, nvn, nvt, &idx)) {
+                    if (err) *err = "bad line/point element: " + line;
+                    return false;
+                }
+                tok += std::strspn(tok, " \t\r");
+            }
+            ++otherPrims;
+            continue;
+        }
+        if (tok[0] == 'f' && Blank(tok[1])) {
+            tok += 2;
+            tok += std::strspn(tok, " \t");
+            std::vector<ObjIndex> face;
+            while (!LineEnd(tok[0])) {
+                ObjIndex idx;
+                if (!TakeCorner(&tok, nv, nvn, nvt, &idx)) {
                     if (err) *err = "bad face line: " + line;
                     return false;
                 }
                 face.push_back(idx);
+                tok += std::strspn(tok, " \t\r");
             }
-            faces.push_back(face);
+            faces.push_back(std::move(face));
             faceMaterials.push_back(material);
-        } else if (tag == "usemtl") {
-            std::string mname = Trim(line.substr(line.find("usemtl") + 6));
+            continue;
+        }
+        if (std::strncmp(tok, "usemtl", 6) == 0) {
+            tok += 6;
+            const std::string mname = TakeWord(&tok);
             auto it = materialMap.find(mname);
-            int newId = it == materialMap.end() ? -1 : it->second;
+            const int newId = it == materialMap.end() ? -1 : it->second;
             if (newId != material) {
                 exportGroup();
+                faces.clear(); faceMaterials.clear();
                 material = newId;
             }
-        } else if (tag == "mtllib") {
-            std::string file = Trim(line.substr(line.find("mtllib") + 6));
-            const std::string full = (!file.empty() && file[0] == '/') ? file : dir + "/" + file;
-            ParseMtl(full, &out->materials, &materialMap);
-        } else if (tag == "g" || tag == "o") {
+            continue;
+        }
+        if (std::strncmp(tok, "mtllib", 6) == 0 && Blank(tok[6])) {
+            std::stringstream names(std::string(tok + 7));
+            std::string file;
+            while (std::getline(names, file, ' ')) {
+                // MaterialFileReader: the search path joined with the name as written
+                const std::string full = baseDir.empty() ? file : baseDir + file;
+                std::ifstream mtl(full, std::ios::binary);
+                if (mtl) { ParseMtl(mtl, &out->materials, &materialMap); break; }
+            }
+            continue;
+        }
+        if (tok[0] == 'g' && Blank(tok[1])) {
             exportGroup();
             if (!shape.indices.empty()) out->shapes.push_back(shape);
             shape = ObjShape();
-            std::string rest = line.size() > 1 ? Trim(line.substr(1)) : std::string();
-            name = rest;
+            shapeHasOther = false;
+            clearGroup();
+            std::vector<std::string> names;
+            while (!LineEnd(tok[0])) {
+                names.push_back(TakeWord(&tok));
+                tok += std::strspn(tok, " \t\r");
+            }
+            name.clear();
+            for (size_t i = 1; i < names.size(); ++i) name += (i > 1 ? " " : "") + names[i];
+            continue;
         }
+        if (tok[0] == 'o' && Blank(tok[1])) {
+            exportGroup();
+            if (!shape.indices.empty() || shapeHasOther) out->shapes.push_back(shape);
+            clearGroup();
+            shape = ObjShape();
+            shapeHasOther = false;
+            name = tok + 2;
+            continue;
+        }
+        // vw, t, s and unknown statements carry nothing the loader reads
     }
-    bool had = exportGroup();
-    if (had || !shape.indices.empty()) out->shapes.push_back(shape);
+    const bool exported = exportGroup();
+    if (exported || !shape.indices.empty()) out->shapes.push_back(shape);
     return true;
 }
 
@@ -303,7 +505,15 @@ bool CreateMeshFromObjData(const ObjData& d, const ObjShape* shapes, uint32_t sh
     std::vector<Float3> tangents;
     for (uint32_t s = 0; s < shapeCount; ++s) {
         const ObjShape& shape = shapes[s];
-        GenerateTangents(d, shape, params.flipTexcoordV, &tangents);
+        // a corner without position or normal fails the mesh (:212-213); the reference
+        // reads such corners' attributes out of bounds in MikkTSpace first, so they and
+        // out-of-range indices are refused before any attribute is read
+        for (const ObjIndex& idx : shape.indices)
+            if (idx.v < 0 || idx.vn < 0 || (size_t)idx.v * 3 + 2 >= d.positions.size() ||
+                (size_t)idx.vn * 3 + 2 >= d.normals.size() || (idx.vt >= 0 && (size_t)idx.vt * 2 + 1 >= d.texcoords.size()))
+                return false;
+        // a shape MikkTSpace refuses (no triangles) is skipped (WavefrontOBJLoading.cpp:195-199)
+        if (!ShapeTangents(d, shape, params.flipTexcoordV, &tangents)) continue;
         const size_t faces = shape.indices.size() / 3;
         for (size_t f = 0; f < faces; ++f) {
             const int mat = shape.materialIds[f];

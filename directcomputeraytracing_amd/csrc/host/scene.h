@@ -176,5 +176,9 @@ void TranslateObjMaterials(const ObjData& data, int32_t textureIndexBase, std::v
                            std::vector<std::string>* textureNames);
 bool LoadMitsubaXML(CScene* scene, const std::string& path);
 bool LoadTextureFile(const std::string& path, CTexture* out);
+// MikkTSpace genTangSpaceDefault over a triangle list given per corner (3 per triangle;
+// texcoords carry z = 1); false for an empty list (tangent_space.cpp).
+bool GenerateMikkTangents(const std::vector<Float3>& positions, const std::vector<Float3>& normals,
+                          const std::vector<Float3>& texcoords, std::vector<Float3>* out);
 
 }  // namespace dcrt

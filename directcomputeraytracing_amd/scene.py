@@ -193,3 +193,40 @@ def build_blas(vertices: np.ndarray, indices: np.ndarray) -> dict:
           "BuildBLAS")
     return {"nodes": nodes[:count.value], "indices": reordered.reshape(-1, 3), "triangles": tri_map,
             "max_depth": depth.value, "max_stack_size": stack.value}
+
+
+def load_obj_meshes(path, scene_layout: bool = True, material_index_base: int = 0) -> dict:
+    """OBJ -> meshes before any BVH build (WavefrontOBJLoading.cpp:155-465) through
+    ``dcrt_obj_load``: ``scene_layout`` gives the per-shape meshes of
+    CScene::LoadFromWavefrontOBJFile (RH->LH), otherwise the one merged mesh the XML
+    loader builds. Returns {"meshes": [{"vertices" (N, 11) f32, "indices" (T, 3) u32,
+    "material_ids" (T,) u32}], "materials": [{"albedo", "ior", "roughness", "opacity",
+    "albedo_texture_index", "opacity_texture_index"}]} (copies)."""
+    lib = _abi.load_library()
+    h = C.c_void_p()
+    check(lib.dcrt_obj_load(str(path).encode(), _abi.OBJ_SCENE_LAYOUT if scene_layout else 0,
+                            material_index_base, C.byref(h)), f"dcrt_obj_load({path})")
+    try:
+        n = C.c_uint32()
+        check(lib.dcrt_obj_mesh_count(h, C.byref(n)))
+        meshes = []
+        for i in range(n.value):
+            m = _abi.ObjMesh()
+            check(lib.dcrt_obj_get_mesh(h, i, C.byref(m)))
+            nv, nt = m.vertex_count, m.triangle_count
+            verts = np.ctypeslib.as_array(C.cast(m.vertices, C.POINTER(C.c_float)), (nv * 11,)).reshape(nv, 11).copy() \
+                if nv else np.zeros((0, 11), np.float32)
+            idx = np.ctypeslib.as_array(m.indices, (nt * 3,)).reshape(nt, 3).copy() if nt else np.zeros((0, 3), np.uint32)
+            mat = np.ctypeslib.as_array(m.material_ids, (nt,)).copy() if nt else np.zeros(0, np.uint32)
+            meshes.append({"vertices": verts, "indices": idx, "material_ids": mat})
+        check(lib.dcrt_obj_material_count(h, C.byref(n)))
+        materials = []
+        for i in range(n.value):
+            mt = _abi.ObjMaterial()
+            check(lib.dcrt_obj_get_material(h, i, C.byref(mt)))
+            materials.append({"albedo": tuple(mt.albedo), "ior": mt.ior, "roughness": mt.roughness,
+                              "opacity": mt.opacity, "albedo_texture_index": mt.albedo_texture_index,
+                              "opacity_texture_index": mt.opacity_texture_index})
+        return {"meshes": meshes, "materials": materials}
+    finally:
+        lib.dcrt_obj_free(h)

@@ -327,6 +327,34 @@ DCRT_API int dcrt_bvh_build_blas(const dcrt_vertex* vertices, const uint32_t* in
                                  uint32_t* out_reordered_indices, uint32_t* out_reordered_triangles,
                                  uint32_t* out_max_depth, uint32_t* out_max_stack_size);
 
+/* OBJ loading into meshes, before any BVH build:
+ *  - DCRT_OBJ_SCENE_LAYOUT: the meshes CScene::LoadFromWavefrontOBJFile builds
+ *    (WavefrontOBJLoading.cpp:409-465): one mesh per OBJ shape, RH->LH transform
+ *    (x negated), winding change, V flip, material ids offset by material_index_base;
+ *  - 0: Mesh::LoadFromWavefrontOBJFile as the XML loader calls it
+ *    (SceneXMLLoading.cpp:1334-1341): every shape into one mesh, no transform.
+ * Vertices carry the MikkTSpace tangents (WavefrontOBJLoading.cpp:147-153). */
+#define DCRT_OBJ_SCENE_LAYOUT 1u
+typedef struct dcrt_obj_meshes dcrt_obj_meshes;
+typedef struct dcrt_obj_mesh {
+    const dcrt_vertex* vertices;
+    uint32_t vertex_count;
+    const uint32_t* indices;          /* 3 per triangle                         */
+    const uint32_t* material_ids;     /* 1 per triangle (0xFFFFFFFF = none)      */
+    uint32_t triangle_count;
+} dcrt_obj_mesh;
+/* The translated OBJ materials (WavefrontOBJLoading.cpp:305-338) of a load. */
+typedef struct dcrt_obj_material {
+    float albedo[3], ior, roughness, opacity;
+    int32_t albedo_texture_index, opacity_texture_index;
+} dcrt_obj_material;
+DCRT_API int dcrt_obj_load(const char* path, uint32_t flags, uint32_t material_index_base, dcrt_obj_meshes** out);
+DCRT_API int dcrt_obj_mesh_count(const dcrt_obj_meshes* meshes, uint32_t* out_count);
+DCRT_API int dcrt_obj_get_mesh(const dcrt_obj_meshes* meshes, uint32_t index, dcrt_obj_mesh* out_mesh);
+DCRT_API int dcrt_obj_material_count(const dcrt_obj_meshes* meshes, uint32_t* out_count);
+DCRT_API int dcrt_obj_get_material(const dcrt_obj_meshes* meshes, uint32_t index, dcrt_obj_material* out_material);
+DCRT_API void dcrt_obj_free(dcrt_obj_meshes* meshes);
+
 /* ===== tracer: CWavefrontPathTracer on MI355X ============================== */
 DCRT_API int dcrt_tracer_create(const dcrt_tracer_config* config, dcrt_tracer** out_tracer);  /* Create()  */
 DCRT_API void dcrt_tracer_destroy(dcrt_tracer* tracer);                                        /* Destroy() */
