@@ -174,6 +174,9 @@ SIGNATURES = [
     ("dcrt_bvh_build_blas", _I, [C.POINTER(Vertex), C.POINTER(C.c_uint32), _U, C.POINTER(BVHNode),
                                  C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    ("dcrt_scene_get_content_counts", _I, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    ("dcrt_scene_get_loaded_mesh", _I, [_P, _U, C.POINTER(ObjMesh)]),
+    ("dcrt_scene_get_instance", _I, [_P, _U, C.POINTER(C.c_uint32), _FP]),
     ("dcrt_obj_load", _I, [C.c_char_p, _U, _U, C.POINTER(_P)]),
     ("dcrt_obj_mesh_count", _I, [_P, C.POINTER(C.c_uint32)]),
     ("dcrt_obj_get_mesh", _I, [_P, _U, C.POINTER(ObjMesh)]),

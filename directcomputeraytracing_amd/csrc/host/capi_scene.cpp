@@ -17,6 +17,7 @@ void SetLastError(const std::string& s) { g_lastError = s; }
 
 struct dcrt_scene {
     dcrt::CScene scene;
+    std::vector<uint32_t> loadedIndices, loadedMaterialIds;   // dcrt_scene_get_loaded_mesh's buffers
 };
 
 using dcrt::SetLastError;
@@ -265,6 +266,47 @@ DCRT_API int dcrt_bvh_build_blas(const dcrt_vertex* vertices, const uint32_t* in
     if (out_max_stack_size) *out_max_stack_size = r.maxStackSize;
     return DCRT_OK;
     DCRT_GUARD_END
+}
+
+DCRT_API int dcrt_scene_get_content_counts(const dcrt_scene* s, uint32_t* meshes, uint32_t* instances)
+{
+    if (!s || !meshes || !instances) return DCRT_E_INVALID_ARG;
+    *meshes = (uint32_t)s->scene.meshes.size();
+    *instances = (uint32_t)s->scene.meshInstances.size();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_loaded_mesh(dcrt_scene* s, uint32_t index, dcrt_obj_mesh* out)
+{
+    if (!s || !out || index >= s->scene.meshes.size()) return DCRT_E_INVALID_ARG;
+    DCRT_GUARD_BEGIN
+    const dcrt::Mesh& m = s->scene.meshes[index];
+    const uint32_t n = m.GetTriangleCount();
+    if (m.bvhTriangleOrder.size() != n) { SetLastError("mesh has no BVH yet"); return DCRT_E_NO_SCENE; }
+    s->loadedIndices.assign((size_t)n * 3, 0);
+    s->loadedMaterialIds.assign(n, 0);
+    for (uint32_t t = 0; t < n; ++t) {   // BVH position t holds load-order triangle order[t]
+        const uint32_t src = m.bvhTriangleOrder[t];
+        for (int k = 0; k < 3; ++k) s->loadedIndices[(size_t)src * 3 + k] = m.indices[(size_t)t * 3 + k];
+        s->loadedMaterialIds[src] = m.materialIds[t];
+    }
+    out->vertices = m.vertices.data();
+    out->vertex_count = (uint32_t)m.vertices.size();
+    out->indices = s->loadedIndices.data();
+    out->material_ids = s->loadedMaterialIds.data();
+    out->triangle_count = n;
+    return DCRT_OK;
+    DCRT_GUARD_END
+}
+
+DCRT_API int dcrt_scene_get_instance(const dcrt_scene* s, uint32_t index, uint32_t* mesh, float transform[12])
+{
+    if (!s || !mesh || !transform || index >= s->scene.meshInstances.size()) return DCRT_E_INVALID_ARG;
+    *mesh = s->scene.meshInstances[index].meshIndex;
+    const dcrt::Float4x3& t = s->scene.instanceTransforms[index];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 3; ++c) transform[r * 3 + c] = t.m[r][c];
+    return DCRT_OK;
 }
 
 // ---- OBJ meshes before the BVH build (WavefrontOBJLoading.cpp:155-263,374-465)

@@ -40,6 +40,7 @@ void Mesh::BuildBVH(std::vector<uint32_t>* reordered)
     bvhMaxStackSize = result.maxStackSize;
     std::vector<uint32_t> ids = materialIds;
     for (size_t i = 0; i < ids.size(); ++i) materialIds[i] = ids[(*reordered)[i]];
+    bvhTriangleOrder = *reordered;
 }
 
 bool Mesh::GenerateRectangle(uint32_t materialId, bool applyTransform, const Float4x4& transform)

@@ -49,6 +49,7 @@ struct Mesh {
     uint32_t bvhMaxDepth = 0;
     uint32_t bvhMaxStackSize = 0;
     std::vector<uint32_t> materialIds;
+    std::vector<uint32_t> bvhTriangleOrder;   // BVH position -> load-order triangle (BuildBLAS output)
 
     uint32_t GetTriangleCount() const { return (uint32_t)indices.size() / 3; }
     void BuildBVH(std::vector<uint32_t>* reorderedTriangleIndices);   // Mesh.cpp:59-79

@@ -142,6 +142,29 @@ class Scene:
         check(self._lib.dcrt_scene_get_frame_params(self._h, int(frame_seed), C.byref(p)), "GetFrameParams")
         return p
 
+    def loaded_content(self):
+        """Meshes and instances as loaded, before the BVH build reordered them (the inputs
+        of Mesh::BuildBVH / BuildTLAS, Scene.cpp:160-215): ([{"vertices", "indices",
+        "material_ids"}], [(mesh_index, (4, 3) transform)]), copies."""
+        nm, ni = C.c_uint32(), C.c_uint32()
+        check(self._lib.dcrt_scene_get_content_counts(self._h, C.byref(nm), C.byref(ni)))
+        meshes = []
+        for i in range(nm.value):
+            m = _abi.ObjMesh()
+            check(self._lib.dcrt_scene_get_loaded_mesh(self._h, i, C.byref(m)), "GetLoadedMesh")
+            nv, nt = m.vertex_count, m.triangle_count
+            meshes.append({
+                "vertices": np.ctypeslib.as_array(C.cast(m.vertices, C.POINTER(C.c_float)), (nv * 11,)).reshape(nv, 11).copy(),
+                "indices": np.ctypeslib.as_array(m.indices, (nt * 3,)).reshape(nt, 3).copy(),
+                "material_ids": np.ctypeslib.as_array(m.material_ids, (nt,)).copy()})
+        instances = []
+        for j in range(ni.value):
+            mesh = C.c_uint32()
+            t = (C.c_float * 12)()
+            check(self._lib.dcrt_scene_get_instance(self._h, j, C.byref(mesh), t))
+            instances.append((mesh.value, np.array(t[:], np.float32).reshape(4, 3)))
+        return meshes, instances
+
     # ---- numpy views of the flattened buffers (valid until the scene changes)
     def arrays(self) -> dict:
         f = self.flat()

@@ -319,6 +319,17 @@ DCRT_API int dcrt_scene_get_frame_params(const dcrt_scene* scene, uint32_t frame
 DCRT_API int dcrt_scene_get_bvh_info(const dcrt_scene* scene, uint32_t* tlas_nodes, uint32_t* total_nodes,
                                      uint32_t* max_stack_size);
 
+/* The scene content as loaded, before BVHAccel reordered it -- the inputs of
+ * Mesh::BuildBVH / BuildTLAS (Mesh.cpp:59-79, Scene.cpp:160-215): mesh i's vertices,
+ * triangles (mesh-local vertex indices) and material ids in load order; instance j's
+ * mesh index and XMFLOAT4X3 transform (4 rows of 3) in load order. Pointers stay valid
+ * until the scene changes. Used to check the BVH build against an independent one. */
+typedef struct dcrt_obj_mesh dcrt_obj_mesh;
+DCRT_API int dcrt_scene_get_content_counts(const dcrt_scene* scene, uint32_t* out_meshes, uint32_t* out_instances);
+DCRT_API int dcrt_scene_get_loaded_mesh(dcrt_scene* scene, uint32_t mesh, dcrt_obj_mesh* out_mesh);
+DCRT_API int dcrt_scene_get_instance(const dcrt_scene* scene, uint32_t instance, uint32_t* out_mesh_index,
+                                     float out_transform[12]);
+
 /* Standalone BVHAccel::BuildBLAS + PackBVH over one triangle soup
  * (BVHAccel.cpp:376-447). out_nodes holds 2*triangle_count-1 entries at most;
  * out_reordered_indices 3*triangle_count; out_reordered_triangles triangle_count. */
@@ -336,13 +347,13 @@ DCRT_API int dcrt_bvh_build_blas(const dcrt_vertex* vertices, const uint32_t* in
  * Vertices carry the MikkTSpace tangents (WavefrontOBJLoading.cpp:147-153). */
 #define DCRT_OBJ_SCENE_LAYOUT 1u
 typedef struct dcrt_obj_meshes dcrt_obj_meshes;
-typedef struct dcrt_obj_mesh {
+struct dcrt_obj_mesh {
     const dcrt_vertex* vertices;
     uint32_t vertex_count;
     const uint32_t* indices;          /* 3 per triangle                         */
     const uint32_t* material_ids;     /* 1 per triangle (0xFFFFFFFF = none)      */
     uint32_t triangle_count;
-} dcrt_obj_mesh;
+};
 /* The translated OBJ materials (WavefrontOBJLoading.cpp:305-338) of a load. */
 typedef struct dcrt_obj_material {
     float albedo[3], ior, roughness, opacity;

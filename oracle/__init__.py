@@ -80,8 +80,111 @@ def load():
                                          P(C.c_uint8)]
     lib.oracle_math_eval.restype = None
     lib.oracle_math_eval.argtypes = [C.c_int, P(C.c_float), U, P(C.c_float)]
+    lib.oracle_bvh_build_blas.restype = C.c_int
+    lib.oracle_bvh_build_blas.argtypes = [P(A.Vertex), P(U), U, P(OracleBVHNode), P(U), P(U), P(U), P(U), P(U)]
+    lib.oracle_bvh_build_tlas.restype = C.c_int
+    lib.oracle_bvh_build_tlas.argtypes = [P(C.c_float), P(C.c_float), U, P(OracleBVHNode), P(U), P(U), P(U), P(U), P(U)]
+    lib.oracle_bvh_pack.restype = None
+    lib.oracle_bvh_pack.argtypes = [P(OracleBVHNode), U, C.c_int, P(A.BVHNode), U, U]
     _lib = lib
     return lib
+
+
+class OracleBVHNode(C.Structure):
+    _fields_ = [("center", C.c_float * 3), ("extents", C.c_float * 3), ("child_or_prim", C.c_uint32),
+                ("count_or_instance", C.c_uint32), ("is_leaf", C.c_uint32), ("split_axis", C.c_uint32)]
+
+
+_NODE_DTYPE = np.dtype([("center", np.float32, 3), ("extents", np.float32, 3), ("child_or_prim", np.uint32),
+                        ("count_or_instance", np.uint32), ("is_leaf", np.uint32), ("split_axis", np.uint32)])
+
+
+def build_blas(vertices, indices):
+    """BVHAccel::BuildBLAS (BVHAccel.cpp:376-394), independent C restatement:
+    vertices (N, 11) f32 dcrt_vertex rows, indices (T, 3). Returns the unpacked nodes
+    (structured array), BVH-ordered index triples, tri_order[new] = old, depth, stack."""
+    lib = load()
+    from directcomputeraytracing_amd import _abi as A
+    v = np.ascontiguousarray(vertices, np.float32)
+    idx = np.ascontiguousarray(indices, np.uint32).reshape(-1)
+    n = idx.size // 3
+    nodes = np.zeros(max(1, 2 * n), _NODE_DTYPE)
+    out_idx = np.zeros(idx.size, np.uint32)
+    order = np.zeros(n, np.uint32)
+    cnt, depth, stack = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    rc = lib.oracle_bvh_build_blas(v.ctypes.data_as(C.POINTER(A.Vertex)), _up(idx), n,
+                                   nodes.ctypes.data_as(C.POINTER(OracleBVHNode)), C.byref(cnt), _up(out_idx),
+                                   _up(order), C.byref(depth), C.byref(stack))
+    if rc != 0:
+        raise ValueError("oracle_bvh_build_blas: empty mesh")
+    return {"nodes": nodes[:cnt.value].copy(), "indices": out_idx.reshape(-1, 3), "order": order,
+            "max_depth": depth.value, "max_stack_size": stack.value}
+
+
+def pack_bvh(nodes, is_blas, node_offset=0, prim_offset=0):
+    """BVHAccel::PackBVH (BVHAccel.cpp:413-447) -> (N, 8) uint32 (the 32-B GPU node)."""
+    lib = load()
+    from directcomputeraytracing_amd import _abi as A
+    nodes = np.ascontiguousarray(nodes, _NODE_DTYPE)
+    out = np.zeros((len(nodes), 8), np.uint32)
+    lib.oracle_bvh_pack(nodes.ctypes.data_as(C.POINTER(OracleBVHNode)), len(nodes), int(is_blas),
+                        out.ctypes.data_as(C.POINTER(A.BVHNode)), node_offset, prim_offset)
+    return out
+
+
+def build_scene_bvh(meshes, instances):
+    """The BVH half of CScene::LoadFromFile (Scene.cpp:160-215, 337-421, 431-434): BLAS
+    per mesh, TLAS over the instances' transformed BLAS-root boxes, the TLAS leaves
+    patched to their BLAS roots and instance numbers, everything packed.
+
+    meshes: [{"vertices" (N, 11), "indices" (T, 3) load order, "material_ids" (T,)}];
+    instances: [(mesh_index, transform (4, 3) XMFLOAT4X3)] in load order.
+    Returns nodes (N, 8) u32, triangles (T, 3) u32 (global vertex indices),
+    material_ids, instance_order (reordered -> original), stack_size and the forward
+    instance transforms (I, 12) as Scene.cpp:429-434 stores them."""
+    lib = load()
+    blas = [build_blas(m["vertices"], m["indices"]) for m in meshes]
+    ni = len(instances)
+    boxes = np.zeros((ni, 6), np.float32)
+    xf = np.zeros((ni, 12), np.float32)
+    for i, (mesh, t) in enumerate(instances):
+        root = blas[mesh]["nodes"][0]
+        boxes[i, :3], boxes[i, 3:] = root["center"], root["extents"]
+        xf[i] = np.asarray(t, np.float32).reshape(12)
+    tnodes = np.zeros(max(1, 2 * ni), _NODE_DTYPE)
+    order = np.zeros(ni, np.uint32)
+    depths = np.zeros(ni, np.uint32)
+    cnt, depth, stack = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    if lib.oracle_bvh_build_tlas(_fp(boxes), _fp(xf), ni, tnodes.ctypes.data_as(C.POINTER(OracleBVHNode)), C.byref(cnt),
+                                 _up(order), C.byref(depth), C.byref(stack), _up(depths)) != 0:
+        raise ValueError("oracle_bvh_build_tlas: no instances")
+    tlas = tnodes[:cnt.value].copy()
+    stack_size = max(int(depths[r]) + blas[instances[int(order[r])][0]]["max_depth"] for r in range(ni))
+    parts, blas_offsets = [], []
+    node_offset, tri_offset = len(tlas), 0
+    for m, b in zip(meshes, blas):
+        parts.append(pack_bvh(b["nodes"], True, node_offset, tri_offset))
+        blas_offsets.append(node_offset)
+        node_offset += len(b["nodes"])
+        tri_offset += len(m["indices"])
+    for node in tlas:
+        if node["count_or_instance"] > 0:   # a leaf: its instance's BLAS root and number
+            prim = int(node["child_or_prim"])
+            node["child_or_prim"] = blas_offsets[instances[int(order[prim])][0]]
+            node["count_or_instance"] = prim
+    nodes = np.concatenate([pack_bvh(tlas, False)] + parts)
+    tris, mats, voff = [], [], 0
+    for m, b in zip(meshes, blas):
+        tris.append(b["indices"].astype(np.uint32) + np.uint32(voff))
+        mats.append(np.asarray(m["material_ids"], np.uint32)[b["order"]])
+        voff += len(m["vertices"])
+    fwd = np.zeros((ni, 12), np.float32)
+    for r in range(ni):
+        t = xf[int(order[r])].reshape(4, 3)
+        fwd[r] = t.T.reshape(12)     # XMFLOAT4X3(_11, _21, _31, _41, _12, ...)
+    return {"nodes": nodes, "triangles": np.concatenate(tris) if tris else np.zeros((0, 3), np.uint32),
+            "material_ids": np.concatenate(mats) if mats else np.zeros(0, np.uint32), "instance_order": order,
+            "stack_size": stack_size, "forward_transforms": fwd, "tlas_node_count": len(tlas)}
 
 
 def _fp(a):
@@ -216,3 +319,34 @@ def resolve_image(film, params, thresholds):
 def sum_log_luminance(film):
     film = np.ascontiguousarray(film, np.float32)
     return load().oracle_sum_log_luminance(_fp(film), film.shape[1], film.shape[0])
+
+
+def flat_with_own_bvh(scene):
+    """The product's flat scene with the BVH half replaced by the oracle's own build
+    (build_scene_bvh over the scene's loaded meshes and instances): nodes, triangles,
+    material ids, stack size. Per-instance arrays (inverse transforms -- DirectXMath's
+    XMMatrixInverse is parity unpinned -- flags, overrides, light indices) are taken from
+    the product after checking that both builds order the instances identically. The
+    returned FlatScene keeps its arrays alive."""
+    from directcomputeraytracing_amd import _abi as A
+    meshes, instances = scene.loaded_content()
+    own = build_scene_bvh(meshes, instances)
+    src = scene.flat()
+    n = src.instance_count
+    fwd = np.ctypeslib.as_array(C.cast(src.instance_transforms, C.POINTER(C.c_float)), (n * 12,)).reshape(n, 12)
+    if not np.array_equal(fwd.view(np.uint32), own["forward_transforms"].view(np.uint32)):
+        raise AssertionError("instance order differs between the product and the oracle BVH build")
+    keep = {"nodes": np.ascontiguousarray(own["nodes"], np.uint32),
+            "triangles": np.ascontiguousarray(own["triangles"], np.uint32),
+            "material_ids": np.ascontiguousarray(own["material_ids"], np.uint32)}
+    f = A.FlatScene()
+    C.pointer(f)[0] = src
+    f.triangles = keep["triangles"].ctypes.data_as(C.POINTER(C.c_uint32))
+    f.triangle_count = keep["triangles"].shape[0]
+    f.bvh_nodes = keep["nodes"].ctypes.data_as(C.POINTER(A.BVHNode))
+    f.bvh_node_count = keep["nodes"].shape[0]
+    f.tlas_node_count = own["tlas_node_count"]
+    f.material_ids = keep["material_ids"].ctypes.data_as(C.POINTER(C.c_uint32))
+    f.bvh_traversal_stack_size = own["stack_size"]
+    f._keep = (keep, scene)
+    return f

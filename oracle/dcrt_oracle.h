@@ -79,6 +79,29 @@ float oracle_sum_log_luminance(const float* film_rgba, uint32_t width, uint32_t 
 void oracle_resolve_image(const float* film_rgba, uint32_t width, uint32_t height, int enabled, int auto_exposure, float ev100,
                           float luminance_white, const float* srgb_thresholds, uint8_t* out_rgba8);
 
+/* ---- BVH build (dcrt_oracle_bvh.c, BVHAccel.cpp:76-447) ---------------------- */
+/* BVHAccel::BVHNode before packing: center/extents box, child or first primitive,
+ * primitive count (TLAS leaves: count until the scene patches in the instance). */
+typedef struct oracle_bvh_node {
+    float center[3], extents[3];
+    uint32_t child_or_prim;
+    uint32_t count_or_instance;
+    uint32_t is_leaf;
+    uint32_t split_axis;
+} oracle_bvh_node;
+/* BuildBLAS over one mesh: nodes (capacity 2 * tri_count - 1), BVH-ordered index
+ * triples, tri_order[new] = load-order triangle; maxDepth / maxStackSize. */
+int oracle_bvh_build_blas(const dcrt_vertex* vertices, const uint32_t* indices, uint32_t tri_count, oracle_bvh_node* nodes,
+                          uint32_t* node_count, uint32_t* reordered_indices, uint32_t* tri_order, uint32_t* max_depth,
+                          uint32_t* max_stack);
+/* BuildTLAS over instance boxes (BLAS root center+extents, 6 floats) and XMFLOAT4X3
+ * transforms (12 floats, 4 rows of 3). */
+int oracle_bvh_build_tlas(const float* blas_root_boxes, const float* transforms, uint32_t instance_count,
+                          oracle_bvh_node* nodes, uint32_t* node_count, uint32_t* instance_order, uint32_t* max_depth,
+                          uint32_t* max_stack, uint32_t* instance_depths);
+void oracle_bvh_pack(const oracle_bvh_node* nodes, uint32_t count, int is_blas, dcrt_bvh_node* out, uint32_t node_offset,
+                     uint32_t prim_offset);
+
 #ifdef __cplusplus
 }
 #endif

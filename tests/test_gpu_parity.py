@@ -5,6 +5,10 @@ bit-exact; the float outputs are also required bit-exact here because both
 sides compile without contraction and with IEEE div/sqrt and share the same
 deterministic transcendentals (DESIGN.md "Numerics"). Where a float
 comparison is not bit-exact the tolerance is stated in the assertion.
+
+The oracle side renders the scene with its OWN BVH (oracle.flat_with_own_bvh: the
+oracle's independent BVHAccel restatement over the scene's loaded meshes, see
+tests/test_bvh_pin.py), not with the product's flattened nodes and triangles.
 """
 import numpy as np
 import pytest
@@ -63,7 +67,7 @@ def test_bxdf_luts_match_golden(gpu_tracer, golden_luts, oracle_mod):
 def test_trace_rays_bit_exact(gpu_tracer, golden_luts, oracle_mod, features):
     s = cornell(64, 64, 2)
     gpu_tracer.on_scene_loaded(s)
-    flat = s.flat()
+    flat = oracle_mod.flat_with_own_bvh(s)
     for room in (True, False):
         rays = _rays(50000, 11 + features + room, room)
         h_gpu = gpu_tracer.trace_rays(rays, features)
@@ -77,7 +81,7 @@ def test_trace_rays_bit_exact(gpu_tracer, golden_luts, oracle_mod, features):
 def _render_and_compare(tracer, oracle_mod, luts, scene, seeds):
     tracer.set_luts(luts)
     tracer.on_scene_loaded(scene)
-    flat = scene.flat()
+    flat = oracle_mod.flat_with_own_bvh(scene)
     for seed in seeds:
         fr = scene.frame_params(seed)
         tracer.set_frame_params(fr)
@@ -167,7 +171,7 @@ def test_film_accumulation_matches_oracle(native_lib, golden_luts, oracle_mod):
         s = cornell(96, 64, 3)
         t.set_luts(golden_luts)
         t.on_scene_loaded(s)
-        flat = s.flat()
+        flat = oracle_mod.flat_with_own_bvh(s)
         for filt in (FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3),
                      FilterParams(FILTER_GAUSSIAN, 1.5, 2.0, 1 / 3, 1 / 3, 3),
                      FilterParams(FILTER_MITCHELL, 2.0, 1.5, 1 / 3, 1 / 3, 3)):
@@ -196,7 +200,7 @@ def test_film_radius_just_below_half_integer(native_lib, golden_luts, oracle_mod
         s = cornell(150, 70, 2)
         t.set_luts(golden_luts)
         t.on_scene_loaded(s)
-        flat = s.flat()
+        flat = oracle_mod.flat_with_own_bvh(s)
         for filt in (FilterParams(FILTER_BOX, below(1.5), 1.5, 1 / 3, 1 / 3, 3),
                      FilterParams(FILTER_TRIANGLE, below(1.5), 1.5, 1 / 3, 1 / 3, 3),
                      FilterParams(FILTER_GAUSSIAN, below(2.5), 2.0, 1 / 3, 1 / 3, 3),
@@ -310,7 +314,7 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
             t.destroy()
     for f in films[1:]:
         assert same_bits(f, films[0]).all()
-    p_ref, v_ref, _, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(7), oracle_mod.WAVEFRONT)
+    p_ref, v_ref, _, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(7), oracle_mod.WAVEFRONT)
     for pos, val in samples:
         assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
@@ -362,7 +366,7 @@ def test_tiny_pool_renders_every_pixel(native_lib, golden_luts, oracle_mod):
         pos, val = t.read_samples()
     finally:
         t.destroy()
-    p_ref, v_ref, _, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(4), oracle_mod.WAVEFRONT)
+    p_ref, v_ref, _, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(4), oracle_mod.WAVEFRONT)
     assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
 
@@ -394,7 +398,7 @@ def test_traversal_counters_match_oracle(native_lib, golden_luts, oracle_mod):
         t.render_images(2, 1)
         st = t.traversal_stats()
         c = t.counters()
-        _, _, _, ref = oracle_mod.render(s.flat(), golden_luts, s.frame_params(2), oracle_mod.WAVEFRONT)
+        _, _, _, ref = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(2), oracle_mod.WAVEFRONT)
         assert c["extension_rays"] == ref["extension_rays"]
         assert c["shadow_rays"] == ref["shadow_rays"]
         assert st["ext_node_visits"] == ref["node_visits"]
@@ -570,7 +574,7 @@ def test_megakernel_matches_oracle_megakernel(native_lib, golden_luts, oracle_mo
             t.render_images(seed, 1)
             pos, val = t.read_samples()
             rng = t.read_rng()
-            p_ref, v_ref, r_ref, c_ref = oracle_mod.render(s.flat(), golden_luts, s.frame_params(seed), oracle_mod.MEGAKERNEL,
+            p_ref, v_ref, r_ref, c_ref = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(seed), oracle_mod.MEGAKERNEL,
                                                            rng=True)
             assert np.array_equal(rng, r_ref)
             assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
@@ -614,7 +618,7 @@ def test_anyhit_megakernel_bit_exact(native_lib, golden_luts, oracle_mod, name):
         t.clear_film()
         t.render_images(2, 1)
         pos, val = t.read_samples()
-        p_ref, v_ref, r_ref, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(2), oracle_mod.MEGAKERNEL, rng=True)
+        p_ref, v_ref, r_ref, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(2), oracle_mod.MEGAKERNEL, rng=True)
         assert np.array_equal(t.read_rng(), r_ref)
         assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
         assert same_bits(val, v_ref).all()
