@@ -21,6 +21,9 @@ constexpr uint32_t kBlockW = 8, kBlockH = 8;           // one wave64 = one 8x8 p
 #define DCRT_CONTROL_BLOCK 256
 #endif
 constexpr uint32_t kControlBlock = DCRT_CONTROL_BLOCK;  // CONTROL workgroup (the path pool is a multiple of it)
+// the block appends keep per-wave counts in sm[16 q + wave] and the atomic's result in
+// sm[16 q + 15]: at most 15 waves per workgroup
+static_assert(kControlBlock % 64 == 0 && kControlBlock <= 960, "CONTROL workgroup: whole waves, at most 15");
 
 // Queue counters are sharded: producer workgroup b appends to shard b % kShards,
 // each shard counter on its own 256-B line. One returning device-scope atomic on
@@ -184,6 +187,15 @@ template <typename T>
 DEV T& slot(T* base, uint32_t i)
 {
     return *(T*)((char*)base + (uint64_t)(i * (uint32_t)sizeof(T)));
+}
+
+// Element i of a film sample array (batch x W*H entries): a 64-bit byte offset -- a 4K
+// batch of more than 32 images puts i * 16 past 2^32, which slot() would wrap onto
+// another pixel
+template <typename T>
+DEV T& sample_at(T* base, uint32_t i)
+{
+    return *(T*)((char*)base + (uint64_t)i * (uint64_t)sizeof(T));
 }
 
 // The state only CONTROL and MATERIAL touch, one 64-B record per slot (one whole 64-B

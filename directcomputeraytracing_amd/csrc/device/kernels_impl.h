@@ -206,9 +206,9 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
             li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
             const uint32_t p = slot(pool.pixel, path);
-            slot(film.samplePosition, p) = slot(pool.pixelSample, path);
-            slot(film.sampleValue, p) = make_float4(li.x, li.y, li.z, 0.0f);
-            if (debugRng) slot(film.debugRng, p) = ps.rng;
+            sample_at(film.samplePosition, p) = slot(pool.pixelSample, path);
+            sample_at(film.sampleValue, p) = make_float4(li.x, li.y, li.z, 0.0f);
+            if (debugRng) sample_at(film.debugRng, p) = ps.rng;
             // last, after stores that consumed the loads: another workgroup's scan may see the
             // slot idle from here on and start a new path in it
             slot(pool.flags, path) = kFlagIdle;
@@ -289,6 +289,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
 #ifndef DCRT_MATERIAL_BLOCK
 #define DCRT_MATERIAL_BLOCK 256
 #endif
+static_assert(DCRT_MATERIAL_BLOCK % 64 == 0 && DCRT_MATERIAL_BLOCK <= 960, "MATERIAL workgroup: whole waves, at most 15 (block_append3)");
 // The any-scene MATERIAL variant is held to 5 waves/SIMD (<= 96 VGPRs; 117 and 4 waves
 // unbounded): it then spills 3 VGPRs and still gains, coffee 3.12 -> 3.02, lamp 7.78 ->
 // 7.62 ms/spp (three / two A/B passes). The scene-specialised variants reach 5 waves by
@@ -451,7 +452,7 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
             const SampleOut so = *sampleOut;
             outPos = so.samplePosition;
             outVal = so.sampleValue;
-            if (so.debugRng) slot(so.debugRng, pix) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+            if (so.debugRng) sample_at(so.debugRng, pix) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
             slot(pool.flags, out) = kFlagIdle;
         } else {
             slot(pool.flags, out) = flags;
@@ -486,8 +487,8 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     }
     if (fin) slot(pool.finQueue, fshard * pool.finCap + fb) = path;
     if (ends) {
-        slot(outPos, pix) = pixSample;
-        slot(outVal, pix) = sample;
+        sample_at(outPos, pix) = pixSample;
+        sample_at(outVal, pix) = sample;
     }
     DCRT_MCLK(6);
     ++round;

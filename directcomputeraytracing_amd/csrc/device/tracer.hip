@@ -124,6 +124,56 @@ CastFn CastKernel(bool instr, bool opacity, bool allCached)
     return table[(instr ? 4 : 0) + (opacity ? 2 : 0) + (allCached ? 1 : 0)];
 }
 
+// The LDS stack depth traversal of the uploaded tree needs: the most interior nodes on
+// any root-to-leaf path through a TLAS leaf into its BLAS (each descent pushes the far
+// child; BVHAccel.inc.hlsl:143-154). Children lie after their parent (depth-first
+// layout), BLAS roots after the TLAS; anything else is malformed (false).
+bool RequiredTraversalStack(const dcrt_flat_scene& s, uint32_t* out)
+{
+    const uint32_t n = s.bvh_node_count;
+    *out = 0;
+    if (n == 0) return true;
+    std::vector<uint32_t> blasDepth(n, UINT32_MAX);   // memo: deepest path below a BLAS root
+    struct Item { uint32_t node, depth; };
+    std::vector<Item> todo;
+    auto walk = [&](uint32_t root, bool tlas, uint32_t* deepest) {
+        todo.assign(1, { root, 0u });
+        *deepest = 0;
+        while (!todo.empty()) {
+            const Item it = todo.back();
+            todo.pop_back();
+            const dcrt_bvh_node& nd = s.bvh_nodes[it.node];
+            if (nd.misc >= 4u) {   // a leaf
+                uint32_t d = it.depth;
+                if (tlas && (nd.misc & 4u)) {
+                    const uint32_t b = nd.right_child_or_prim_index;
+                    if (b >= n || b < s.tlas_node_count) return false;
+                    d += blasDepth[b];
+                }
+                *deepest = std::max(*deepest, d);
+                continue;
+            }
+            const uint32_t right = nd.right_child_or_prim_index;
+            if (it.node + 1 >= n || right <= it.node || right >= n) return false;
+            todo.push_back({ it.node + 1, it.depth + 1 });
+            todo.push_back({ right, it.depth + 1 });
+        }
+        return true;
+    };
+    // BLAS roots: the TLAS leaves' targets
+    for (uint32_t i = 0; i < std::min(s.tlas_node_count, n); ++i) {
+        const dcrt_bvh_node& nd = s.bvh_nodes[i];
+        if (!(nd.misc & 4u)) continue;
+        const uint32_t b = nd.right_child_or_prim_index;
+        if (b >= n || b < s.tlas_node_count) return false;
+        if (blasDepth[b] != UINT32_MAX) continue;
+        uint32_t d = 0;
+        if (!walk(b, false, &d)) return false;
+        blasDepth[b] = d;
+    }
+    return walk(0, true, out);
+}
+
 }  // namespace
 
 struct dcrt_tracer {
@@ -281,6 +331,12 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
             refillLanes = r;
             parkLanes = p;
         }
+    }
+    // every pool array is addressed through 32-bit byte offsets (slot(), ext_rec()): the
+    // widest per-slot record, PathState (64 B), bounds the pool at 2^26 slots
+    if ((uint64_t)poolSize * sizeof(PathState) > (1ull << 32)) {
+        SetLastError("path pool too large: at most 2^26 slots (32-bit pool offsets)");
+        return DCRT_E_LIMIT;
     }
     // WavefrontPathTracer.cpp:120-264 (SoA instead of AoS)
     const size_t P = poolSize;
@@ -489,6 +545,17 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     d.nodeCount = s.bvh_node_count;
     d.triangleCount = s.triangle_count;
     d.stackSize = std::max<uint32_t>(s.bvh_traversal_stack_size, 1u);
+    {
+        // the traversal pushes without a bound check: refuse a stack size below what the
+        // uploaded tree needs (TLAS leaf depth + BLAS depth, Scene.cpp:199-207)
+        uint32_t need = 0;
+        if (!RequiredTraversalStack(s, &need)) { SetLastError("malformed BVH node references"); return DCRT_E_INVALID_ARG; }
+        if (s.bvh_traversal_stack_size < need) {
+            SetLastError("bvh_traversal_stack_size " + std::to_string(s.bvh_traversal_stack_size) +
+                         " is below the uploaded BVH's depth " + std::to_string(need));
+            return DCRT_E_INVALID_ARG;
+        }
+    }
     // BLAS leaves (no TLAS-leaf bit, a primitive count) all with one triangle
     d.singlePrimLeaves = 1u;
     for (uint32_t i = 0; i < s.bvh_node_count; ++i) {
