@@ -27,6 +27,8 @@ import sys
 import time
 from pathlib import Path
 
+import numpy as np
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
@@ -69,13 +71,45 @@ def parse():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary from tools/pmc_traffic.py (default: the newest profiles/r*_pmc_traffic*.json "
                          "whose recorded workload is this run's)")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="timed repeats of the K steps; value is the median (SURVEY 8(d): median of 5 after warm-up)")
+    ap.add_argument("--spaceship-spp", type=int, default=4,
+                    help="configs[3] leg of the default Cornell run: spaceship 4K images (0 = skip)")
     return ap.parse_args()
 
 
+def host_cpus() -> dict:
+    """The host the CPU baseline runs on: nproc (= std::thread::hardware_concurrency()),
+    the CPUs this process may use (affinity, cgroup quota) and the CPU model."""
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = nproc
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        model = next((l.split(":", 1)[1].strip() for l in Path("/proc/cpuinfo").read_text().splitlines()
+                      if l.startswith("model name")), None)
+    except OSError:
+        pass
+    usable = affinity if quota is None else max(1, min(affinity, int(quota)))
+    return {"nproc": nproc, "affinity": affinity, "cgroup_cpus": quota, "usable": usable, "model": model}
+
+
 def cpu_baseline(scene, luts_arrays, seconds: float, label: str = "1920x1080 8-bounce Cornell") -> dict:
-    """Oracle megakernel (MegakernelPathTracing.hlsl restated in C) on host cores, bounded."""
+    """Oracle megakernel (MegakernelPathTracing.hlsl restated in C) on host cores, bounded.
+    Threads: every CPU this process may run on (hardware_concurrency() limited only by the
+    container's affinity / cgroup CPU quota, which caps what more threads could use)."""
     import oracle  # cpu_baseline leg only
-    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1, 16))
+    host = host_cpus()
+    threads = host["usable"]
     luts = oracle.luts_from_arrays(luts_arrays)
     flat = scene.flat()
     fr = scene.frame_params(0)
@@ -100,9 +134,11 @@ def cpu_baseline(scene, luts_arrays, seconds: float, label: str = "1920x1080 8-b
     done_rows = band * images
     mrays = rays / elapsed / 1e6
     return {"value": round(mrays, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "nproc": host["nproc"], "cpu_model": host["model"], "affinity_cpus": host["affinity"],
+            "cgroup_cpus": host["cgroup_cpus"],
             "sample": f"oracle megakernel (scalar C restatement of MegakernelPathTracing.hlsl), {W}x{done_rows} "
                       f"rows ({images} image(s) of {band} rows, seeds 0..{images - 1}) of the {label} "
-                      f"image at 1 spp, {elapsed:.1f} s",
+                      f"image at 1 spp, {elapsed:.1f} s, {threads} threads",
             "ms_per_spp_extrapolated": round(elapsed * 1e3 * H / done_rows, 1)}
 
 
@@ -232,41 +268,69 @@ def main():
     images = args.steps * world            # weak scaling: each step is one image per GPU-equivalent
     for t in tracers:
         t.prepare_images(images)           # sample textures of the timed batches + graph: not timed work
-        t.clear_film()
-        t.reset_stats()
-    barrier_sync()
-    t0 = time.perf_counter()
     snapshots = bool(args.snapshot_spp and args.snapshot_spp < images)
-    if snapshots:
-        # progressive rendering (configs[4]): every K images the films so far are summed
-        # over the pipelines and reduced onto rank 0 (a preview); the tracers' films keep
-        # accumulating, so the last snapshot is the whole render
-        done = 0
-        while done < images:
-            n = min(args.snapshot_spp, images - done)
-            render_all(done, n)
-            done += n
-            snapshot_film()
-    else:
-        render_all(0, images)
-        combine_films()
-        if dist is not None:
-            reduce_film()
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
+
+    def timed_run():
+        """One timed repeat of exactly K steps: (wall s, this rank's render s, reduce s)."""
+        for t in tracers:
+            t.clear_film()
+            t.reset_stats()
+        barrier_sync()
+        t0 = time.perf_counter()
+        t_render = t_reduce = 0.0
+        if snapshots:
+            # progressive rendering (configs[4]): every K images the films so far are summed
+            # over the pipelines and reduced onto rank 0 (a preview); the tracers' films keep
+            # accumulating, so the last snapshot is the whole render
+            done = 0
+            while done < images:
+                n = min(args.snapshot_spp, images - done)
+                t1 = time.perf_counter()
+                render_all(done, n)
+                t2 = time.perf_counter()
+                done += n
+                snapshot_film()
+                t_render += t2 - t1
+                t_reduce += time.perf_counter() - t2
+        else:
+            render_all(0, images)
+            combine_films()
+            tracer.synchronize()
+            t_render = time.perf_counter() - t0
+            if dist is not None:
+                t1 = time.perf_counter()
+                reduce_film()
+                if on_device:
+                    import torch
+                    torch.cuda.synchronize()
+                t_reduce = time.perf_counter() - t1
+        barrier_sync()
+        return time.perf_counter() - t0, t_render, t_reduce
+
+    runs = [timed_run() for _ in range(max(1, args.repeats))]
     rays = 0
     for t in tracers:
         c = t.counters()
         rays += c["extension_rays"] + c["shadow_rays"]
-
+    walls = [r[0] for r in runs]
+    rank_render = [r[1] for r in runs]
+    rank_reduce = [r[2] for r in runs]
+    per_rank = None
     if dist is not None:
         import torch
-        tt = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda" if on_device else "cpu")
-        tmax = tt[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = tt[1:].clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed, rays = float(tmax.item()), float(tsum.item())
+        assert dist.get_world_size() == args.gpus, f"--gpus {args.gpus} but the process group has {dist.get_world_size()} ranks"
+        dev = "cuda" if on_device else "cpu"
+        tw = torch.tensor(walls, dtype=torch.float64, device=dev)
+        dist.all_reduce(tw, op=dist.ReduceOp.MAX)          # each repeat: the slowest rank's wall time
+        walls = [float(x) for x in tw.cpu()]
+        tr = torch.tensor([float(rays)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tr, op=dist.ReduceOp.SUM)
+        rays = float(tr.item())
+        mine = torch.tensor([float(np.median(rank_render)), float(np.median(rank_reduce))], dtype=torch.float64, device=dev)
+        gathered = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(gathered, mine)
+        per_rank = [[float(x) for x in g.cpu()] for g in gathered]
+    elapsed = float(np.median(walls))
 
     if args.save_film and rank == 0:
         # the reduced film (N > 1), the last snapshot (one rank, snapshots taken), else tracer 0's
@@ -287,54 +351,19 @@ def main():
         for t in tracers:
             t.destroy()
         tracer = make_tracer(args.pool, (world, rank, args.stripe) if world > 1 else None)
-    tracer.set_instrumentation(True, False)
-    tracer.reset_stats()
-    tracer.render_images(0, R, filt)
-    st = tracer.traversal_stats()
-    cr = tracer.counters()
-    tracer.set_instrumentation(False, True)
-    tracer.reset_stats()
-    tracer.render_images(0, R, filt)
-    tm = tracer.traversal_stats()
-    tracer.set_instrumentation(False, False)
-    ext_bytes = (EXT_RAY_BYTES * cr["extension_rays"] + NODE_BYTES * st["ext_node_visits"]
-                 + TRI_BYTES * st["ext_triangle_tests"] + BLAS_BYTES * st["ext_blas_entries"])
-    shadow_bytes = (SHADOW_RAY_BYTES * cr["shadow_rays"] + NODE_BYTES * st["shadow_node_visits"]
-                    + TRI_BYTES * st["shadow_triangle_tests"] + BLAS_BYTES * st["shadow_blas_entries"])
-    # the timed launch is the merged EXTENSION+SHADOW cast kernel unless DCRT_SPLIT_CASTS=1
-    merged = os.environ.get("DCRT_SPLIT_CASTS", "0") in ("", "0")
-    cast_bytes = ext_bytes + shadow_bytes if merged else ext_bytes
-    launches = max(1, tm["ext_launches"])
-    avg_ms = tm["ext_kernel_ms"] / launches
-    bytes_per_launch = cast_bytes / launches
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    # measured HBM traffic of the same cast launches: a committed rocprofv3 PMC summary of
-    # THIS workload (tools/profile.sh + tools/pmc_traffic.py record the workload they profiled),
-    # never a profile of another image count, pool or scene
-    # whole-pipeline roofline ("and for the whole pipeline"): the reference's
-    # algorithmic bytes of every stage for the timed images (cast terms as above, CONTROL +
-    # MATERIAL per path-iteration = per extension ray, NEW_PATH per new path, the film pass
-    # per pixel x image), from the roofline leg's counts of the same images, over the timed
-    # region's wall time (max over ranks), per GPU
+    roof = cast_roofline(tracer, R, filt, {"config": args.config, "resolution": [args.width, args.height], "images": R,
+                                           "path_pool": args.pool, "world": world}, args.traffic_json)
+    st, cr = roof.pop("_stats"), roof.pop("_counters")
+    # whole-pipeline figure ("and for the whole pipeline"): the reference's
+    # algorithmic bytes of every stage for the timed images (cast terms, CONTROL + MATERIAL
+    # per path-iteration = per extension ray, NEW_PATH per new path, the film pass per pixel
+    # x image), from the roofline leg's counts of the same images, over the timed region's
+    # wall time, per GPU. These bytes are largely served from LDS / L2 / MALL: the figure is
+    # an algorithmic rate, not an HBM measurement (the HBM statement is roofline.frac).
     film_bytes = FILM_BYTES_BASE + FILM_BYTES_PER_TAP * (2 * int(filt.radius + 0.5) + 1) ** 2
-    pipe_bytes_R = (ext_bytes + shadow_bytes + (CONTROL_BYTES + MATERIAL_BYTES) * cr["extension_rays"]
+    pipe_bytes_R = (roof["bytes_per_launch"] * roof["launches"] + (CONTROL_BYTES + MATERIAL_BYTES) * cr["extension_rays"]
                     + NEW_PATH_BYTES * cr["new_paths"] + film_bytes * args.width * args.height * R / world)
     pipe_achieved = pipe_bytes_R * (images / R) / elapsed / 1e9
-    workload_key = {"config": args.config, "resolution": [args.width, args.height], "images": R,
-                    "path_pool": args.pool, "world": world}
-    traffic, traffic_src = None, "no committed PMC profile of this workload"
-    cands = [Path(args.traffic_json)] if args.traffic_json else \
-        sorted((ROOT / "profiles").glob("r*_pmc_traffic*.json"), reverse=True)
-    for tj in cands:
-        try:
-            d = json.loads(tj.read_text())
-        except Exception:
-            continue
-        if d.get("workload") == workload_key and d.get("ext_hbm_bytes_per_launch"):
-            traffic = d["ext_hbm_bytes_per_launch"]
-            traffic_src = (f"{tj.relative_to(ROOT) if tj.is_relative_to(ROOT) else tj}: rocprofv3 PMC, "
-                           f"FETCH_SIZE x2 + WRITE_SIZE per cast launch, same workload")
-            break
 
     result = {
         "metric": ("Mrays/s and ms/spp at 1920x1080, 8-bounce wavefront" if args.config == "cornell"
@@ -346,6 +375,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
         "ms_per_spp": round(elapsed * 1e3 / images, 3),
+        "repeats": len(walls),
+        "repeat_ms_per_spp": [round(w * 1e3 / images, 3) for w in walls],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -358,42 +389,159 @@ def main():
                    "parallelism": (f"film stripes x{world}" if world > 1 else "single GPU")
                                   + (f", {K} concurrent pipelines per GPU" if K > 1 else ""),
                    "rays": int(rays)},
-        "roofline": {"bound": "hbm",
-                     "basis": "algorithmic bytes: the reference's traversal counts (node visits, triangle tests, "
-                              "BLAS entries, from the instrumented kernel) x SURVEY 8(d)'s bytes per unit, "
-                              "wherever the bytes are served from (LDS scene cache, L1, L2, MALL or HBM)",
-                     "kernel": "cast_kernel (EXTENSION_RAY_CAST + SHADOW_RAY_CAST, one launch)" if merged
-                               else "extension_kernel (EXTENSION_RAY_CAST)",
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "hbm_measured": None if traffic is None else
-                     {"achieved": round(traffic / (avg_ms * 1e-3) / 1e9, 1),
-                      "frac": round(traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-                     "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 2),
-                     "launches": int(launches), "images": R,
-                     "per_ext_ray": {"nodes": st["ext_node_visits"] / max(1, cr["extension_rays"]),
-                                     "tris": st["ext_triangle_tests"] / max(1, cr["extension_rays"]),
-                                     "blas": st["ext_blas_entries"] / max(1, cr["extension_rays"])},
-                     "per_shadow_ray": {"nodes": st["shadow_node_visits"] / max(1, cr["shadow_rays"]),
-                                        "tris": st["shadow_triangle_tests"] / max(1, cr["shadow_rays"]),
-                                        "blas": st["shadow_blas_entries"] / max(1, cr["shadow_rays"])}},
-        "pipeline_roofline": {"bound": "hbm", "achieved": round(pipe_achieved, 1), "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": round(pipe_achieved / HBM_PEAK_GBS, 4),
+        "roofline": roof,
+        "pipeline_roofline": {"bound": "algorithmic (not an HBM measurement)", "achieved_algorithmic": round(pipe_achieved, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac_algorithmic": round(pipe_achieved / HBM_PEAK_GBS, 4),
                               "bytes_per_spp": int(pipe_bytes_R / R),
                               "basis": "per GPU: algorithmic bytes of cast + CONTROL (92 B) + MATERIAL (600 B) per "
                                        "path-iteration + NEW_PATH (88 B) per new path + film pass per pixel-image "
-                                       "(SURVEY 8(d)) over the timed region's wall time"},
+                                       "(SURVEY 8(d)) over the timed region's wall time; mostly LDS / cache served"},
         "cpu_baseline": None,
     }
+    if per_rank is not None:
+        # diagnosable first 8-GPU run: every rank's render time (its stripes + halo rows) and the
+        # RCCL film reduce, medians over the repeats; the halo overhead is rows rendered / owned
+        owned = len(render_rows(args.height, world, rank, args.stripe, 0))
+        rendered = len(render_rows(args.height, world, rank, args.stripe, halo))
+        result["multi_gpu"] = {"world_size": world, "per_rank_render_ms": [round(r[0] * 1e3, 3) for r in per_rank],
+                               "per_rank_reduce_ms": [round(r[1] * 1e3, 3) for r in per_rank],
+                               "reduce": "torch.distributed.reduce(SUM) of the RGBA32F film, "
+                                         + ("RCCL over xGMI" if on_device else args.dist_backend),
+                               "film_bytes": args.width * args.height * 16,
+                               "rank0_rows_owned": owned, "rank0_rows_rendered": rendered,
+                               "rank0_halo_overhead": round(rendered / max(1, owned) - 1.0, 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         label = "1920x1080 8-bounce Cornell" if args.config == "cornell" else f"{args.config} config"
         result["cpu_baseline"] = cpu_baseline(scene, luts_arrays, args.cpu_seconds, label)
+    tracer.destroy()
+    if rank == 0 and world == 1 and args.config == "cornell" and args.spaceship_spp > 0 and args.mode == "wavefront":
+        result["spaceship"] = spaceship_leg(args, luts_arrays)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    tracer.destroy()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def cast_roofline(tracer, R, filt, workload_key, traffic_json=None) -> dict:
+    """The merged EXTENSION+SHADOW cast launch over images 0..R-1 of the tracer's scene:
+    algorithmic bytes (the reference's traversal counts x SURVEY 8(d) bytes per unit, from
+    the instrumented variant), HIP-event launch time, and the HBM bytes a committed
+    rocprofv3 PMC profile of THIS workload measured per launch (tools/prof_config.sh /
+    tools/profile.sh + tools/pmc_traffic.py)."""
+    tracer.set_instrumentation(True, False)
+    tracer.reset_stats()
+    tracer.render_images(0, R, filt)
+    st = tracer.traversal_stats()
+    cr = tracer.counters()
+    tracer.set_instrumentation(False, True)
+    tracer.reset_stats()
+    tracer.render_images(0, R, filt)
+    tm = tracer.traversal_stats()
+    tracer.set_instrumentation(False, False)
+    info = tracer.info()
+    ext_bytes = (EXT_RAY_BYTES * cr["extension_rays"] + NODE_BYTES * st["ext_node_visits"]
+                 + TRI_BYTES * st["ext_triangle_tests"] + BLAS_BYTES * st["ext_blas_entries"])
+    shadow_bytes = (SHADOW_RAY_BYTES * cr["shadow_rays"] + NODE_BYTES * st["shadow_node_visits"]
+                    + TRI_BYTES * st["shadow_triangle_tests"] + BLAS_BYTES * st["shadow_blas_entries"])
+    # the timed launch is the merged EXTENSION+SHADOW cast kernel unless DCRT_SPLIT_CASTS=1
+    merged = os.environ.get("DCRT_SPLIT_CASTS", "0") in ("", "0")
+    cast_bytes = ext_bytes + shadow_bytes if merged else ext_bytes
+    launches = max(1, tm["ext_launches"])
+    avg_ms = tm["ext_kernel_ms"] / launches
+    bytes_per_launch = cast_bytes / launches
+    alg = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = None, "no committed PMC profile of this workload"
+    cands = [Path(traffic_json)] if traffic_json else sorted((ROOT / "profiles").glob("r*_pmc_traffic*.json"), reverse=True)
+    for tj in cands:
+        try:
+            d = json.loads(tj.read_text())
+        except Exception:
+            continue
+        if d.get("workload") == workload_key and d.get("ext_hbm_bytes_per_launch"):
+            traffic = d["ext_hbm_bytes_per_launch"]
+            traffic_src = (f"{tj.relative_to(ROOT) if tj.is_relative_to(ROOT) else tj}: rocprofv3 PMC, "
+                           f"FETCH_SIZE x2 + WRITE_SIZE per cast launch, same workload")
+            break
+    hbm = None if traffic is None else traffic / (avg_ms * 1e-3) / 1e9
+    # what bounds the launch, from the evidence: a scene resident in the LDS scene cache
+    # (Cornell) runs node / triangle fetches from LDS and is VALU-issue bound (DESIGN §4);
+    # a scene that does not fit walks its nodes through L2 / MALL (L2-miss latency bound)
+    bound = "lds/valu (scene in the LDS cache)" if info["scene_in_lds"] else "memory latency (L2/MALL-resident scene)"
+    return {"bound": bound,
+            "kernel": "cast_kernel (EXTENSION_RAY_CAST + SHADOW_RAY_CAST, one launch)" if merged
+                      else "extension_kernel (EXTENSION_RAY_CAST)",
+            "achieved": None if hbm is None else round(hbm, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": None if hbm is None else round(hbm / HBM_PEAK_GBS, 4),
+            "basis": "measured HBM: rocprofv3 PMC bytes per cast launch (traffic) / HIP-event launch time",
+            "traffic": traffic, "traffic_source": traffic_src,
+            "achieved_algorithmic": round(alg, 1), "frac_algorithmic": round(alg / HBM_PEAK_GBS, 4),
+            "algorithmic_basis": "the reference's traversal counts (node visits, triangle tests, BLAS entries, "
+                                 "from the instrumented kernel) x SURVEY 8(d)'s bytes per unit, wherever the bytes "
+                                 "are served from (LDS scene cache, L1, L2, MALL or HBM)",
+            "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 2),
+            "launches": int(launches), "images": R, "scene_in_lds": bool(info["scene_in_lds"]),
+            "per_ext_ray": {"nodes": st["ext_node_visits"] / max(1, cr["extension_rays"]),
+                            "tris": st["ext_triangle_tests"] / max(1, cr["extension_rays"]),
+                            "blas": st["ext_blas_entries"] / max(1, cr["extension_rays"])},
+            "per_shadow_ray": {"nodes": st["shadow_node_visits"] / max(1, cr["shadow_rays"]),
+                               "tris": st["shadow_triangle_tests"] / max(1, cr["shadow_rays"]),
+                               "blas": st["shadow_blas_entries"] / max(1, cr["shadow_rays"])},
+            "_stats": st, "_counters": cr}
+
+
+def spaceship_leg(args, luts_arrays) -> dict:
+    """configs[3] on this GPU (the traversal that touches HBM: 2 x 261 k-triangle hull BLAS
+    instanced 8 times, 3840x2160, 8 bounces): ms/spp over a few images (median of the
+    repeats, two concurrent pipelines as in the headline), then the cast roofline of the
+    same images on one pipeline with the HBM fraction from its committed PMC profile."""
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, render_images_concurrently, scenes
+    from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition
+    scene = Scene((3840, 2160))
+    desc = scenes.setup_config(scene, "spaceship", args.scene_dir)
+    W, H = scene.resolution
+    pool = scenes.default_pool(W, H)
+    filt = scene.filter_params()
+    halo = max(1, halo_for_radius(filt.radius, H))
+    n = args.spaceship_spp
+    K = max(1, args.streams)
+    subs = []
+    try:
+        for s_ in range(K):
+            t = WavefrontPathTracer(path_pool_size=pool // K, iterations_per_render=args.iterations)
+            t.on_scene_loaded(scene)
+            if K > 1:
+                t.set_film_partition(*stream_partition(H, 1, 0, K, s_, args.stripe), halo)
+            subs.append(t)
+        for t in subs:
+            t.clear_film()
+        render_images_concurrently(subs, 10_000, 1, filt)      # warm-up (graphs)
+        for t in subs:
+            t.prepare_images(n)
+        walls = []
+        for _ in range(max(1, min(args.repeats, 3))):
+            for t in subs:
+                t.clear_film()
+                t.reset_stats()
+            t0 = time.perf_counter()
+            render_images_concurrently(subs, 0, n, filt)
+            walls.append(time.perf_counter() - t0)
+        rays = sum(t.counters()["extension_rays"] + t.counters()["shadow_rays"] for t in subs)
+    finally:
+        for t in subs:
+            t.destroy()
+    el = float(np.median(walls))
+    tr = WavefrontPathTracer(path_pool_size=pool, iterations_per_render=args.iterations)
+    try:
+        tr.on_scene_loaded(scene)
+        roof = cast_roofline(tr, n, filt, {"config": "spaceship", "resolution": [W, H], "images": n,
+                                           "path_pool": pool, "world": 1})
+    finally:
+        tr.destroy()
+    roof.pop("_stats"), roof.pop("_counters")
+    return {"workload": f"{desc}, {n} spp, 1 GPU, {K} concurrent pipelines", "ms_per_spp": round(el * 1e3 / n, 3),
+            "repeat_ms_per_spp": [round(w * 1e3 / n, 3) for w in walls], "mrays_per_s": round(rays / el / 1e6, 2),
+            "path_pool": pool, "roofline": roof}
 
 
 if __name__ == "__main__":

@@ -130,6 +130,12 @@ class TraversalStats(C.Structure):
                 ("shadow_blas_entries", C.c_uint64), ("ext_launches", C.c_uint64), ("ext_kernel_ms", C.c_double)]
 
 
+class TracerInfo(C.Structure):
+    _fields_ = [("path_pool_size", C.c_uint32), ("scene_in_lds", C.c_uint32), ("cached_nodes", C.c_uint32),
+                ("cached_triangles", C.c_uint32), ("cast_block", C.c_uint32), ("traversal_stack", C.c_uint32),
+                ("material_generic", C.c_uint32)]
+
+
 class ObjMesh(C.Structure):
     _fields_ = [("vertices", C.POINTER(Vertex)), ("vertex_count", C.c_uint32), ("indices", C.POINTER(C.c_uint32)),
                 ("material_ids", C.POINTER(C.c_uint32)), ("triangle_count", C.c_uint32)]
@@ -208,6 +214,7 @@ SIGNATURES = [
     ("dcrt_tracer_set_instrumentation", _I, [_P, _I, _I]),
     ("dcrt_tracer_traversal_stats", _I, [_P, C.POINTER(TraversalStats)]),
     ("dcrt_tracer_reset_stats", _I, [_P]),
+    ("dcrt_tracer_get_info", _I, [_P, C.POINTER(TracerInfo)]),
     ("dcrt_tracer_synchronize", _I, [_P]),
     ("dcrt_tracer_get_luts", _I, [_P, C.POINTER(BxDFLuts)]),
     ("dcrt_tracer_set_luts", _I, [_P, C.POINTER(BxDFLuts)]),

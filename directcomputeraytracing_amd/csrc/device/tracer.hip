@@ -1270,6 +1270,20 @@ DCRT_API int dcrt_tracer_set_instrumentation(dcrt_tracer* t, int counters, int e
     return DCRT_OK;
 }
 
+DCRT_API int dcrt_tracer_get_info(dcrt_tracer* t, dcrt_tracer_info* out)
+{
+    TRACER_GUARD(t);
+    if (!out) return DCRT_E_INVALID_ARG;
+    out->path_pool_size = t->poolSize;
+    out->scene_in_lds = t->hasScene && t->castAllCached ? 1u : 0u;
+    out->cached_nodes = t->hasScene ? t->scene.cachedNodes : 0u;
+    out->cached_triangles = t->hasScene ? t->scene.cachedTris : 0u;
+    out->cast_block = t->castBlock;
+    out->traversal_stack = t->hasScene ? t->scene.stackSize : 0u;
+    out->material_generic = t->materialCaps == kCapAll ? 1u : 0u;
+    return DCRT_OK;
+}
+
 DCRT_API int dcrt_tracer_traversal_stats(dcrt_tracer* t, dcrt_traversal_stats* out)
 {
     TRACER_GUARD(t);

@@ -168,6 +168,12 @@ class WavefrontPathTracer:
         check(self._lib.dcrt_tracer_traversal_stats(self._h, C.byref(s)), "TraversalStats")
         return {k: getattr(s, k) for k, _ in _abi.TraversalStats._fields_}
 
+    def info(self) -> dict:
+        """What the tracer chose for the uploaded scene (pool, LDS scene cache, variants)."""
+        s = _abi.TracerInfo()
+        check(self._lib.dcrt_tracer_get_info(self._h, C.byref(s)), "GetInfo")
+        return {k: getattr(s, k) for k, _ in _abi.TracerInfo._fields_}
+
     def reset_stats(self) -> None:
         check(self._lib.dcrt_tracer_reset_stats(self._h), "ResetStats")
 

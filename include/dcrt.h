@@ -266,6 +266,17 @@ typedef struct dcrt_traversal_stats {
     double ext_kernel_ms;         /* summed HIP-event time of the timed EXTENSION_RAY_CAST launches */
 } dcrt_traversal_stats;
 
+/* What the tracer chose for the uploaded scene (diagnostics; bench.py reports it). */
+typedef struct dcrt_tracer_info {
+    uint32_t path_pool_size;      /* slots after rounding to whole CONTROL workgroups     */
+    uint32_t scene_in_lds;        /* 1: the whole BVH + triangles sit in the cast kernel's
+                                     LDS scene cache (the LDS-only cast variant)          */
+    uint32_t cached_nodes, cached_triangles;   /* how much of the scene the LDS cache holds */
+    uint32_t cast_block;          /* cast-kernel workgroup size                          */
+    uint32_t traversal_stack;     /* LDS stack rows per lane                             */
+    uint32_t material_generic;    /* 1: the any-scene MATERIAL variant                   */
+} dcrt_tracer_info;
+
 typedef struct dcrt_tracer dcrt_tracer;
 typedef struct dcrt_scene dcrt_scene;
 
@@ -415,6 +426,7 @@ DCRT_API int dcrt_tracer_counters(dcrt_tracer* tracer, dcrt_ray_stats* out_stats
 DCRT_API int dcrt_tracer_set_instrumentation(dcrt_tracer* tracer, int counters, int ext_timing);
 DCRT_API int dcrt_tracer_traversal_stats(dcrt_tracer* tracer, dcrt_traversal_stats* out_stats);
 DCRT_API int dcrt_tracer_reset_stats(dcrt_tracer* tracer);
+DCRT_API int dcrt_tracer_get_info(dcrt_tracer* tracer, dcrt_tracer_info* out_info);
 DCRT_API int dcrt_tracer_synchronize(dcrt_tracer* tracer);
 DCRT_API int dcrt_tracer_get_luts(dcrt_tracer* tracer, dcrt_bxdf_luts* out_luts);
 DCRT_API int dcrt_tracer_set_luts(dcrt_tracer* tracer, const dcrt_bxdf_luts* luts);

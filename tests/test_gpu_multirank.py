@@ -23,7 +23,8 @@ def _port():
 
 def test_two_rank_bench_film_equals_single_rank(tmp_path):
     common = ["--steps", "1", "--warmup", "0", "--width", "256", "--height", "144", "--bounces", "4",
-              "--pool", str(1 << 16), "--no-cpu-baseline", "--roofline-images", "1", "--stripe", "16"]
+              "--pool", str(1 << 16), "--no-cpu-baseline", "--roofline-images", "1", "--stripe", "16",
+              "--spaceship-spp", "0"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     single = tmp_path / "single.npy"
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *common, "--save-film", str(single)],
@@ -37,6 +38,14 @@ def test_two_rank_bench_film_equals_single_rank(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(line) == 1 and '"n_gpus": 2' in line[0]
+    import json
+    d = json.loads(line[0])
+    # the diagnosable multi-GPU fields: every rank's render time, the reduce, the halo overhead
+    m = d["multi_gpu"]
+    assert m["world_size"] == 2 and len(m["per_rank_render_ms"]) == 2 and len(m["per_rank_reduce_ms"]) == 2
+    assert all(x > 0 for x in m["per_rank_render_ms"]) and all(x >= 0 for x in m["per_rank_reduce_ms"])
+    assert m["rank0_rows_rendered"] >= m["rank0_rows_owned"] > 0 and m["rank0_halo_overhead"] >= 0
+    assert d["repeats"] == 5 and len(d["repeat_ms_per_spp"]) == 5
     a, b = np.load(single), np.load(multi)
     # 2 images on 2 ranks vs 1 image on 1 rank: compare the 1-rank film of the same 2 images
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *common, "--steps", "2", "--save-film", str(single)],
@@ -64,7 +73,7 @@ def test_progressive_snapshots_give_the_same_film(tmp_path):
     """bench.py --snapshot-spp K (configs[4]'s progressive reduce every K images, two
     pipelines summed per snapshot): the last snapshot is the film of one pass, bit for bit."""
     common = ["--steps", "3", "--warmup", "0", "--width", "160", "--height", "96", "--bounces", "4",
-              "--pool", str(1 << 16), "--no-cpu-baseline", "--roofline-images", "1"]
+              "--pool", str(1 << 16), "--no-cpu-baseline", "--roofline-images", "1", "--spaceship-spp", "0"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     films = []
     for extra in ([], ["--snapshot-spp", "1"]):
@@ -74,6 +83,30 @@ def test_progressive_snapshots_give_the_same_film(tmp_path):
         assert r.returncode == 0, r.stderr[-2000:]
         films.append(np.load(out))
     assert np.array_equal(films[0].view(np.uint32), films[1].view(np.uint32))
+
+
+def test_bench_default_line_fields(tmp_path):
+    """The default Cornell line's protocol fields: median of the repeats with each repeat
+    listed, the cast roofline as a measured-HBM statement with the algorithmic fraction
+    beside it, the pipeline figure labelled algorithmic, the CPU baseline's host, and the
+    configs[3] spaceship leg (ms/spp, traversal counts, its own roofline)."""
+    import json
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--width", "320",
+                        "--height", "180", "--pool", str(1 << 18), "--cpu-seconds", "1", "--spaceship-spp", "1",
+                        "--scene-dir", str(tmp_path)], capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["repeats"] == 5 and len(d["repeat_ms_per_spp"]) == 5
+    assert abs(d["ms_per_spp"] - sorted(d["repeat_ms_per_spp"])[2]) < 1e-3
+    roof = d["roofline"]
+    assert roof["frac_algorithmic"] > 0 and roof["bound"].startswith("lds/valu") and roof["scene_in_lds"]
+    assert d["pipeline_roofline"]["bound"].startswith("algorithmic")
+    cb = d["cpu_baseline"]
+    assert cb["cores"] >= 1 and cb["nproc"] >= cb["cores"] and cb["cpu_model"]
+    sp = d["spaceship"]
+    assert sp["ms_per_spp"] > 0 and sp["roofline"]["per_shadow_ray"]["nodes"] > 0
+    assert sp["roofline"]["bound"].startswith("memory latency") and not sp["roofline"]["scene_in_lds"]
 
 
 def test_torch_rccl_buffer_interop():
