@@ -431,8 +431,14 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     // (v_bfe takes its offset from the low 5 bits of misc: the split axis for an interior
     // node; for a leaf, whose neg is unused, a bit of negMask above bit 3, i.e. 0)
     const bool neg = __builtin_amdgcn_ubfe(s.negMask, misc, 1u) != 0u;
+#ifdef DCRT_REFERENCE_NODE_LAYOUT
     const uint32_t next = s.node + 1u;
     const uint32_t rightRef = right | (s.node & 0x80000000u);
+#else
+    // sibling-pair layout (dcrt_tracer::UploadScene): children at (right, right + 1)
+    const uint32_t next = right | (s.node & 0x80000000u);
+    const uint32_t rightRef = next + 1u;
+#endif
     const uint32_t nearChild = neg ? rightRef : next;
     const uint32_t farChild = neg ? next : rightRef;
     stack_at(lds, s.sp + stride) = farChild;

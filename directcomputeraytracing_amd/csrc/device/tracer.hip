@@ -124,6 +124,93 @@ CastFn CastKernel(bool instr, bool opacity, bool allCached)
     return table[(instr ? 4 : 0) + (opacity ? 2 : 0) + (allCached ? 1 : 0)];
 }
 
+// Device node order (traversal order, hits and counts are the tree's, so they do not
+// change): siblings side by side -- an interior node's children at (c, c + 1), its right
+// field holding c -- so a popped far child sits in the 64-B line its near sibling brought
+// in; the TLAS and then the top levels of every BLAS first, level by level (the prefix
+// the LDS scene cache mirrors: the nodes every ray entering a BLAS visits), then each
+// remaining subtree depth-first with its sibling pairs (one subtree, one address range).
+// The reference's depth-first order (left child = node + 1) would put one BLAS's
+// leftmost path in the cache prefix. newIndex[old] is the node's device index.
+void PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bvh_node>* out, std::vector<uint32_t>* newIndex)
+{
+    const uint32_t n = s.bvh_node_count;
+    const dcrt_bvh_node* nd = s.bvh_nodes;
+    std::vector<uint32_t> order;
+    order.reserve(n);
+    newIndex->assign(n, UINT32_MAX);
+    auto place = [&](uint32_t old) { (*newIndex)[old] = (uint32_t)order.size(); order.push_back(old); };
+    auto interior = [&](uint32_t i) { return nd[i].misc < 4u; };
+    std::vector<uint32_t> frontier{ 0u }, next, blasRoots;
+    place(0);
+    while (!frontier.empty()) {   // the TLAS, breadth first
+        next.clear();
+        for (uint32_t i : frontier) {
+            if (interior(i)) {
+                place(i + 1); place(nd[i].right_child_or_prim_index);
+                next.push_back(i + 1); next.push_back(nd[i].right_child_or_prim_index);
+            } else if (nd[i].misc & 4u) {
+                const uint32_t root = nd[i].right_child_or_prim_index;
+                if ((*newIndex)[root] == UINT32_MAX) { place(root); blasRoots.push_back(root); }
+            }
+        }
+        frontier.swap(next);
+    }
+    std::vector<std::vector<uint32_t>> level(blasRoots.size());
+    for (size_t b = 0; b < blasRoots.size(); ++b) level[b] = { blasRoots[b] };
+    for (bool grew = true; grew;) {   // BLAS top levels, level-major over the BLASes
+        grew = false;
+        size_t add = 0;
+        for (const auto& l : level)
+            for (uint32_t i : l) add += interior(i) ? 2 : 0;
+        if (add == 0 || order.size() + add > topNodes) break;
+        for (auto& l : level) {
+            next.clear();
+            for (uint32_t i : l)
+                if (interior(i)) {
+                    place(i + 1); place(nd[i].right_child_or_prim_index);
+                    next.push_back(i + 1); next.push_back(nd[i].right_child_or_prim_index);
+                }
+            l.swap(next);
+        }
+        grew = true;
+    }
+    std::vector<uint32_t> todo;   // the rest: each subtree depth first, sibling pairs
+    for (const auto& l : level)
+        for (uint32_t r : l) {
+            todo.assign(1, r);
+            while (!todo.empty()) {
+                const uint32_t i = todo.back();
+                todo.pop_back();
+                if (!interior(i)) continue;
+                place(i + 1); place(nd[i].right_child_or_prim_index);
+                todo.push_back(nd[i].right_child_or_prim_index);
+                todo.push_back(i + 1);
+            }
+        }
+    // trees no TLAS leaf reaches (a mesh without instances): each laid out the same way
+    for (uint32_t r = 0; r < n; ++r) {
+        if ((*newIndex)[r] != UINT32_MAX) continue;
+        place(r);
+        todo.assign(1, r);
+        while (!todo.empty()) {
+            const uint32_t i = todo.back();
+            todo.pop_back();
+            if (!interior(i)) continue;
+            place(i + 1); place(nd[i].right_child_or_prim_index);
+            todo.push_back(nd[i].right_child_or_prim_index);
+            todo.push_back(i + 1);
+        }
+    }
+    out->resize(order.size());
+    for (size_t k = 0; k < order.size(); ++k) {
+        dcrt_bvh_node d = nd[order[k]];
+        if (d.misc < 4u) d.right_child_or_prim_index = (*newIndex)[order[k] + 1];          // c: left at c, right at c + 1
+        else if (d.misc & 4u) d.right_child_or_prim_index = (*newIndex)[d.right_child_or_prim_index];   // BLAS root
+        (*out)[k] = d;
+    }
+}
+
 // The LDS stack depth traversal of the uploaded tree needs: the most interior nodes on
 // any root-to-leaf path through a TLAS leaf into its BLAS (each descent pushes the far
 // child; BVHAccel.inc.hlsl:143-154). Children lie after their parent (depth-first
@@ -462,7 +549,28 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     dcrt_float4x3* xf = nullptr;
     CHECKED(upload(&vtx, s.vertices, s.vertex_count));
     CHECKED(upload(&tris, s.triangles, (size_t)s.triangle_count * 3));
-    CHECKED(upload(&nodes, s.bvh_nodes, s.bvh_node_count));
+    // the traversal pushes without a bound check: refuse a stack size below what the
+    // uploaded tree needs (TLAS leaf depth + BLAS depth, Scene.cpp:199-207); the walk also
+    // checks every node reference
+    uint32_t stackNeed = 0;
+    if (!RequiredTraversalStack(s, &stackNeed)) { SetLastError("malformed BVH node references"); return DCRT_E_INVALID_ARG; }
+    if (s.bvh_traversal_stack_size < stackNeed) {
+        SetLastError("bvh_traversal_stack_size " + std::to_string(s.bvh_traversal_stack_size) +
+                     " is below the uploaded BVH's depth " + std::to_string(stackNeed));
+        return DCRT_E_INVALID_ARG;
+    }
+    {
+#ifdef DCRT_REFERENCE_NODE_LAYOUT
+        CHECKED(upload(&nodes, s.bvh_nodes, s.bvh_node_count));
+#else
+        std::vector<dcrt_bvh_node> relaid;
+        std::vector<uint32_t> newIndex;
+        PairLayout(s, 4096u, &relaid, &newIndex);
+        if (relaid.size() != s.bvh_node_count) { SetLastError("BVH nodes referenced twice"); return DCRT_E_INVALID_ARG; }
+        CHECKED(upload(&nodes, relaid.data(), relaid.size()));
+        HIPCHECK(hipStreamSynchronize(stream));   // (relaid is a host temporary)
+#endif
+    }
     uint32_t* mids = nullptr; uint32_t* lidx = nullptr; uint32_t* iflags = nullptr; uint32_t* ovr = nullptr;
     dcrt_material* mats = nullptr; dcrt_light* lights = nullptr;
     CHECKED(upload(&mids, s.material_ids, s.triangle_count));
@@ -545,17 +653,6 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     d.nodeCount = s.bvh_node_count;
     d.triangleCount = s.triangle_count;
     d.stackSize = std::max<uint32_t>(s.bvh_traversal_stack_size, 1u);
-    {
-        // the traversal pushes without a bound check: refuse a stack size below what the
-        // uploaded tree needs (TLAS leaf depth + BLAS depth, Scene.cpp:199-207)
-        uint32_t need = 0;
-        if (!RequiredTraversalStack(s, &need)) { SetLastError("malformed BVH node references"); return DCRT_E_INVALID_ARG; }
-        if (s.bvh_traversal_stack_size < need) {
-            SetLastError("bvh_traversal_stack_size " + std::to_string(s.bvh_traversal_stack_size) +
-                         " is below the uploaded BVH's depth " + std::to_string(need));
-            return DCRT_E_INVALID_ARG;
-        }
-    }
     // BLAS leaves (no TLAS-leaf bit, a primitive count) all with one triangle
     d.singlePrimLeaves = 1u;
     for (uint32_t i = 0; i < s.bvh_node_count; ++i) {
