@@ -294,7 +294,6 @@ struct TravState {
     uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked; not kept with ALL_CACHED)
     bool found, parked, noZero;   // noZero: no component of o, d is +-0
     bool anyHit;          // merged cast kernel: this lane's ray is a shadow ray (first hit ends it)
-    uint32_t pathFlags;   // shadow ray: the path's flags as MATERIAL wrote them (shadowD.w)
     // Near/far choice of the current space: bit a = (ld[a] < 0) for the axes a = 0..2,
     // bit 3 = front-to-back order on (0: the whole mask is 0, near child = node + 1 always)
     uint32_t negMask;
@@ -431,14 +430,8 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     // (v_bfe takes its offset from the low 5 bits of misc: the split axis for an interior
     // node; for a leaf, whose neg is unused, a bit of negMask above bit 3, i.e. 0)
     const bool neg = __builtin_amdgcn_ubfe(s.negMask, misc, 1u) != 0u;
-#ifdef DCRT_REFERENCE_NODE_LAYOUT
     const uint32_t next = s.node + 1u;
     const uint32_t rightRef = right | (s.node & 0x80000000u);
-#else
-    // sibling-pair layout (dcrt_tracer::UploadScene): children at (right, right + 1)
-    const uint32_t next = right | (s.node & 0x80000000u);
-    const uint32_t rightRef = next + 1u;
-#endif
     const uint32_t nearChild = neg ? rightRef : next;
     const uint32_t farChild = neg ? next : rightRef;
     stack_at(lds, s.sp + stride) = farChild;

@@ -198,53 +198,72 @@ DEV T& sample_at(T* base, uint32_t i)
     return *(T*)((char*)base + (uint64_t)i * (uint64_t)sizeof(T));
 }
 
-// The state only CONTROL and MATERIAL touch, one 64-B record per slot (one whole 64-B
-// memory sector per path instead of a 12- or 16-B piece of four arrays' sectors):
-// xoshiro state, throughput + bsdfPdf, Li and the light sampling result.
+// A live path's state travels with its extension ray: one 64-B record at the ray's
+// extension-queue position q (beside the 32-B ray record), written densely by its producer
+// (CONTROL for a new path, MATERIAL for a continuing one) and read densely by the next
+// MATERIAL pass at the same position -- no slot-indexed state, so no access to a 128-B
+// line half of which belongs to an ended path, and no load that waits for the slot.
+// xoshiro state, throughput + bsdfPdf, Li + lsr.x, (lsr.y, lsr.z, flags, path slot).
 struct PathState {
     uint4 rng;
     float4 thr;      // T.xyz, bsdfPdf
-    float4 liLsr;    // Li.xyz (isDelta: kFlagDelta in flags), lsr.x
-    float4 lsr2;     // lsr.y, lsr.z, -, -
+    float4 liLsr;    // Li.xyz, lsr.x
+    float4 lsrMisc;  // lsr.y, lsr.z, asfloat(flags: delta, bounce), asfloat(path slot)
 };
+// A path MATERIAL ends with its shadow ray pending: what CONTROL's completion needs
+// (Li += lsr when the shadow ray is unoccluded, WriteSample), at its finish-queue position.
+struct FinishRec {
+    float4 liLsr;    // Li.xyz, lsr.x
+    float4 lsrSlot;  // lsr.y, lsr.z, asfloat(path slot), -
+};
+// Destination of a shadow ray's result (carried in its record's direction.w): the
+// continuing path's extension-queue position, or its finish-queue position | kDestFinish
+constexpr uint32_t kDestFinish = 0x80000000u;
 
 struct PathPool {
     // the extension cast's result, indexed by the ray's item in the extension queue (its
-    // index in the shards' prefix order, the same for the cast and the next MATERIAL pass),
-    // not by path slot: written and read densely, and MATERIAL loads it beside the queue
-    // entry instead of behind it
-    float4* hit;         // t, u, v, asfloat(triangle | backface << 31)
-    uint32_t* hitInst;
+    // index in the shards' prefix order, the same for the cast and the next MATERIAL pass):
+    // 2 float4 per item, (t, u, v, asfloat(triangle | backface << 31)) and (the ray's
+    // direction, asfloat(instance)) -- MATERIAL then needs nothing of the ray record
+    float4* hit;
     // Shadow rays, like the extension rays, travel in their queue: entry e of shard s has
     // a 32-B record at 2 * (s * recCap + e) float4s, (origin, tMax) and (direction, the
-    // path's flags as MATERIAL left them), beside its path slot in shadowQueue[s * recCap + e]
+    // result's destination), beside its path slot in shadowQueue[s * recCap + e]
+    // (ALLOW_ANYHIT_SHADER's opacity samples are per slot)
     float4* shRec;
-    uint32_t* pixel;     // sample index: image * W*H + y * W + x
-    float2* pixelSample;
-    PathState* state;    // rng, throughput, Li, light sampling result
-    uint4* rngNew;       // a new path's rng, as CONTROL wrote it (dense 16-B writes; its
-                         // first MATERIAL pass reads it here, later passes from `state`)
-    uint32_t* flags;
+    uint32_t* pixel;     // per slot: sample index image * W*H + y * W + x
+    float2* pixelSample; // per slot
+    uint32_t* flags;     // per slot: kFlagIdle (CONTROL's claims), else 0
     float* extOpacity;         // ALLOW_ANYHIT_SHADER: g_ExtensionRayOpacitySamples
     float* shadowOpacity;      //                      g_ShadowRayOpacitySamples
-    // Queues (kShards x size entries each). The extension and finish queues alternate by
-    // iteration parity: `extQueue` / `finQueue` are this iteration's (appended to),
-    // `extPrev` / `finPrev` the previous iteration's (MATERIAL / CONTROL work lists);
-    // the host sets the four pointers per launch.
+    // Queues (kShards x recCap entries each), alternating by iteration parity: the `*Rec`,
+    // `state`, `shadowHit`, `finRec`, `finHit` pointers are this iteration's (written), the
+    // `*Prev` ones the previous iteration's (MATERIAL / CONTROL work lists); the host sets
+    // them per launch.
     // Extension rays travel IN the extension queue: entry e of shard s is a 32-B record at
-    // 2 * (s * recCap + e) float4s, (origin, 0) and (direction, asfloat(path slot |
-    // kEntryFirst)); tMax = inf, tMin = 0 implicit. Its producer (CONTROL, MATERIAL) writes
-    // it densely at its queue position, the cast reads it there without an index load, and
-    // the next MATERIAL pass takes the path and the incoming direction from one 16-B load.
+    // 2 * (s * recCap + e) float4s, (origin, 0) and (direction, asfloat(path slot)); tMax =
+    // inf, tMin = 0 implicit. Its producer (CONTROL, MATERIAL) writes it densely at its queue
+    // position with the path's state record (`state`, same position), the cast reads it there
+    // without an index load.
     float4* extRec;
     const float4* extPrevRec;
+    PathState* state;            // kShards x recCap, 64-bit offsets (state_at)
+    const PathState* statePrev;
+    uint32_t* shadowHit;         // the shadow cast's result for ext position q (1 = occluded)
+    const uint32_t* shadowHitPrev;
     uint32_t* shadowQueue;
-    uint32_t* finQueue;        // kFinShards x finCap entries
-    const uint32_t* finPrev;
+    FinishRec* finRec;           // kFinShards x finCap
+    const FinishRec* finPrevRec;
+    uint32_t* finHit;            // the shadow cast's result for finish position f
+    const uint32_t* finHitPrev;
     uint32_t size;
     uint32_t recCap;           // entries per extension-queue shard
     uint32_t finCap;           // entries per finish-queue shard
 };
+// State record of extension-queue position q: a 64-bit byte offset (one parity's records
+// pass 4 GiB at 2^26 slots)
+DEV PathState& state_at(PathState* base, uint32_t q) { return *(PathState*)((char*)base + (uint64_t)q * 64u); }
+DEV const PathState& state_at(const PathState* base, uint32_t q) { return *(const PathState*)((const char*)base + (uint64_t)q * 64u); }
 
 // Sample textures (m_SamplePositionTexture / m_SampleValueTexture) for every image of a
 // batch: image b's sample of pixel (x, y) sits at b * W*H + y * W + x.

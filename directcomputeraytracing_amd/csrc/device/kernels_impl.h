@@ -196,19 +196,21 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
         qmap(prev, kQFinish, &fm);
         const uint32_t nFin = fm.prefix[kFinShards];
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nFin; i += gridDim.x * blockDim.x) {
-            const uint32_t path = qentry(pool.finPrev, pool.finCap, fm, i);
-            const bool shadowHit = (slot(pool.flags, path) & kFlagShadowRayHit) != 0;
-            const PathState& ps = slot(pool.state, path);
-            const float4 l4 = ps.liLsr, l2 = ps.lsr2;
-            F3 li{l4.x, l4.y, l4.z};
-            const F3 lsr{l4.w, l2.x, l2.y};
+            // the path's finish record and its shadow ray's result, both at its finish-queue
+            // position (dense); only the pixel is per slot
+            const uint32_t f = qpos(pool.finCap, fm, i);
+            const FinishRec fr = pool.finPrevRec[f];
+            const bool shadowHit = pool.finHitPrev[f] != 0u;
+            const uint32_t path = asu(fr.lsrSlot.z);
+            F3 li{fr.liLsr.x, fr.liLsr.y, fr.liLsr.z};
+            const F3 lsr{fr.liLsr.w, fr.lsrSlot.x, fr.lsrSlot.y};
             li.x = li.x + (!shadowHit ? lsr.x : 0.0f);
             li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
             li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
             const uint32_t p = slot(pool.pixel, path);
             sample_at(film.samplePosition, p) = slot(pool.pixelSample, path);
             sample_at(film.sampleValue, p) = make_float4(li.x, li.y, li.z, 0.0f);
-            if (debugRng) sample_at(film.debugRng, p) = ps.rng;
+            // (debug RNG: MATERIAL stored it when it ended the path)
             // last, after stores that consumed the loads: another workgroup's scan may see the
             // slot idle from here on and start a new path in it
             slot(pool.flags, path) = kFlagIdle;
@@ -250,11 +252,13 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     const uint32_t block = shard + claimed * kShards;
     bool newPath = false;
     V3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 0.0f);
+    Rng rng;
+    rng.s0 = rng.s1 = rng.s2 = rng.s3 = 0u;
     if (got) {
         uint32_t px = 0, py = 0, image = 0;
         if (block_pixel(*fc, film, block, lane, &px, &py, &image)) {
             // NEW_PATH :211-237 (image `image` of the batch has frame seed frameSeed + image)
-            Rng rng = rng_init(px, py, fc->frameSeed + image);
+            rng = rng_init(px, py, fc->frameSeed + image);
             const float psx = next1(rng), psy = next1(rng);
             const float fsx = (psx + (float)px) / (float)fc->resolution[0];
             const float fsy = (psy + (float)py) / (float)fc->resolution[1];
@@ -263,13 +267,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) pool.extOpacity[tid] = next1(rng);   // :223-226
             pool.pixel[tid] = image * (film.width * film.height) + py * film.width + px;
             pool.pixelSample[tid] = make_float2(psx, psy);
-            // (into its own dense array: a 16-B piece of each 64-B state record was a partly
-            // written sector per path)
-            pool.rngNew[tid] = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
-            // Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0 are implicit: the path's
-            // first MATERIAL pass takes them as constants (kEntryFirst); isDelta = true, bounce 0
-            // (writing them into the state record too measured the same: 2.687 vs 2.682 ms/spp)
-            pool.flags[tid] = kFlagDelta;
+            pool.flags[tid] = 0u;   // busy
             newPath = true;
         }
     }
@@ -278,9 +276,17 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     uint32_t eslot, unused;
     block_append2(newPath, qctr(cnt, kQExt, shard), false, qctr(cnt, kQExt, shard), sm + 32, &eslot, &unused);
     if (newPath) {
-        float4* r = ext_rec(pool.extRec, shard * pool.recCap + eslot);
+        const uint32_t q = shard * pool.recCap + eslot;
+        float4* r = ext_rec(pool.extRec, q);
         r[0] = make_float4(o.x, o.y, o.z, 0.0f);
-        r[1] = make_float4(d.x, d.y, d.z, asf(tid | kEntryFirst));
+        r[1] = make_float4(d.x, d.y, d.z, asf(tid));
+        // NEW_PATH's state (:227-237): Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0,
+        // isDelta = true, bounce 0 -- beside the ray, densely
+        PathState& st = state_at(pool.state, q);
+        st.rng = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+        st.thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+        st.liLsr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        st.lsrMisc = make_float4(0.0f, 0.0f, asf(kFlagDelta), asf(tid));
     }
     }
 }
@@ -327,31 +333,34 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     V3 nO = mk(0.0f, 0.0f, 0.0f), nD = mk(0.0f, 0.0f, 0.0f);   // the next extension ray
     float4 sO = make_float4(0.0f, 0.0f, 0.0f, 0.0f);            // the shadow ray (origin, tMax)
     V3 sD = mk(0.0f, 0.0f, 0.0f);
-    uint32_t sFlags = 0;
+    // the path's state after this pass, stored at the positions the appends return
+    uint32_t pathFlags = 0;
+    float4 sThr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    V3 sT = mk(0.0f, 0.0f, 0.0f), sL = mk(0.0f, 0.0f, 0.0f), sLsr = mk(0.0f, 0.0f, 0.0f);
+    uint4 sRng = make_uint4(0u, 0u, 0u, 0u);
     if (active) {
         ++itemsDone;
-        // the ray's record in the previous iteration's extension queue: its direction and
-        // the path slot (the hit record is at item i, independent of it)
-        const float4 rd = ext_rec(pool.extPrevRec, qpos(pool.recCap, qm, i))[1];
-        const uint32_t entry = asu(rd.w);
-        path = entry & ~kEntryFirst;
-        const bool first = (entry & kEntryFirst) != 0u;   // NEW_PATH's constants, not loaded
-        const float4 h4 = slot(pool.hit, i);
+        // Everything this pass reads is indexed by the item (no load waits for another):
+        // the path's state record at its extension-queue position q, the cast's hit record
+        // (with the ray's direction) at item i, the result of the path's last shadow ray at q
+        const uint32_t q = qpos(pool.recCap, qm, i);
+        const PathState& ps = state_at(pool.statePrev, q);
+        const float4 h4 = pool.hit[2 * i], hd = pool.hit[2 * i + 1];
+        const bool shadowHit = pool.shadowHitPrev[q] != 0u;
         HitRecord hit;
-        hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = slot(pool.hitInst, i);
-        const V3 dir = mk(rd.x, rd.y, rd.z);
-        const PathState& ps = slot(pool.state, path);
-        const uint4 r4 = first ? slot(pool.rngNew, path) : ps.rng;
+        hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = asu(hd.w);
+        const V3 dir = mk(hd.x, hd.y, hd.z);
+        const uint4 r4 = ps.rng;
         Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
-        float4 thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : ps.thr;
-        const float4 l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ps.liLsr;
-        const float4 l2 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ps.lsr2;
+        float4 thr = ps.thr;
+        const float4 l4 = ps.liLsr, l2 = ps.lsrMisc;
+        path = asu(l2.w);
+        uint32_t flags = asu(l2.z);
         F3 li{l4.x, l4.y, l4.z};
-        uint32_t flags = slot(pool.flags, path);
         {
-            // CONTROL's Li += light sampling result (:520-528), done here for live paths
+            // CONTROL's Li += light sampling result (:520-528), done here for live paths (a
+            // path without a shadow ray carries lsr = 0: Li + 0 either way)
             const F3 lsr0{l4.w, l2.x, l2.y};
-            const bool shadowHit = (flags & kFlagShadowRayHit) != 0;
             li.x = li.x + (!shadowHit ? lsr0.x : 0.0f);
             li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
             li.z = li.z + (!shadowHit ? lsr0.z : 0.0f);
@@ -435,35 +444,34 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
                 if (hasShadow) slot(pool.shadowOpacity, out) = next1(rng);
             }
         }
-        if (!hasShadow) flags = flags & ~kFlagShadowRayHit;
         ends = terminate && !hasShadow;
-        if (ends) {
+        // (the state written below goes to the queue positions the appends return)
+        pathFlags = flags;
+        sThr = thr;
+        sT = T;
+        sL = L;
+        sLsr = lsr;
+        sRng = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+        if (ends || terminate) {
             // The path ends here with no shadow ray pending: all CONTROL would still do is
             // Li += light sampling result (0: the same bits as L + 0.0f) and WriteSample
             // (RayTracingCommon.inc.hlsl:118-122), so both happen in this pass and the slot
-            // goes idle at once (CONTROL reads nothing for it; no path state is stored). The
-            // pixel is loaded here and the sample stored after the queue appends, whose
+            // goes idle at once. (A path ending WITH a shadow ray pending goes to the finish
+            // queue; CONTROL completes it. Its debug RNG state, final now, is stored here.)
+            // The pixel is loaded here and the sample stored after the queue appends, whose
             // atomic round trip hides the load.
-            pix = slot(pool.pixel, out);
-            pixSample = slot(pool.pixelSample, out);
-            sample = make_float4(L.x + 0.0f, L.y + 0.0f, L.z + 0.0f, 0.0f);
-            // the sample pointers are read here too, not after the appends: read there (behind
-            // the barriers and the atomic) they were one more round trip at the wave's end
             const SampleOut so = *sampleOut;
-            outPos = so.samplePosition;
-            outVal = so.sampleValue;
+            if (ends || so.debugRng) pix = slot(pool.pixel, out);
+            if (ends) {
+                pixSample = slot(pool.pixelSample, out);
+                sample = make_float4(L.x + 0.0f, L.y + 0.0f, L.z + 0.0f, 0.0f);
+                // the sample pointers are read here too, not after the appends: read there
+                // (behind the barriers and the atomic) they were one more round trip
+                outPos = so.samplePosition;
+                outVal = so.sampleValue;
+                slot(pool.flags, out) = kFlagIdle;
+            }
             if (so.debugRng) sample_at(so.debugRng, pix) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
-            slot(pool.flags, out) = kFlagIdle;
-        } else {
-            slot(pool.flags, out) = flags;
-            // (the shadow cast writes the path's flags with the occlusion bit — a plain store,
-            // no read of the flags in front of it — taking them from the shadow ray's record)
-            sFlags = flags;
-            PathState& po = slot(pool.state, out);
-            po.rng = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
-            po.thr = make_float4(T.x, T.y, T.z, thr.w);
-            po.liLsr = make_float4(L.x, L.y, L.z, lsr.x);
-            po.lsr2 = make_float4(lsr.y, lsr.z, 0.0f, 0.0f);
         }
     }
     DCRT_MCLK(5);
@@ -473,19 +481,32 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     uint32_t fb;
     block_append3(active && !terminate, qctr(cnt, kQExt, shard), active && hasShadow, qctr(cnt, kQShadow, shard),
                   fin, qctr(cnt, kQFinish, fshard), sm + (round & 1u) * 48u, &es, &ss, &fb);
+    const uint32_t qNext = shard * pool.recCap + es;           // the continuing path's records
+    const uint32_t fPos = fshard * pool.finCap + fb;           // a finishing path's record
     if (active && !terminate) {
-        float4* r = ext_rec(pool.extRec, shard * pool.recCap + es);
+        float4* r = ext_rec(pool.extRec, qNext);
         r[0] = make_float4(nO.x, nO.y, nO.z, 0.0f);
         r[1] = make_float4(nD.x, nD.y, nD.z, asf(path));
+        PathState& st = state_at(pool.state, qNext);
+        st.rng = sRng;
+        st.thr = make_float4(sT.x, sT.y, sT.z, sThr.w);
+        st.liLsr = make_float4(sL.x, sL.y, sL.z, sLsr.x);
+        st.lsrMisc = make_float4(sLsr.y, sLsr.z, asf(pathFlags), asf(path));
+    }
+    if (fin) {
+        FinishRec& fr = pool.finRec[fPos];
+        fr.liLsr = make_float4(sL.x, sL.y, sL.z, sLsr.x);
+        fr.lsrSlot = make_float4(sLsr.y, sLsr.z, asf(path), 0.0f);
     }
     if (active && hasShadow) {
-        const uint32_t q = shard * pool.recCap + ss;
-        float4* r = ext_rec(pool.shRec, q);
+        const uint32_t sq = shard * pool.recCap + ss;
+        float4* r = ext_rec(pool.shRec, sq);
         r[0] = sO;
-        r[1] = make_float4(sD.x, sD.y, sD.z, asf(sFlags));
-        slot(pool.shadowQueue, q) = path;
+        // where the shadow cast writes the result: the continuing path's next state, or its
+        // finish record
+        r[1] = make_float4(sD.x, sD.y, sD.z, asf(terminate ? (fPos | kDestFinish) : qNext));
+        slot(pool.shadowQueue, sq) = path;
     }
-    if (fin) slot(pool.finQueue, fshard * pool.finCap + fb) = path;
     if (ends) {
         sample_at(outPos, pix) = pixSample;
         sample_at(outVal, pix) = sample;
@@ -671,6 +692,22 @@ __device__ __forceinline__ void flush_stats(const TraversalStats& st, unsigned l
     if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&dst[0], a); atomicAdd(&dst[1], b); atomicAdd(&dst[2], c); }
 }
 
+// The extension cast's result at the ray's queue item: the hit and, for MATERIAL, the
+// ray's direction and instance (so MATERIAL reads nothing of the ray record)
+__device__ __forceinline__ void emit_hit(const PathPool& pool, uint32_t item, const TravState& s)
+{
+    float4* h = pool.hit + 2 * (size_t)item;
+    h[0] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
+    h[1] = make_float4(s.d.x, s.d.y, s.d.z, asf(s.found ? s.hit.inst : 0u));
+}
+// The shadow cast's result where MATERIAL asked for it: the continuing path's next
+// extension-queue position, or its finish-queue position (kDestFinish)
+__device__ __forceinline__ void emit_occlusion(const PathPool& pool, uint32_t dest, const TravState& s)
+{
+    uint32_t* dst = (dest & kDestFinish) ? pool.finHit : pool.shadowHit;
+    dst[dest & ~kDestFinish] = s.found ? 1u : 0u;
+}
+
 // OPACITY: the ALLOW_ANYHIT_SHADER variant (a separate instantiation, so the default
 // kernels carry none of its state).
 template <bool INSTR, bool OPACITY>
@@ -692,10 +729,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(Path
             if (OPACITY) s.opacitySample = pool.extOpacity[asu(d.w) & ~kEntryFirst];
             return i;   // the result goes to the ray's queue item
         },
-        [&](uint32_t item, const TravState& s) __attribute__((always_inline)) {
-            pool.hit[item] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
-            pool.hitInst[item] = s.found ? s.hit.inst : 0u;
-        },
+        [&](uint32_t item, const TravState& s) __attribute__((always_inline)) { emit_hit(pool, item, s); },
         st, DCRT_WAVE_TAG(g));
     if (INSTR) flush_stats(st, instr);
     (void)g;
@@ -741,16 +775,11 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
         [&](uint32_t i, uint32_t q, TravState& s) __attribute__((always_inline)) {
             const float4* r = ext_rec((const float4*)pool.shRec, q);
             const float4 o = r[0], d = r[1];
-            const uint32_t path = slot(pool.shadowQueue, q);
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, o.w);
-            s.pathFlags = asu(d.w);
-            if (OPACITY) s.opacitySample = pool.shadowOpacity[path];
-            return path;
+            if (OPACITY) s.opacitySample = pool.shadowOpacity[slot(pool.shadowQueue, q)];
+            return asu(d.w);   // the result's destination (MATERIAL's kDestFinish code)
         },
-        [&](uint32_t path, const TravState& s) __attribute__((always_inline)) {
-            // the path's flags as MATERIAL wrote them (carried in shadowD.w): a plain store
-            pool.flags[path] = (s.found ? kFlagShadowRayHit : 0u) | (s.pathFlags & ~kFlagShadowRayHit);
-        },
+        [&](uint32_t dest, const TravState& s) __attribute__((always_inline)) { emit_occlusion(pool, dest, s); },
         st, DCRT_WAVE_TAG(g));
     if (INSTR) flush_stats(st, instr + 3);
     end_iteration(cnt, nextCnt, g, n);
@@ -790,22 +819,20 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
             // stay below 4 GiB, dcrt_tracer::Create); a shadow ray's path slot beside it
             const float4* r = ext_rec(shadow ? shRec : extRec, v);
             const float4 o = r[0], d = r[1];
-            const uint32_t path = shadow ? slot(shQueue, v) : asu(d.w) & ~kEntryFirst;
             trav_init(s, mk(o.x, o.y, o.z), mk(d.x, d.y, d.z), 0.0f, shadow ? o.w : inf());
             s.anyHit = shadow;
-            s.pathFlags = asu(d.w);
-            if (OPACITY) s.opacitySample = shadow ? pool.shadowOpacity[path] : pool.extOpacity[path];
+            if (OPACITY) {
+                const uint32_t path = shadow ? slot(shQueue, v) : asu(d.w);
+                s.opacitySample = shadow ? pool.shadowOpacity[path] : pool.extOpacity[path];
+            }
             if (INSTR) st = TraversalStats{};
-            return shadow ? path : i;   // an extension ray's result goes to its queue item
+            // an extension ray's result goes to its queue item, a shadow ray's to the
+            // destination MATERIAL put in its record
+            return shadow ? asu(d.w) : i;
         },
         [&](uint32_t item, const TravState& s) __attribute__((always_inline)) {
-            if (s.anyHit) {
-                // the path's flags as MATERIAL wrote them (carried in shadowD.w): a plain store
-                pool.flags[item] = (s.found ? kFlagShadowRayHit : 0u) | (s.pathFlags & ~kFlagShadowRayHit);
-            } else {
-                pool.hit[item] = s.found ? make_float4(s.hit.t, s.hit.u, s.hit.v, asf(s.hit.tri)) : make_float4(inf(), 0.0f, 0.0f, 0.0f);
-                pool.hitInst[item] = s.found ? s.hit.inst : 0u;
-            }
+            if (s.anyHit) emit_occlusion(pool, item, s);
+            else emit_hit(pool, item, s);
             if (INSTR) {
                 TraversalStats& dst = s.anyHit ? stShadow : stExt;
                 dst.nodes += st.nodes; dst.tris += st.tris; dst.blas += st.blas;

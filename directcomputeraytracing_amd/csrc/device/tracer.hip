@@ -124,93 +124,6 @@ CastFn CastKernel(bool instr, bool opacity, bool allCached)
     return table[(instr ? 4 : 0) + (opacity ? 2 : 0) + (allCached ? 1 : 0)];
 }
 
-// Device node order (traversal order, hits and counts are the tree's, so they do not
-// change): siblings side by side -- an interior node's children at (c, c + 1), its right
-// field holding c -- so a popped far child sits in the 64-B line its near sibling brought
-// in; the TLAS and then the top levels of every BLAS first, level by level (the prefix
-// the LDS scene cache mirrors: the nodes every ray entering a BLAS visits), then each
-// remaining subtree depth-first with its sibling pairs (one subtree, one address range).
-// The reference's depth-first order (left child = node + 1) would put one BLAS's
-// leftmost path in the cache prefix. newIndex[old] is the node's device index.
-void PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bvh_node>* out, std::vector<uint32_t>* newIndex)
-{
-    const uint32_t n = s.bvh_node_count;
-    const dcrt_bvh_node* nd = s.bvh_nodes;
-    std::vector<uint32_t> order;
-    order.reserve(n);
-    newIndex->assign(n, UINT32_MAX);
-    auto place = [&](uint32_t old) { (*newIndex)[old] = (uint32_t)order.size(); order.push_back(old); };
-    auto interior = [&](uint32_t i) { return nd[i].misc < 4u; };
-    std::vector<uint32_t> frontier{ 0u }, next, blasRoots;
-    place(0);
-    while (!frontier.empty()) {   // the TLAS, breadth first
-        next.clear();
-        for (uint32_t i : frontier) {
-            if (interior(i)) {
-                place(i + 1); place(nd[i].right_child_or_prim_index);
-                next.push_back(i + 1); next.push_back(nd[i].right_child_or_prim_index);
-            } else if (nd[i].misc & 4u) {
-                const uint32_t root = nd[i].right_child_or_prim_index;
-                if ((*newIndex)[root] == UINT32_MAX) { place(root); blasRoots.push_back(root); }
-            }
-        }
-        frontier.swap(next);
-    }
-    std::vector<std::vector<uint32_t>> level(blasRoots.size());
-    for (size_t b = 0; b < blasRoots.size(); ++b) level[b] = { blasRoots[b] };
-    for (bool grew = true; grew;) {   // BLAS top levels, level-major over the BLASes
-        grew = false;
-        size_t add = 0;
-        for (const auto& l : level)
-            for (uint32_t i : l) add += interior(i) ? 2 : 0;
-        if (add == 0 || order.size() + add > topNodes) break;
-        for (auto& l : level) {
-            next.clear();
-            for (uint32_t i : l)
-                if (interior(i)) {
-                    place(i + 1); place(nd[i].right_child_or_prim_index);
-                    next.push_back(i + 1); next.push_back(nd[i].right_child_or_prim_index);
-                }
-            l.swap(next);
-        }
-        grew = true;
-    }
-    std::vector<uint32_t> todo;   // the rest: each subtree depth first, sibling pairs
-    for (const auto& l : level)
-        for (uint32_t r : l) {
-            todo.assign(1, r);
-            while (!todo.empty()) {
-                const uint32_t i = todo.back();
-                todo.pop_back();
-                if (!interior(i)) continue;
-                place(i + 1); place(nd[i].right_child_or_prim_index);
-                todo.push_back(nd[i].right_child_or_prim_index);
-                todo.push_back(i + 1);
-            }
-        }
-    // trees no TLAS leaf reaches (a mesh without instances): each laid out the same way
-    for (uint32_t r = 0; r < n; ++r) {
-        if ((*newIndex)[r] != UINT32_MAX) continue;
-        place(r);
-        todo.assign(1, r);
-        while (!todo.empty()) {
-            const uint32_t i = todo.back();
-            todo.pop_back();
-            if (!interior(i)) continue;
-            place(i + 1); place(nd[i].right_child_or_prim_index);
-            todo.push_back(nd[i].right_child_or_prim_index);
-            todo.push_back(i + 1);
-        }
-    }
-    out->resize(order.size());
-    for (size_t k = 0; k < order.size(); ++k) {
-        dcrt_bvh_node d = nd[order[k]];
-        if (d.misc < 4u) d.right_child_or_prim_index = (*newIndex)[order[k] + 1];          // c: left at c, right at c + 1
-        else if (d.misc & 4u) d.right_child_or_prim_index = (*newIndex)[d.right_child_or_prim_index];   // BLAS root
-        (*out)[k] = d;
-    }
-}
-
 // The LDS stack depth traversal of the uploaded tree needs: the most interior nodes on
 // any root-to-leaf path through a TLAS leaf into its BLAS (each descent pushes the far
 // child; BVHAccel.inc.hlsl:143-154). Children lie after their parent (depth-first
@@ -276,7 +189,10 @@ struct dcrt_tracer {
     std::vector<void*> poolAllocs, sceneAllocs, filmAllocs, sampleAllocs, rowAllocs;
     PathPool pool{};                   // (queue pointers set per launch: LaunchIteration)
     float4* extRecs = nullptr;         // 2 parities x kShards x recCap extension-ray records (2 float4)
-    uint32_t* finQueues = nullptr;     // 2 parities x kFinShards x pool.finCap
+    PathState* stateRecs = nullptr;    // 2 parities x kShards x recCap path state records
+    uint32_t* shadowHits = nullptr;    // 2 parities x kShards x recCap shadow results
+    FinishRec* finRecs = nullptr;      // 2 parities x kFinShards x pool.finCap
+    uint32_t* finHits = nullptr;       // 2 parities x kFinShards x pool.finCap
     DeviceScene scene{};
     bool hasScene = false;
     uint32_t castBlock = 256;
@@ -419,20 +335,18 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
             parkLanes = p;
         }
     }
-    // every pool array is addressed through 32-bit byte offsets (slot(), ext_rec()): the
-    // widest per-slot record, PathState (64 B), bounds the pool at 2^26 slots
-    if ((uint64_t)poolSize * sizeof(PathState) > (1ull << 32)) {
+    // pool arrays and queue records are addressed through 32-bit byte offsets (slot(),
+    // ext_rec()): an extension-queue parity holds up to 2 records of 32 B per slot, which
+    // bounds the pool at 2^26 slots (the state records, 64 B, use 64-bit offsets)
+    if ((uint64_t)poolSize * 64u > (1ull << 32)) {
         SetLastError("path pool too large: at most 2^26 slots (32-bit pool offsets)");
         return DCRT_E_LIMIT;
     }
     // WavefrontPathTracer.cpp:120-264 (SoA instead of AoS)
     const size_t P = poolSize;
-    CHECKED(DeviceAlloc(&pool.hit, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.hitInst, P, &poolAllocs));
+    CHECKED(DeviceAlloc(&pool.hit, 2 * P, &poolAllocs));   // 2 float4 per extension-queue item
     CHECKED(DeviceAlloc(&pool.pixel, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.pixelSample, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.state, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.rngNew, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.extOpacity, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowOpacity, P, &poolAllocs));
@@ -451,6 +365,9 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     // (32-bit byte offsets address one parity's records: at most 2^32 bytes, e.g. 2^26 slots)
     if ((uint64_t)pool.recCap * kShards * 32u > (1ull << 32)) { SetLastError("path pool too large for the extension-queue records"); return DCRT_E_LIMIT; }
     CHECKED(DeviceAlloc(&extRecs, (size_t)pool.recCap * kShards * 2 * 2, &poolAllocs));
+    // the paths' state records and their shadow rays' results, at the same positions
+    CHECKED(DeviceAlloc(&stateRecs, (size_t)pool.recCap * kShards * 2, &poolAllocs));
+    CHECKED(DeviceAlloc(&shadowHits, (size_t)pool.recCap * kShards * 2, &poolAllocs));
     // the shadow queue (filled and cast within one iteration): records + path slots
     CHECKED(DeviceAlloc(&pool.shRec, (size_t)pool.recCap * kShards * 2, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowQueue, (size_t)pool.recCap * kShards, &poolAllocs));
@@ -462,7 +379,8 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
         const uint64_t rounds = (P + G * kMaterialBlock - 1) / (G * kMaterialBlock);
         pool.finCap = (uint32_t)(((G + kFinShards - 1) / kFinShards) * rounds * kMaterialBlock);
     }
-    CHECKED(DeviceAlloc(&finQueues, (size_t)pool.finCap * kFinShards * 2, &poolAllocs));
+    CHECKED(DeviceAlloc(&finRecs, (size_t)pool.finCap * kFinShards * 2, &poolAllocs));
+    CHECKED(DeviceAlloc(&finHits, (size_t)pool.finCap * kFinShards * 2, &poolAllocs));
     pool.size = poolSize;
     CHECKED(DeviceAlloc(&dFrame, 1, &poolAllocs));
     CHECKED(DeviceAlloc(&dSampleOut, 1, &poolAllocs));
@@ -559,18 +477,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
                      " is below the uploaded BVH's depth " + std::to_string(stackNeed));
         return DCRT_E_INVALID_ARG;
     }
-    {
-#ifdef DCRT_REFERENCE_NODE_LAYOUT
-        CHECKED(upload(&nodes, s.bvh_nodes, s.bvh_node_count));
-#else
-        std::vector<dcrt_bvh_node> relaid;
-        std::vector<uint32_t> newIndex;
-        PairLayout(s, 4096u, &relaid, &newIndex);
-        if (relaid.size() != s.bvh_node_count) { SetLastError("BVH nodes referenced twice"); return DCRT_E_INVALID_ARG; }
-        CHECKED(upload(&nodes, relaid.data(), relaid.size()));
-        HIPCHECK(hipStreamSynchronize(stream));   // (relaid is a host temporary)
-#endif
-    }
+    CHECKED(upload(&nodes, s.bvh_nodes, s.bvh_node_count));
     uint32_t* mids = nullptr; uint32_t* lidx = nullptr; uint32_t* iflags = nullptr; uint32_t* ovr = nullptr;
     dcrt_material* mats = nullptr; dcrt_light* lights = nullptr;
     CHECKED(upload(&mids, s.material_ids, s.triangle_count));
@@ -916,8 +823,14 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     PathPool pool = this->pool;
     pool.extRec = extRecs + (size_t)par * kShards * pool.recCap * 2;
     pool.extPrevRec = extRecs + (size_t)(par ^ 1u) * kShards * pool.recCap * 2;
-    pool.finQueue = finQueues + (size_t)par * kFinShards * pool.finCap;
-    pool.finPrev = finQueues + (size_t)(par ^ 1u) * kFinShards * pool.finCap;
+    pool.state = stateRecs + (size_t)par * kShards * pool.recCap;
+    pool.statePrev = stateRecs + (size_t)(par ^ 1u) * kShards * pool.recCap;
+    pool.shadowHit = shadowHits + (size_t)par * kShards * pool.recCap;
+    pool.shadowHitPrev = shadowHits + (size_t)(par ^ 1u) * kShards * pool.recCap;
+    pool.finRec = finRecs + (size_t)par * kFinShards * pool.finCap;
+    pool.finPrevRec = finRecs + (size_t)(par ^ 1u) * kFinShards * pool.finCap;
+    pool.finHit = finHits + (size_t)par * kFinShards * pool.finCap;
+    pool.finHitPrev = finHits + (size_t)(par ^ 1u) * kFinShards * pool.finCap;
     // CONTROL and MATERIAL get one workgroup per 256 slots (their grid-stride loops then run
     // once): the hardware dispatcher balances them, where a capped grid leaves a partial
     // second round of workgroups (occupancy 7 and 3 waves/SIMD, not 8) as a tail.
