@@ -16,6 +16,7 @@ constexpr uint32_t kFlagIdle = 0x80000000u;           // WavefrontPathTracing.hl
 constexpr uint32_t kFlagShadowRayHit = 0x40000000u;
 constexpr uint32_t kFlagTerminate = 0x20000000u;
 constexpr uint32_t kFlagDelta = 0x10000000u;           // the path's last BSDF lobe was a delta (SPathAccumulation.isDelta)
+constexpr uint32_t kFlagFirst = 0x08000000u;           // a new path's state record holds NEW_PATH's rng only (PathState)
 constexpr uint32_t kBlockW = 8, kBlockH = 8;           // one wave64 = one 8x8 pixel block
 #ifndef DCRT_CONTROL_BLOCK
 #define DCRT_CONTROL_BLOCK 256
@@ -203,12 +204,15 @@ DEV T& sample_at(T* base, uint32_t i)
 // (CONTROL for a new path, MATERIAL for a continuing one) and read densely by the next
 // MATERIAL pass at the same position -- no slot-indexed state, so no access to a 128-B
 // line half of which belongs to an ended path, and no load that waits for the slot.
-// xoshiro state, throughput + bsdfPdf, Li + lsr.x, (lsr.y, lsr.z, flags, path slot).
+// xoshiro state, (lsr.y, lsr.z, flags, path slot), throughput + bsdfPdf, Li + lsr.x. A new
+// path's record is its first 32 B only (CONTROL: rng and the misc word with kFlagFirst; one
+// whole 32-B sector): its T = 1, bsdfPdf = 0, Li = 0, lsr = 0 are NEW_PATH's constants,
+// which its first MATERIAL pass takes instead of the unwritten half.
 struct PathState {
     uint4 rng;
+    float4 lsrMisc;  // lsr.y, lsr.z, asfloat(flags: first, delta, bounce), asfloat(path slot)
     float4 thr;      // T.xyz, bsdfPdf
     float4 liLsr;    // Li.xyz, lsr.x
-    float4 lsrMisc;  // lsr.y, lsr.z, asfloat(flags: delta, bounce), asfloat(path slot)
 };
 // A path MATERIAL ends with its shadow ray pending: what CONTROL's completion needs
 // (Li += lsr when the shadow ray is unoccluded, WriteSample), at its finish-queue position.

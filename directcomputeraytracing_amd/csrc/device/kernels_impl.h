@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     uint32_t* cursor = &g->nextBlock[shard * kShardStride];
     // pixel blocks of this shard: shard, shard + kShards, ...
     const uint32_t shardBlocks = g->totalBlocks > shard ? (g->totalBlocks - shard + kShards - 1) / kShards : 0u;
-    const bool staticFill = g->staticFill != 0u;   // (the grid then covers the pool exactly once)
+    const bool staticFill = g->staticFill != 0u;
     if (!staticFill) {
         // (one read for the workgroup: the scan below holds barriers, so the exit must be uniform)
         __shared__ uint32_t exhausted;
@@ -229,8 +229,11 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
         __syncthreads();
         if (exhausted) return;
     }
+    // (the grid is a multiple of kShards, or one round: every virtual workgroup vb of this
+    // workgroup is in its shard)
     for (uint32_t base = blockIdx.x * blockDim.x; base < pool.size; base += gridDim.x * blockDim.x) {
     const uint32_t tid = base + threadIdx.x;
+    const uint32_t vb = base / kControlBlock;
     const bool idle = (pool.flags[tid] & kFlagIdle) != 0;
     // A fully idle wave claims the next 8x8 block (one atomic per workgroup); at a batch
     // start (all slots idle, cursors preset) wave j of the shard takes block j outright.
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     uint32_t claimed = 0;
     bool got = false;
     if (staticFill) {
-        claimed = (blockIdx.x / kShards) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        claimed = (vb / kShards) * (kControlBlock >> 6) + (threadIdx.x >> 6);
         got = waveIdle && claimed < shardBlocks;
     } else {
         bool want = false;
@@ -280,13 +283,12 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
         float4* r = ext_rec(pool.extRec, q);
         r[0] = make_float4(o.x, o.y, o.z, 0.0f);
         r[1] = make_float4(d.x, d.y, d.z, asf(tid));
-        // NEW_PATH's state (:227-237): Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0,
-        // isDelta = true, bounce 0 -- beside the ray, densely
+        // NEW_PATH's state (:227-237) beside the ray: the rng, isDelta = true, bounce 0, the
+        // slot (32 B); Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0 are implicit
+        // (kFlagFirst: writing all 64 B cost the 4K batches' first passes 3 GB of writes)
         PathState& st = state_at(pool.state, q);
         st.rng = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
-        st.thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-        st.liLsr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        st.lsrMisc = make_float4(0.0f, 0.0f, asf(kFlagDelta), asf(tid));
+        st.lsrMisc = make_float4(0.0f, 0.0f, asf(kFlagDelta | kFlagFirst), asf(tid));
     }
     }
 }
@@ -352,10 +354,14 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         const V3 dir = mk(hd.x, hd.y, hd.z);
         const uint4 r4 = ps.rng;
         Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
-        float4 thr = ps.thr;
-        const float4 l4 = ps.liLsr, l2 = ps.lsrMisc;
+        const float4 l2 = ps.lsrMisc;
         path = asu(l2.w);
         uint32_t flags = asu(l2.z);
+        // a new path's first pass: NEW_PATH's constants, not the record's unwritten half
+        const bool first = (flags & kFlagFirst) != 0u;
+        flags &= ~kFlagFirst;
+        float4 thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : ps.thr;
+        const float4 l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ps.liLsr;
         F3 li{l4.x, l4.y, l4.z};
         {
             // CONTROL's Li += light sampling result (:520-528), done here for live paths (a

@@ -50,14 +50,6 @@ constexpr uint32_t kMaxImageBatch = 64;               // images in flight per Re
 #endif
 constexpr uint32_t kMaterialBlock = DCRT_MATERIAL_BLOCK;   // MATERIAL workgroup (one queue-append atomic each)
 constexpr uint32_t kMaxPersistentBlocks = 256 * 8;   // CUs x resident workgroups
-#ifndef DCRT_CONTROL_MAX_BLOCKS
-#define DCRT_CONTROL_MAX_BLOCKS 0xFFFFFFFFu
-#endif
-#ifndef DCRT_MATERIAL_MAX_BLOCKS
-#define DCRT_MATERIAL_MAX_BLOCKS 0xFFFFFFFFu
-#endif
-constexpr uint32_t kControlMaxBlocks = DCRT_CONTROL_MAX_BLOCKS;
-constexpr uint32_t kMaterialMaxBlocks = DCRT_MATERIAL_MAX_BLOCKS;
 
 template <typename T>
 int DeviceAlloc(T** p, size_t count, std::vector<void*>* owner)
@@ -181,6 +173,9 @@ struct dcrt_tracer {
     hipStream_t stream = nullptr;
     bool ownsStream = false;
     uint32_t poolSize = 0;
+    // CONTROL / MATERIAL grids (ResidentGrid): workgroups that loop over the pool's 256-slot
+    // "virtual workgroups" vb = blockIdx.x + round * gridDim.x
+    uint32_t controlGrid = 0, materialGrid = 0;
     uint32_t iterationsPerRender = kDefaultIterations;
     bool debugRng = false;
     uint32_t refillLanes = 36, parkLanes = 24;   // DCRT_TRAVERSAL_TUNE="refill,park" overrides (profiles/r01_tune_sweep.txt)
@@ -350,18 +345,41 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.extOpacity, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowOpacity, P, &poolAllocs));
-    // the extension and finish queues: one per iteration parity (extRecs / finQueues). An
-    // extension-queue shard s receives the new paths of CONTROL's workgroups b = s mod
-    // kShards and the continuing paths of MATERIAL's (one 256-slot / 256-item round each when
-    // their grids cover the pool): at most 2 ceil(G / kShards) 256 entries; a capped grid
-    // (several rounds) falls back to the whole pool per shard.
+    // the extension and finish queues: one per iteration parity (extRecs / finRecs)
+    static_assert(kControlBlock == 256u && kMaterialBlock == 256u, "queue capacities assume 256-slot workgroups");
+    const uint32_t V = poolSize / 256u;   // virtual workgroups (256 slots / items each)
     {
-        const uint32_t G = (poolSize + 255u) / 256u;
-        const bool oneRound = std::min<uint32_t>(poolSize / kControlBlock, kControlMaxBlocks) * kControlBlock >= poolSize &&
-                              std::min<uint32_t>(G, kMaterialMaxBlocks) * kMaterialBlock >= poolSize && kControlBlock == 256u &&
-                              kMaterialBlock == 256u;
-        pool.recCap = oneRound ? std::min<uint32_t>(poolSize, 2u * ((G + kShards - 1) / kShards) * 256u) : poolSize;
+        // One workgroup per virtual workgroup would make a pass over an idle or nearly empty
+        // pool cost the dispatch of P / 256 workgroups (2^26 slots: 262144 workgroups,
+        // CONTROL 91 us and MATERIAL 57 us with nothing to do). The grids hold what is
+        // resident instead, a multiple of kShards (= kFinShards), so a workgroup's virtual
+        // workgroups all belong to its own shard: vb mod kShards = blockIdx.x mod kShards.
+        // DCRT_CONTROL_GRID / DCRT_MATERIAL_GRID = k: k x resident; 0: one workgroup per virtual
+        // workgroup (A/B overrides).
+        hipDeviceProp_t prop;
+        HIPCHECK(hipGetDeviceProperties(&prop, device));
+        int cPerCU = 0, mPerCU = 0;
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&cPerCU, control_kernel, (int)kControlBlock, 0));
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&mPerCU, material_kernel<kCapAll>, (int)kMaterialBlock, 0));
+        auto resident = [&](int perCU, const char* knob, uint32_t mul) {
+            if (const char* g = std::getenv(knob)) mul = (uint32_t)std::max(0, std::atoi(g));
+            if (mul == 0) return V;
+            const uint64_t r = (uint64_t)std::max(1, perCU) * (uint64_t)std::max(1, prop.multiProcessorCount) * mul;
+            const uint32_t g = (uint32_t)std::max<uint64_t>(kShards, r / kShards * kShards);
+            return std::min(g, V);   // (= V: one round, any V)
+        };
+        // 2x / 4x resident (two A/B passes of the default bench on cornell / spaceship / coffee,
+        // ms/spp: one workgroup per virtual workgroup 2.40 / 2.84 / 2.96; 1x / 1x 2.28-2.38 /
+        // 2.63 / 3.02; 1x / 4x 2.37 / 2.58 / 2.95; 2x / 4x 2.35-2.38 / 2.54 / 2.92; 4x / 4x
+        // 2.37 / 2.55 / 2.95; 2x / 8x 2.37-2.39 / 2.55 / 2.92)
+        controlGrid = resident(cPerCU, "DCRT_CONTROL_GRID", 2);
+        materialGrid = resident(mPerCU, "DCRT_MATERIAL_GRID", 4);
+        static_assert(kFinShards == kShards, "MATERIAL's grid is a multiple of both shard counts");
     }
+    // The extension queue's shard s receives the new paths of CONTROL's virtual workgroups
+    // vb = s mod kShards and the continuing paths of MATERIAL's (at most 256 each): at most
+    // 2 ceil(V / kShards) 256 entries
+    pool.recCap = std::min<uint32_t>(poolSize, 2u * ((V + kShards - 1) / kShards) * 256u);
     // (32-bit byte offsets address one parity's records: at most 2^32 bytes, e.g. 2^26 slots)
     if ((uint64_t)pool.recCap * kShards * 32u > (1ull << 32)) { SetLastError("path pool too large for the extension-queue records"); return DCRT_E_LIMIT; }
     CHECKED(DeviceAlloc(&extRecs, (size_t)pool.recCap * kShards * 2 * 2, &poolAllocs));
@@ -372,13 +390,9 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     CHECKED(DeviceAlloc(&pool.shRec, (size_t)pool.recCap * kShards * 2, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowQueue, (size_t)pool.recCap * kShards, &poolAllocs));
 
-    {
-        // MATERIAL workgroup b appends the paths it ends with a shadow ray pending to finish
-        // shard b % kFinShards
-        const uint64_t G = std::min<uint32_t>((poolSize + kMaterialBlock - 1) / kMaterialBlock, kMaterialMaxBlocks);
-        const uint64_t rounds = (P + G * kMaterialBlock - 1) / (G * kMaterialBlock);
-        pool.finCap = (uint32_t)(((G + kFinShards - 1) / kFinShards) * rounds * kMaterialBlock);
-    }
+    // MATERIAL's virtual workgroup vb appends the paths it ends with a shadow ray pending to
+    // finish shard vb mod kFinShards
+    pool.finCap = ((V + kFinShards - 1) / kFinShards) * kMaterialBlock;
     CHECKED(DeviceAlloc(&finRecs, (size_t)pool.finCap * kFinShards * 2, &poolAllocs));
     CHECKED(DeviceAlloc(&finHits, (size_t)pool.finCap * kFinShards * 2, &poolAllocs));
     pool.size = poolSize;
@@ -831,11 +845,6 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     pool.finPrevRec = finRecs + (size_t)(par ^ 1u) * kFinShards * pool.finCap;
     pool.finHit = finHits + (size_t)par * kFinShards * pool.finCap;
     pool.finHitPrev = finHits + (size_t)(par ^ 1u) * kFinShards * pool.finCap;
-    // CONTROL and MATERIAL get one workgroup per 256 slots (their grid-stride loops then run
-    // once): the hardware dispatcher balances them, where a capped grid leaves a partial
-    // second round of workgroups (occupancy 7 and 3 waves/SIMD, not 8) as a tail.
-    const uint32_t controlGrid = std::min<uint32_t>(poolSize / kControlBlock, kControlMaxBlocks);
-    const uint32_t materialGrid = std::min<uint32_t>((poolSize + kMaterialBlock - 1) / kMaterialBlock, kMaterialMaxBlocks);
     const bool opacity = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) != 0;
     const uint32_t castGrid = CastGrid(castBlock, opacity);
     hipLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, pool, film, (const FrameConstants*)dFrame, cnt,
@@ -1033,9 +1042,8 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     frame.frame_seed = firstSeed;
     CHECKED(UploadFilter(filter));
     CHECKED(BeginImage());
-    // static batch-start claims need one CONTROL thread per slot (an uncapped grid)
-    const uint32_t controlGrid = poolSize / kControlBlock;
-    const uint32_t staticGrid = controlGrid <= kControlMaxBlocks ? controlGrid : 0u;
+    // static batch-start claims: one per wave of CONTROL's virtual workgroups
+    const uint32_t staticGrid = poolSize / kControlBlock;
     hipLaunchKernelGGL(begin_images_kernel, dim3(1), dim3(64), 0, stream, dGlobals, (const FrameConstants*)dFrame, count, firstSeed, batch,
                        staticGrid);
     HIPCHECK(hipGetLastError());

@@ -12,7 +12,7 @@ CONFIG="${CONFIG:-spaceship}"
 STEPS="${STEPS:-8}"
 OUT="$ROOTDIR/${OUT:-gpurun_out/prof_$CONFIG}"
 mkdir -p "$OUT"
-ARGS="--config $CONFIG --steps $STEPS --warmup 0 --no-cpu-baseline --streams 1 ${PROF_ARGS:-}"
+ARGS="--config $CONFIG --steps $STEPS --warmup 0 --no-cpu-baseline --streams 1 --repeats 1 --spaceship-spp 0 ${PROF_ARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT" -o trace -- \
     python3 "$ROOTDIR/bench.py" $ARGS > "$OUT/trace_bench.log" 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
