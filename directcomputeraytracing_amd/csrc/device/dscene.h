@@ -294,6 +294,10 @@ struct TravState {
     uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked; not kept with ALL_CACHED)
     bool found, parked, noZero;   // noZero: no component of o, d is +-0
     bool anyHit;          // merged cast kernel: this lane's ray is a shadow ray (first hit ends it)
+    // trav_visit_pair: `node` is a hit interior node whose children are tested next
+    // (expand), its right child (with the BLAS bit) and near-child choice
+    bool expand, expNeg;
+    uint32_t expRight;
     // Near/far choice of the current space: bit a = (ld[a] < 0) for the axes a = 0..2,
     // bit 3 = front-to-back order on (0: the whole mask is 0, near child = node + 1 always)
     uint32_t negMask;
@@ -322,6 +326,7 @@ DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax, bool f2b = 
     s.node = 0; s.sp = 0; s.inst = 0;
     s.leafRef = 0; s.leafMisc = 0;
     s.found = false; s.parked = false; s.anyHit = false;
+    s.expand = false; s.expNeg = false; s.expRight = 0;
     s.noZero = o.x != 0.0f && o.y != 0.0f && o.z != 0.0f && d.x != 0.0f && d.y != 0.0f && d.z != 0.0f;
     s.hit.t = 0.0f; s.hit.u = 0.0f; s.hit.v = 0.0f; s.hit.tri = 0u; s.hit.inst = 0u;
     s.opacitySample = 0.0f; s.matOverride = DCRT_INSTANCE_MATERIAL_OVERRIDE_NONE; s.opaque = false;
@@ -371,6 +376,7 @@ DEV bool trav_pop(TravState& s, uint32_t* lds, uint32_t stride)
     if (s.sp == 0u) return true;
     const uint32_t packed = stack_at(lds, s.sp);
     s.sp -= stride;
+    s.expand = false;
     const bool restore = (int)s.node < 0 && (int)packed >= 0;   // BLAS -> TLAS
     s.node = packed;
     if (restore) {
@@ -461,6 +467,77 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         s.leafRef = right;
         s.leafMisc = misc;
     }
+    return done;
+}
+
+// Phase A with one dependent fetch per hit interior node instead of one per visited node
+// (the non-instrumented kernels; the counting kernels keep trav_visit). A node reached by
+// a pop or a BLAS entry is visited as in trav_visit (its box tested with the current tMax);
+// a hit interior node is then expanded: both child records are fetched together and both
+// boxes tested with the current tMax. The near child (by the split axis' direction sign) is
+// taken when it hits, the far one pushed when both hit, taken when only it hits.
+// Same leaves, same order, same tMax at each leaf as BVHIntersect[NoInterp]
+// (BVHAccel.inc.hlsl:119-229), hence the same hits bit for bit:
+// * the near child is tested with the tMax the reference's next visit would use (no leaf
+//   lies between the two tests);
+// * a far child that misses at the parent would miss at its pop too: ray_aabb's only tMax
+//   term is t0 < tMax and tMax never grows;
+// * a far child that hits at the parent is pushed and tested again when popped (visit).
+// The stack holds a subset of the reference's entries (a push needs both children to hit),
+// so the uploaded stack size bounds it too.
+template <bool ALL_CACHED = false>
+DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift)
+{
+    const uint32_t stride = stack_stride<ALL_CACHED>(shift);
+    const uint32_t top = stack_at(lds, s.sp);
+    const uint32_t blasBit = s.node & 0x80000000u;
+    const uint32_t nextRef = s.node + 1u;
+    // record A: the node itself (visit) or its near child (expand); record B: the far child
+    // (expand only)
+    const uint32_t aRef = s.expand ? (s.expNeg ? s.expRight : nextRef) : s.node;
+    const uint32_t bRef = s.expNeg ? nextRef : s.expRight;
+    auto fetch = [&](uint32_t ref, float4& a, float4& b) __attribute__((always_inline)) {
+        const uint32_t idx = ref & 0x7FFFFFFFu;
+        if (ALL_CACHED || idx < sc.cachedNodes) {
+            const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
+            a = c[idx * 2];
+            b = c[idx * 2 + 1];
+        } else {
+            a = sc.nodes[idx * 2];
+            b = sc.nodes[idx * 2 + 1];
+        }
+    };
+    float4 a0, b0, a1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b1 = a1;
+    fetch(aRef, a0, b0);
+    if (s.expand) fetch(bRef, a1, b1);
+    const bool hitA = ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a0, b0);
+    const bool hitB = s.expand && ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a1, b1);
+    // the node taken next: A if it hits, else B if it hits (push B when both hit)
+    const bool take = hitA | hitB;
+    const uint32_t takeRef = hitA ? aRef : bRef;
+    const uint32_t right = asu(hitA ? b0.z : b1.z);
+    const uint32_t misc = asu(hitA ? b0.w : b1.w);
+    stack_at(lds, s.sp + stride) = bRef;
+    const bool push = hitA & hitB;
+    const bool empty = s.sp == 0u;
+    const bool pop = !take && !empty;
+    const bool done = !take && empty;
+    const bool restore = pop && (int)s.node < 0 && (int)top >= 0;   // BLAS -> TLAS: back to the world ray
+    const bool leaf = misc >= 4u;
+    s.node = take ? takeRef : (pop ? top : s.node);
+    s.sp = push ? s.sp + stride : (pop ? s.sp - stride : s.sp);
+    s.expand = take & !leaf;
+    s.expNeg = __builtin_amdgcn_ubfe(s.negMask, misc, 1u) != 0u;
+    s.expRight = right | blasBit;
+    if (__builtin_expect(restore, 0)) {
+        s.lo = mk(s.o.x, s.o.y, s.o.z);
+        s.ld = mk(s.d.x, s.d.y, s.d.z);
+        s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+        s.negMask = neg_mask(s.d, s.negMask);
+    }
+    s.parked = take & leaf;
+    s.leafRef = right;
+    s.leafMisc = misc;
     return done;
 }
 

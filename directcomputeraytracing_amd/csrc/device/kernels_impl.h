@@ -563,6 +563,12 @@ constexpr int kVisitsPerCheck = DCRT_VISITS_PER_CHECK;
 #endif
 // queue items per round-robin group of the cast kernels' static work split (power of two)
 constexpr uint32_t kInterleave = DCRT_INTERLEAVE;
+// PAIR (persistent_trace): phase A steps with trav_visit_pair instead of trav_visit. The
+// tracer takes it for scenes whose nodes + triangles exceed an XCD's L2 (latency-bound
+// fetches: spaceship 2.50 -> 2.46 ms/spp); on L2-resident scenes the second box test per
+// step costs more than the shorter fetch chain saves (coffee 2.92 -> 3.02, lamp 7.21 ->
+// 7.48). The test / megakernel paths always use it (the GPU parity tests cover it on every
+// scene).
 
 #ifdef DCRT_WAVE_TIMELINE
 // Diagnostic build only (tools/wave_timeline.py): per-wave start/end realtime stamps
@@ -575,8 +581,8 @@ __device__ uint32_t g_waveItems[2][16][8192];
 #endif
 
 
-template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, typename Lookup, typename Fetch,
-          typename Emit>
+template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, bool PAIR = false, typename Lookup,
+          typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
                                                  uint32_t kParkLanes, uint32_t* lds, uint32_t shift, Lookup lookup, Fetch fetch,
                                                  Emit emit, TraversalStats& st, int waveTag = -1)
@@ -648,7 +654,9 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
 #pragma unroll
             for (int k = 0; k < kVisitsPerCheck; ++k) {
                 if (ls == kRun) {
-                    if (trav_visit<INSTR, ALL_CACHED>(sc, s, lds, shift, st)) ls = kFin;
+                    const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair(sc, s, lds, shift)
+                                                                   : trav_visit<INSTR, ALL_CACHED>(sc, s, lds, shift, st);
+                    if (fin) ls = kFin;
                     else if (s.parked) ls = kPark;
                 }
             }
@@ -797,7 +805,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
 // iteration instead of two, and a shadow ray can fill a lane an extension ray left
 // idle. Per lane the ray keeps its own semantics (closest hit vs first hit), so the
 // results are those of the two separate kernels.
-template <bool INSTR, bool OPACITY, bool ALL_CACHED>
+template <bool INSTR, bool OPACITY, bool ALL_CACHED, bool PAIR>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHED_CAST_WAVES_PER_EU : DCRT_CAST_WAVES_PER_EU, 8))) void cast_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
                                                                      Counters* nextCnt, Globals* g, unsigned long long* instr)
@@ -813,7 +821,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     const float4* shRec = sgpr_ptr((const float4*)pool.shRec);
     TraversalStats st = {};
     TraversalStats stExt = {}, stShadow = {};
-    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED>(
+    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
             // either kind: its record's position in its queue (no load)
@@ -875,7 +883,7 @@ __device__ __forceinline__ bool trace_full(const DeviceScene& sc, V3 o, V3 d, fl
     s.opacitySample = opacitySample;
     TraversalStats st = {};
     for (;;) {
-        if (trav_visit<false>(sc, s, lds, shift, st)) break;
+        if (trav_visit_pair(sc, s, lds, shift)) break;
         if (s.parked && trav_leaf<ANY_HIT, false, OPACITY>(sc, s, watertight, lds, shift, st)) break;
     }
     *hit = s.hit;
@@ -1015,14 +1023,15 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
 }
 
 // ---- kernel-level batch entry points (tests / roofline) -----------------------------------
-template <bool ANY>
+// INSTR: count the reference's traversal (trav_visit); otherwise the kernels' trav_visit_pair
+template <bool ANY, bool INSTR>
 __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const dcrt_ray* rays, uint32_t n, uint32_t features,
                                                            dcrt_ray_hit* hits, uint32_t* occluded, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
     scene_cache_load(sc, stackMem, block_shift());
     TraversalStats st = {};
-    persistent_trace<ANY, true, false>(
+    persistent_trace<ANY, INSTR, false, false, false, !INSTR>(
         sc, n, features, 16u, 32u, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) { return i; },
         [&](uint32_t i, uint32_t, TravState& s) __attribute__((always_inline)) {
@@ -1041,7 +1050,7 @@ __global__ __launch_bounds__(256) void batch_trace_kernel(DeviceScene sc, const 
             }
         },
         st);
-    if (instr) flush_stats(st, instr);
+    if (INSTR) flush_stats(st, instr);
 }
 
 __global__ void math_eval_kernel(int function, const float* x, uint32_t n, float* y)
@@ -1430,18 +1439,22 @@ template __global__ void shadow_kernel<false, false>(PathPool, DeviceScene, cons
 template __global__ void shadow_kernel<false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void shadow_kernel<true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void shadow_kernel<true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<false, false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<false, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<false, true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<false, true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<true, false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<true, true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
-template __global__ void cast_kernel<true, true, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, false, false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, false, true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, true, false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, true, true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, false, false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, false, true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, true, false, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, true, true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, false, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void megakernel<false>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void megakernel<true>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
-template __global__ void batch_trace_kernel<false>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
-template __global__ void batch_trace_kernel<true>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
+template __global__ void batch_trace_kernel<false, false>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
+template __global__ void batch_trace_kernel<true, false>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
+template __global__ void batch_trace_kernel<false, true>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
+template __global__ void batch_trace_kernel<true, true>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);
 
 }  // namespace dev
 }  // namespace dcrt

@@ -107,12 +107,14 @@ uint32_t FilterSupportRows(float r, uint32_t H)
 
 using CastFn = void (*)(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 // cast_kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER x whole scene in the LDS cache
-CastFn CastKernel(bool instr, bool opacity, bool allCached)
+// x pair-expanding traversal (the non-counting kernels of scenes not in the LDS cache)
+CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair)
 {
     static const CastFn table[8] = {
-        cast_kernel<false, false, false>, cast_kernel<false, false, true>, cast_kernel<false, true, false>,
-        cast_kernel<false, true, true>, cast_kernel<true, false, false>, cast_kernel<true, false, true>,
-        cast_kernel<true, true, false>, cast_kernel<true, true, true>};
+        cast_kernel<false, false, false, false>, cast_kernel<false, false, true, false>, cast_kernel<false, true, false, false>,
+        cast_kernel<false, true, true, false>, cast_kernel<true, false, false, false>, cast_kernel<true, false, true, false>,
+        cast_kernel<true, true, false, false>, cast_kernel<true, true, true, false>};
+    if (pair && !instr && !allCached) return opacity ? cast_kernel<false, true, false, true> : cast_kernel<false, false, false, true>;
     return table[(instr ? 4 : 0) + (opacity ? 2 : 0) + (allCached ? 1 : 0)];
 }
 
@@ -192,7 +194,8 @@ struct dcrt_tracer {
     bool hasScene = false;
     uint32_t castBlock = 256;
     size_t castLds = 0;
-    bool castAllCached = false;        // the scene fits the LDS cache: cast_kernel<., ., true>
+    bool castAllCached = false;        // the scene fits the LDS cache: cast_kernel<., ., true, .>
+    bool castPair = false;             // trav_visit_pair: the scene outgrows an XCD's L2 (UploadScene)
     bool mergedCasts = true;           // one cast_kernel per iteration (DCRT_SPLIT_CASTS=1: EXT then SHADOW)
     uint32_t sceneCaps = kCapAll;      // what the uploaded scene uses (kCap* of dscene.h)
     uint32_t materialCaps = kCapAll;   // the MATERIAL variant launched for it
@@ -605,7 +608,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         // LDS scene cache in what the cast kernel's register-limited occupancy leaves of the
         // CU's 160 KiB per workgroup: BVH nodes first, then pre-gathered triangles
         int regPerCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false, false>, (int)castBlock, castLds));
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false, false, false>, (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, extension_kernel<false, false>, (int)castBlock, castLds));
         const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
         const size_t budget = castLds < perBlock ? perBlock - castLds : 0;
@@ -619,6 +622,10 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         castAllCached = castBlock == 256 && d.cachedNodes == s.bvh_node_count && d.cachedTris == s.triangle_count &&
                         (size_t)d.cachedNodes * 32 + (size_t)s.triangle_count * 144 + (size_t)s.instance_count * 64 <= budget;
         d.cachedInstances = castAllCached ? s.instance_count : 0u;
+        // trav_visit_pair where the traversal's fetches miss L2: nodes + triangles beyond an
+        // XCD's 4 MiB L2 (DCRT_PAIR_TRAVERSAL=0/1 forces it off / on, A/B and tests)
+        castPair = !castAllCached && (size_t)s.bvh_node_count * 32 + (size_t)s.triangle_count * 48 > ((size_t)4 << 20);
+        if (const char* pv = std::getenv("DCRT_PAIR_TRAVERSAL")) castPair = !castAllCached && std::atoi(pv) != 0;
         castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * (castAllCached ? 144 : 48) + (size_t)d.cachedInstances * 64;
         scene = d;
     }
@@ -627,7 +634,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         hipDeviceProp_t prop;
         HIPCHECK(hipGetDeviceProperties(&prop, device));
         int perCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, CastKernel(false, false, castAllCached), (int)castBlock, castLds));
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, CastKernel(false, false, castAllCached, castPair), (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false, false>, (int)castBlock, castLds));
         if (const char* b = std::getenv("DCRT_CAST_BLOCKS_PER_CU")) {   // tuning experiments
             const int v = std::atoi(b);
@@ -635,7 +642,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         }
         castResident = (uint32_t)std::max(1, perCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int opacityPerCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, CastKernel(false, true, castAllCached), (int)castBlock, castLds));
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, CastKernel(false, true, castAllCached, castPair), (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLds));
         castResidentOpacity = (uint32_t)std::max(1, std::min(opacityPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int megaPerCU = 0;
@@ -866,7 +873,7 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     // (hipExtLaunchKernelGGL), so the duration is the kernel's, as rocprofv3 reports it.
     // kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER
     if (mergedCasts) {
-        auto cast = CastKernel(instrCounters, opacity, castAllCached);
+        auto cast = CastKernel(instrCounters, opacity, castAllCached, castPair);
         hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), castLds, stream, e0, e1, 0, pool, scene,
                               (const FrameConstants*)dFrame, cnt, next, dGlobals, dInstr);
     } else {
@@ -1299,6 +1306,9 @@ DCRT_API int dcrt_tracer_get_info(dcrt_tracer* t, dcrt_tracer_info* out)
     out->cast_block = t->castBlock;
     out->traversal_stack = t->hasScene ? t->scene.stackSize : 0u;
     out->material_generic = t->materialCaps == kCapAll ? 1u : 0u;
+    out->pair_traversal = t->hasScene && t->castPair ? 1u : 0u;
+    out->control_grid = t->controlGrid;
+    out->material_grid = t->materialGrid;
     return DCRT_OK;
 }
 
@@ -1376,10 +1386,9 @@ static int TraceBatch(dcrt_tracer* t, const dcrt_ray* d_rays, uint32_t n, dcrt_r
     const uint32_t grid = std::min<uint32_t>((n + t->castBlock - 1) / t->castBlock, t->castResident);
     if (n == 0) return DCRT_OK;
     unsigned long long* instr = t->instrCounters ? t->dInstr : nullptr;
-    if (any)
-        hipLaunchKernelGGL(batch_trace_kernel<true>, dim3(grid), dim3(t->castBlock), t->castLds, t->stream, t->scene, d_rays, n, features, d_hits, d_occ, instr);
-    else
-        hipLaunchKernelGGL(batch_trace_kernel<false>, dim3(grid), dim3(t->castBlock), t->castLds, t->stream, t->scene, d_rays, n, features, d_hits, d_occ, instr);
+    auto kernel = any ? (instr ? batch_trace_kernel<true, true> : batch_trace_kernel<true, false>)
+                      : (instr ? batch_trace_kernel<false, true> : batch_trace_kernel<false, false>);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(t->castBlock), t->castLds, t->stream, t->scene, d_rays, n, features, d_hits, d_occ, instr);
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
 }

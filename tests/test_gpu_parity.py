@@ -454,19 +454,21 @@ def test_xml_scene_mesh_lights_bit_exact(gpu_tracer, golden_luts, oracle_mod):
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 7]))
 
 
-@pytest.mark.parametrize("cache", ["lds", "global"])
+@pytest.mark.parametrize("cache", ["lds", "global", "pair"])
 @pytest.mark.parametrize("features", [0x05, 0x0F, 0x07])
 @pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
 def test_traversal_variants_wavefront_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, scene_name, features, cache):
     """The merged cast kernel's traversal variants through the whole wavefront path:
     Moller-Trumbore (WATERTIGHT off), BVH_NO_FRONT_TO_BACK_TRAVERSAL, both; the cache-only
     kernel (scene, permuted triangle copies and instance transforms in LDS: both scenes
-    fit) and the global-memory kernel (DCRT_NO_LDS_CACHE). xml_mix has transformed
-    rectangle instances (instance-space rays in the BLAS)."""
+    fit), the global-memory kernel (DCRT_NO_LDS_CACHE) and the global-memory kernel with the
+    pair-expanding traversal (trav_visit_pair). xml_mix has transformed rectangle instances
+    (instance-space rays in the BLAS)."""
     from conftest import GOLDEN
     from directcomputeraytracing_amd import Scene, WavefrontPathTracer
-    if cache == "global":
+    if cache in ("global", "pair"):
         monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+    monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1" if cache == "pair" else "0")
     if scene_name == "cornell":
         s = cornell(64, 48, 6)
     else:
@@ -476,6 +478,7 @@ def test_traversal_variants_wavefront_bit_exact(native_lib, golden_luts, oracle_
     t = WavefrontPathTracer(path_pool_size=1 << 12, debug_rng=True)
     try:
         list(_render_and_compare(t, oracle_mod, golden_luts, s, [0, 3]))
+        assert t.info()["pair_traversal"] == (1 if cache == "pair" else 0)
     finally:
         t.destroy()
 
@@ -496,6 +499,7 @@ def test_full_size_spaceship_mesh_bit_exact(gpu_tracer, golden_luts, oracle_mod,
     s.load_from_file(scenes.write_spaceship(tmp_path, 320, 180, nu=512, nv=256, ships=8))
     assert s.bvh_info()["total_nodes"] > 500_000
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [3]))
+    assert gpu_tracer.info()["pair_traversal"] == 1   # (beyond an XCD's L2: trav_visit_pair)
 
 
 def test_cpp_host_example_matches_python_host(native_lib, tmp_path):
