@@ -1,20 +1,24 @@
 #!/bin/bash
-# GPU box: kernel-trace + PMC profiles of the 20- and 64-image bench workloads (one
-# pipeline), their HBM-traffic summaries into profiles/ (so the bench lines below match
-# them), then the default and the --steps 20 bench lines. Copy the outputs named in the
-# last lines into profiles/rNN_* afterwards.
+# GPU box: kernel-trace + PMC profiles (tools/prof_config.sh, one pipeline) of the three
+# workloads the bench's roofline objects are quoted on -- Cornell 1080p 20 and 64 images
+# (the driver's --steps 20 and the default) and the spaceship leg (4K, 4 images) -- their
+# HBM-traffic summaries into profiles/${TAG}_*_pmc_traffic.json (bench.py matches its runs
+# against them), then the default and the --steps 20 bench lines.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-PMC=1 PROF_STEPS="20 64" bash tools/profile.sh || exit $?
-python tools/pmc_traffic.py gpurun_out/prof_20 gpurun_out/${TAG:-r02}_i20 || exit $?
-python tools/pmc_traffic.py gpurun_out/prof_64 gpurun_out/${TAG:-r02}_i64 || exit $?
-cp gpurun_out/${TAG:-r02}_i20_pmc_traffic.json gpurun_out/${TAG:-r02}_i64_pmc_traffic.json profiles/
+TAG=${TAG:-r03}
+mkdir -p gpurun_out profiles
+for w in "cornell 20 c20" "cornell 64 c64" "spaceship 4 s4"; do
+  set -- $w
+  CONFIG=$1 STEPS=$2 OUT=gpurun_out/prof_$3 tools/prof_config.sh || exit $?
+  python tools/pmc_traffic.py gpurun_out/prof_$3 profiles/${TAG}_$3 || exit $?
+  cp gpurun_out/prof_$3/trace_kernel_stats.csv profiles/${TAG}_$3_kernel_stats.csv
+done
 timeout -k 10 300 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || exit $?
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_s20.json 2> gpurun_out/bench_s20.err || exit $?
 python - <<'PY'
 import json
 for f in ("gpurun_out/bench_default.json", "gpurun_out/bench_s20.json"):
-    d = json.load(open(f)); r = d["roofline"]
-    print(f, d["ms_per_spp"], d["value"], r["frac"], r["avg_launch_us"], r["hbm_measured"], r["traffic_source"][:48])
+    d = json.load(open(f)); r = d["roofline"]; s = d.get("spaceship", {}).get("roofline", {})
+    print(f, d["ms_per_spp"], d["value"], r["frac"], r["avg_launch_us"], r["traffic_source"][:40], s.get("frac"), s.get("traffic_source", "")[:40])
 PY
