@@ -507,9 +507,11 @@ DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uin
             b = sc.nodes[idx * 2 + 1];
         }
     };
-    float4 a0, b0, a1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b1 = a1;
+    // (both fetches unconditional: a visit fetches its node twice, the second from L1, which
+    // costs less than the exec-mask branch and the zeroed registers of a conditional fetch)
+    float4 a0, b0, a1, b1;
     fetch(aRef, a0, b0);
-    if (s.expand) fetch(bRef, a1, b1);
+    fetch(s.expand ? bRef : aRef, a1, b1);
     const bool hitA = ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a0, b0);
     const bool hitB = s.expand && ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a1, b1);
     // the node taken next: A if it hits, else B if it hits (push B when both hit)
