@@ -44,6 +44,9 @@ namespace {
 
 constexpr uint32_t kDefaultPoolSize = 1u << 20;      // 2^20 slots: 16 waves x 256 CUs x 256 (MI355X)
 constexpr uint32_t kDefaultIterations = 8;
+// RenderImages' chunks of iterations once its final batch is in flight: a chunk launched after
+// the images completed finds no work, and two chunks are in flight when the host sees it
+constexpr uint32_t kTailChunk = 4;
 constexpr uint32_t kMaxImageBatch = 64;               // images in flight per RenderImages batch (sample textures: 24 B/px each)
 #ifndef DCRT_MATERIAL_BLOCK
 #define DCRT_MATERIAL_BLOCK 256
@@ -231,10 +234,10 @@ struct dcrt_tracer {
     struct GraphCache {
         hipGraphExec_t exec = nullptr;
         uint32_t iters = 0;
-    } graphs[2];
+    } graphs[3];   // unsequenced (Render), sequenced (RenderImages), sequenced tail chunks
     FilterConsts* dFilter = nullptr;
     FilterConsts* hFilter = nullptr;   // pinned staging
-    uint32_t* hStop = nullptr;         // pinned [kInflight]
+    uint32_t* hStop = nullptr;         // pinned [4][2]: Globals::stopped, imagesDone per poll
     hipEvent_t stopEvents[4] = {};
     bool instrCounters = false;
     bool extTiming = false;
@@ -411,7 +414,7 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     HIPCHECK(hipHostMalloc((void**)&hCounters, 2 * sizeof(Counters), hipHostMallocDefault));
     CHECKED(DeviceAlloc(&dFilter, 1, &poolAllocs));
     HIPCHECK(hipHostMalloc((void**)&hFilter, sizeof(FilterConsts), hipHostMallocDefault));
-    HIPCHECK(hipHostMalloc((void**)&hStop, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    HIPCHECK(hipHostMalloc((void**)&hStop, 8 * sizeof(uint32_t), hipHostMallocDefault));
     for (hipEvent_t& e : stopEvents) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     CHECKED(BuildLuts());
     HIPCHECK(hipStreamSynchronize(stream));
@@ -896,10 +899,12 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
 }
 
 // Replay `iters` iterations (even, starting at parity 0) as one captured graph.
+// RenderImages' graph of tail chunks (its final batch) holds kTailChunk iterations
+static uint32_t GraphSlot(bool sequenced, uint32_t iters) { return !sequenced ? 0u : (iters == kTailChunk ? 2u : 1u); }
 int dcrt_tracer::LaunchGraph(bool sequenced, uint32_t iters)
 {
     CHECKED(BuildGraph(sequenced, iters));
-    HIPCHECK(hipGraphLaunch(graphs[sequenced ? 1 : 0].exec, stream));
+    HIPCHECK(hipGraphLaunch(graphs[GraphSlot(sequenced, iters)].exec, stream));
     return DCRT_OK;
 }
 
@@ -907,7 +912,7 @@ int dcrt_tracer::LaunchGraph(bool sequenced, uint32_t iters)
 // a reallocation (EnsureSamples) invalidates it.
 int dcrt_tracer::BuildGraph(bool sequenced, uint32_t iters)
 {
-    GraphCache& gc = graphs[sequenced ? 1 : 0];
+    GraphCache& gc = graphs[GraphSlot(sequenced, iters)];
     if (!gc.exec || gc.iters != iters) {
         if (gc.exec) (void)hipGraphExecDestroy(gc.exec);
         gc.exec = nullptr;
@@ -933,7 +938,11 @@ int dcrt_tracer::PrepareImages(uint32_t count)
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
     if (count == 0 || mode == 1) return DCRT_OK;
     CHECKED(EnsureSamples(AutoBatch(count)));
-    if (!extTiming) CHECKED(BuildGraph(true, std::max<uint32_t>(2, iterationsPerRender & ~1u)));
+    if (!extTiming) {
+        const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
+        CHECKED(BuildGraph(true, chunk));
+        if (chunk > kTailChunk) CHECKED(BuildGraph(true, kTailChunk));
+    }
     HIPCHECK(hipStreamSynchronize(stream));
     return DCRT_OK;
 }
@@ -1060,11 +1069,16 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     bool stopped = false;
     {
         // chunks of `chunk` iterations (a replayed graph, or plain timed launches when the
-        // EXT kernel is being timed), the "stopped" word polled two chunks behind
-        const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
+        // EXT kernel is being timed), the "stopped" word polled two chunks behind; once the
+        // final batch is in flight (imagesDone + batch >= count, polled with it), chunks of
+        // kTailChunk: the chunks launched after the last image completes find no work
+        // (32 empty iterations after a one-batch call took 0.4 ms with 16-iteration chunks)
+        const uint32_t bigChunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
+        bool finalBatch = count <= batch;
         uint32_t inflight[4];
         uint32_t head = 0, size = 0, slot = 0;
         while (!stopped && launched < maxIterations) {
+            const uint32_t chunk = finalBatch ? std::min(bigChunk, kTailChunk) : bigChunk;
             if (extTiming) {
                 for (uint32_t i = 0; i < chunk; ++i) {
                     CHECKED(LaunchIteration(parity, true, true));
@@ -1074,7 +1088,8 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
                 CHECKED(LaunchGraph(true, chunk));
             }
             launched += chunk;
-            HIPCHECK(hipMemcpyAsync(&hStop[slot], &dGlobals->stopped, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+            static_assert(offsetof(Globals, imagesDone) == offsetof(Globals, stopped) + 4, "polled together");
+            HIPCHECK(hipMemcpyAsync(&hStop[2 * slot], &dGlobals->stopped, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
             HIPCHECK(hipEventRecord(stopEvents[slot], stream));
             inflight[(head + size) % 4] = slot;
             ++size;
@@ -1082,7 +1097,8 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
             if (size >= 2) {
                 const uint32_t s0 = inflight[head];
                 HIPCHECK(hipEventSynchronize(stopEvents[s0]));
-                stopped = hStop[s0] != 0;
+                stopped = hStop[2 * s0] != 0;
+                finalBatch = finalBatch || (uint64_t)hStop[2 * s0 + 1] + batch >= count;
                 head = (head + 1) % 4;
                 --size;
             }
