@@ -664,7 +664,17 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             const uint32_t parked = (uint32_t)__popcll(__ballot(ls == kPark));
             const uint32_t idle = 64u - (uint32_t)__popcll(runnable) - parked;
             DCRT_PHASE_COUNT(4);
-            if (runnable == 0ull || parked >= kParkLanes || (idle >= kRefillLanes && cursor < end)) break;
+#ifndef DCRT_ADAPTIVE_PARK
+#define DCRT_ADAPTIVE_PARK 1
+#endif
+#ifndef DCRT_PARK_EIGHTHS
+#define DCRT_PARK_EIGHTHS 4
+#endif
+            // leaf work once kParkLanes lanes wait at leaves -- or half of the wave's rays, when
+            // it holds few (a drain's sparse waves: a lane parked at a leaf would otherwise wait
+            // for every other ray to reach one)
+            const uint32_t parkAt = DCRT_ADAPTIVE_PARK ? min(kParkLanes, max(1u, ((64u - idle) * DCRT_PARK_EIGHTHS) >> 3)) : kParkLanes;
+            if (runnable == 0ull || parked >= parkAt || (idle >= kRefillLanes && cursor < end)) break;
         }
         DCRT_PHASE(1);
         // phase B: the parked lanes' leaf work, shared by many lanes at once

@@ -183,7 +183,12 @@ struct dcrt_tracer {
     uint32_t controlGrid = 0, materialGrid = 0;
     uint32_t iterationsPerRender = kDefaultIterations;
     bool debugRng = false;
-    uint32_t refillLanes = 36, parkLanes = 24;   // DCRT_TRAVERSAL_TUNE="refill,park" overrides (profiles/r01_tune_sweep.txt)
+    // cast-kernel refill / park thresholds (persistent_trace): refill when 36 lanes are idle
+    // in the LDS-only kernel, 28 in the global-memory one (round 3 sweep with the adaptive
+    // park threshold); park at 24 (profiles/r01_tune_sweep.txt); DCRT_TRAVERSAL_TUNE=
+    // "refill,park" overrides both
+    uint32_t refillLanes = 36, parkLanes = 24;
+    bool tuneOverride = false;
     uint64_t imagesCompleted = 0;                // since the last ResetStats (counters())
 
     std::vector<void*> poolAllocs, sceneAllocs, filmAllocs, sampleAllocs, rowAllocs;
@@ -334,6 +339,7 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
         if (std::sscanf(tune, "%u,%u", &r, &p) == 2 && r >= 1 && r <= 64 && p >= 1 && p <= 64) {
             refillLanes = r;
             parkLanes = p;
+            tuneOverride = true;
         }
     }
     // pool arrays and queue records are addressed through 32-bit byte offsets (slot(),
@@ -822,7 +828,10 @@ int dcrt_tracer::BeginImage()
     fc.blocksX = (frame.resolution[0] + kBlockW - 1) / kBlockW;
     fc.bandCount = bandCount;
     fc.blocksPerImage = fc.blocksX * bandCount;
-    fc.refillLanes = refillLanes;
+#ifndef DCRT_REFILL_GLOBAL
+#define DCRT_REFILL_GLOBAL 28
+#endif
+    fc.refillLanes = tuneOverride || castAllCached ? refillLanes : DCRT_REFILL_GLOBAL;
     fc.parkLanes = parkLanes;
     hipLaunchKernelGGL(set_frame_kernel, dim3(1), dim3(1), 0, stream, dFrame, fc);
     const uint32_t total = fc.blocksPerImage;
