@@ -101,14 +101,11 @@ void SPunctualLight::SetEulerAnglesFromDirection(const Float3& direction)
         eulerAngles = dot >= 0.0f ? Float3(0.0f, 0.0f, 0.0f) : Float3(0.0f, 3.14159265358979f, 0.0f);
         return;
     }
-    axis = axis * (1.0f / axisLength);
+    // XMVectorDivide(axis, axisLength): a division per component (Scene.cpp:937)
+    axis = Float3(axis.x / axisLength, axis.y / axisLength, axis.z / axisLength);
     const float angle = (float)std::acos((double)dot);
-    // XMMatrixRotationAxis (Rodrigues)
-    const float c = std::cos(angle), s = std::sin(angle), t = 1.0f - c;
-    Float4x4 R = Float4x4::Identity();
-    R.m[0][0] = t * axis.x * axis.x + c;          R.m[0][1] = t * axis.x * axis.y + s * axis.z; R.m[0][2] = t * axis.x * axis.z - s * axis.y;
-    R.m[1][0] = t * axis.x * axis.y - s * axis.z; R.m[1][1] = t * axis.y * axis.y + c;          R.m[1][2] = t * axis.y * axis.z + s * axis.x;
-    R.m[2][0] = t * axis.x * axis.z + s * axis.y; R.m[2][1] = t * axis.y * axis.z - s * axis.x; R.m[2][2] = t * axis.z * axis.z + c;
+    // XMMatrixRotationAxis: XMVector3Normalize, then XMMatrixRotationNormal (XMScalarSinCos)
+    const Float4x4 R = RotationNormal(Normalize3(axis), angle);
     eulerAngles = MatrixRotationToRollPitchYaw(R);
 }
 

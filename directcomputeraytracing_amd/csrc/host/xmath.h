@@ -114,7 +114,17 @@ inline Float4x4 Transpose(const Float4x4& a)
 // rigid transforms the loaders produce).
 Float4x4 Inverse(const Float4x4& a, float* outDet = nullptr);
 
-// XMMatrixRotationRollPitchYawFromVector(pitch = x, yaw = y, roll = z).
+// XMScalarSinCos / XMVectorSinCos (one lane): DirectXMath's minimax sine and cosine.
+void ScalarSinCos(float* s, float* c, float value);
+void VectorSinCos(float* s, float* c, float value);
+// XMMatrixRotationNormal (XMMatrixRotationAxis after its XMVector3Normalize).
+Float4x4 RotationNormal(Float3 normalAxis, float angle);
+// XMVector3Normalize
+Float3 Normalize3(Float3 v);
+
+// XMMatrixRotationRollPitchYawFromVector(pitch = x, yaw = y, roll = z): sines and cosines
+// from XMVectorSinCos; the products of the three-factor entries are taken in the scalar
+// (_XM_NO_INTRINSICS_) order -- the SSE path's order is not pinned.
 Float4x4 RotationRollPitchYaw(float pitch, float yaw, float roll);
 
 // MathHelper::MatrixRotationToRollPitchYall (MathHelper.cpp:9-25)
