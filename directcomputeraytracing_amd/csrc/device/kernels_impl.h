@@ -598,14 +598,27 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
     // waves, so every wave samples the whole queue and per-wave costs even out
     // (contiguous ranges follow the image's cost structure and leave the slowest
     // waves alone at the end). `cursor` and `end` count in the wave's own sequence.
-    const uint32_t groups = (n + kInterleave - 1) / kInterleave;
+    // A sparse queue (an image's drain: a few thousand long rays) is cut into smaller groups
+    // -- the largest power of two <= n / (4 * waves), at least 1 -- so every wave gets some of
+    // it: with 64-item groups the rays sat 64 to a wave on a few dozen waves (a handful of
+    // CUs), and each of those waves took as long as its slowest lane plus every other lane's
+    // leaf work. (At least 4 groups per wave keep the per-wave item counts within 5/4 of
+    // each other.)
+#ifndef DCRT_ADAPTIVE_GROUPS
+#define DCRT_ADAPTIVE_GROUPS 1
+#endif
+    constexpr uint32_t kLgInterleave = 31u - __builtin_clz(kInterleave);
+    const uint32_t perWave4 = n / (4u * waves);
+    const uint32_t lg = !DCRT_ADAPTIVE_GROUPS || perWave4 >= kInterleave ? kLgInterleave : (perWave4 ? 31u - (uint32_t)__clz((int)perWave4) : 0u);
+    const uint32_t gmask = (1u << lg) - 1u;
+    const uint32_t groups = (n + gmask) >> lg;
     const uint32_t myGroups = groups > waveId ? (groups - waveId + waves - 1) / waves : 0u;
     uint32_t cursor = 0;
-    const uint32_t end = myGroups * kInterleave;
+    const uint32_t end = myGroups << lg;
     const uint32_t chunk = end;   // (diagnostics)
     // (24-bit multiply: a 32-bit a * b + c becomes v_mad_u64_u32 with an arbitrary VGPR as
     // the unused high addend, which made the refill wait for the window's pending load)
-    auto itemIndex = [&](uint32_t k) { return (waveId + __umul24(k / kInterleave, waves)) * kInterleave + k % kInterleave; };
+    auto itemIndex = [&](uint32_t k) { return ((waveId + __umul24(k >> lg, waves)) << lg) + (k & gmask); };
     // lookup(i) is arithmetic only (a ray's record position in its queue): a refill waits for
     // the ray loads alone (the earlier 4-B queue entries needed a prefetch window of lookups
     // one refill ahead, a bpermute and a register)

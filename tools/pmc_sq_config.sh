@@ -16,6 +16,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
            "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum" ${PMC_EXTRA:-}; do
   i=$((i+1))
+  grp=${grp//+/ }   # (PMC_EXTRA groups join their counters with +)
   timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -f csv -d "$OUT" -o pass$i -- \
       python3 "$ROOTDIR/bench.py" $ARGS > "$OUT/pass$i.log" 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"; [ $rc -eq 0 ] || exit $rc
