@@ -73,8 +73,10 @@ def parse():
                          "whose recorded workload is this run's)")
     ap.add_argument("--repeats", type=int, default=5,
                     help="timed repeats of the K steps; value is the median (SURVEY 8(d): median of 5 after warm-up)")
-    ap.add_argument("--spaceship-spp", type=int, default=4,
-                    help="configs[3] leg of the default Cornell run: spaceship 4K images (0 = skip)")
+    ap.add_argument("--spaceship-spp", type=int, default=16,
+                    help="configs[3] leg of the default Cornell run: spaceship 4K images (0 = skip); 16 = four "
+                         "batches per pipeline, the steady state of configs[3]'s 128 spp (4 is one batch: its "
+                         "ramp and drain alone)")
     return ap.parse_args()
 
 
@@ -451,7 +453,7 @@ def cast_roofline(tracer, R, filt, workload_key, traffic_json=None) -> dict:
     avg_ms = tm["ext_kernel_ms"] / launches
     bytes_per_launch = cast_bytes / launches
     alg = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = None, "no committed PMC profile of this workload"
+    traffic, traffic_src, valu = None, "no committed PMC profile of this workload", None
     cands = [Path(traffic_json)] if traffic_json else sorted((ROOT / "profiles").glob("r*_pmc_traffic*.json"), reverse=True)
     for tj in cands:
         try:
@@ -462,6 +464,14 @@ def cast_roofline(tracer, R, filt, workload_key, traffic_json=None) -> dict:
             traffic = d["ext_hbm_bytes_per_launch"]
             traffic_src = (f"{tj.relative_to(ROOT) if tj.is_relative_to(ROOT) else tj}: rocprofv3 PMC, "
                            f"FETCH_SIZE x2 + WRITE_SIZE per cast launch, same workload")
+            if d.get("ext_valu_issue_frac"):
+                # what the launch does bound: the VALU issue slots (a wave64 instruction takes 2
+                # cycles of its SIMD) used over the launch's active cycles, the tail included
+                valu = {"valu_issue_frac": round(d["ext_valu_issue_frac"], 4),
+                        "valu_insts_per_launch": d.get("ext_valu_insts_per_launch"),
+                        "implied_clock_ghz": None if d.get("ext_implied_clock_ghz") is None else round(d["ext_implied_clock_ghz"], 3),
+                        "basis": "SQ_INSTS_VALU x 2 cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) per cast launch, "
+                                 "same PMC profile"}
             break
     hbm = None if traffic is None else traffic / (avg_ms * 1e-3) / 1e9
     # what bounds the launch, from the evidence: a scene resident in the LDS scene cache
@@ -475,6 +485,7 @@ def cast_roofline(tracer, R, filt, workload_key, traffic_json=None) -> dict:
             "frac": None if hbm is None else round(hbm / HBM_PEAK_GBS, 4),
             "basis": "measured HBM: rocprofv3 PMC bytes per cast launch (traffic) / HIP-event launch time",
             "traffic": traffic, "traffic_source": traffic_src,
+            "compute": valu,
             "achieved_algorithmic": round(alg, 1), "frac_algorithmic": round(alg / HBM_PEAK_GBS, 4),
             "algorithmic_basis": "the reference's traversal counts (node visits, triangle tests, BLAS entries, "
                                  "from the instrumented kernel) x SURVEY 8(d)'s bytes per unit, wherever the bytes "

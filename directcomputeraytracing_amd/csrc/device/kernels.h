@@ -235,8 +235,8 @@ struct PathPool {
     // result's destination), beside its path slot in shadowQueue[s * recCap + e]
     // (ALLOW_ANYHIT_SHADER's opacity samples are per slot)
     float4* shRec;
-    uint32_t* pixel;     // per slot: sample index image * W*H + y * W + x
-    float2* pixelSample; // per slot
+    uint32_t* pixel;     // per slot: sample index image * W*H + y * W + x (the sub-pixel
+                         // position is recomputed from it: pixel_sample)
     uint32_t* flags;     // per slot: kFlagIdle (CONTROL's claims), else 0
     float* extOpacity;         // ALLOW_ANYHIT_SHADER: g_ExtensionRayOpacitySamples
     float* shadowOpacity;      //                      g_ShadowRayOpacitySamples
@@ -291,6 +291,22 @@ struct SampleOut {
 
 // Pixel of lane `lane` in claimed block `block` of the batch: image, then 8-row group,
 // then 8-column block. False for lanes outside the film or past the last rendered row.
+// A path's sub-pixel position (NEW_PATH's first two draws, WavefrontPathTracing.hlsl:213-214)
+// recomputed from its sample index p = image * W*H + y * W + x when WriteSample needs it:
+// the same rng_init and the same two draws, so the same bits as storing them per slot -- a
+// 4-B pixel read per ending path instead of a 12-B one (two partly read sectors). Valid
+// while the path's batch is live (fc's frame seed advances only once the batch completed).
+DEV float2 pixel_sample(const FrameConstants& fc, uint32_t p)
+{
+    const uint32_t W = fc.resolution[0], wh = W * fc.resolution[1];
+    const uint32_t image = p / wh, local = p - image * wh;
+    const uint32_t py = local / W, px = local - py * W;
+    Rng r = rng_init(px, py, fc.frameSeed + image);
+    const float psx = next1(r);
+    const float psy = next1(r);
+    return make_float2(psx, psy);
+}
+
 DEV bool block_pixel(const FrameConstants& fc, const Film& film, uint32_t block, uint32_t lane, uint32_t* px, uint32_t* py,
                      uint32_t* image)
 {

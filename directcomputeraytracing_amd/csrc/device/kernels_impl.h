@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
             li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
             const uint32_t p = slot(pool.pixel, path);
-            sample_at(film.samplePosition, p) = slot(pool.pixelSample, path);
+            sample_at(film.samplePosition, p) = pixel_sample(*fc, p);
             sample_at(film.sampleValue, p) = make_float4(li.x, li.y, li.z, 0.0f);
             // (debug RNG: MATERIAL stored it when it ended the path)
             // last, after stores that consumed the loads: another workgroup's scan may see the
@@ -268,8 +268,9 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             const float a0 = next1(rng), a1 = next1(rng), a2 = next1(rng);
             generate_ray(*fc, fsx, fsy, a0, a1, a2, &o, &d);
             if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) pool.extOpacity[tid] = next1(rng);   // :223-226
+            // (the sub-pixel position is recomputed from the pixel where WriteSample needs it:
+            // pixel_sample)
             pool.pixel[tid] = image * (film.width * film.height) + py * film.width + px;
-            pool.pixelSample[tid] = make_float2(psx, psy);
             pool.flags[tid] = 0u;   // busy
             newPath = true;
         }
@@ -328,7 +329,6 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     const bool active = i < count;
     bool terminate = false, hasShadow = false, ends = false;
     uint32_t path = 0, pix = 0;
-    float2 pixSample = make_float2(0.0f, 0.0f);
     float4 sample = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     float2* outPos = nullptr;
     float4* outVal = nullptr;
@@ -469,7 +469,6 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
             const SampleOut so = *sampleOut;
             if (ends || so.debugRng) pix = slot(pool.pixel, out);
             if (ends) {
-                pixSample = slot(pool.pixelSample, out);
                 sample = make_float4(L.x + 0.0f, L.y + 0.0f, L.z + 0.0f, 0.0f);
                 // the sample pointers are read here too, not after the appends: read there
                 // (behind the barriers and the atomic) they were one more round trip
@@ -514,7 +513,7 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         slot(pool.shadowQueue, sq) = path;
     }
     if (ends) {
-        sample_at(outPos, pix) = pixSample;
+        sample_at(outPos, pix) = pixel_sample(*fc, pix);
         sample_at(outVal, pix) = sample;
     }
     DCRT_MCLK(6);

@@ -353,7 +353,6 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     const size_t P = poolSize;
     CHECKED(DeviceAlloc(&pool.hit, 2 * P, &poolAllocs));   // 2 float4 per extension-queue item
     CHECKED(DeviceAlloc(&pool.pixel, P, &poolAllocs));
-    CHECKED(DeviceAlloc(&pool.pixelSample, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.flags, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.extOpacity, P, &poolAllocs));
     CHECKED(DeviceAlloc(&pool.shadowOpacity, P, &poolAllocs));

@@ -50,10 +50,28 @@ def main(src, dst_prefix):
             d["hbm_bytes_per_launch"] = d["hbm_read_bytes_per_launch"] + d["hbm_write_bytes_per_launch"]
         if "FETCH_SIZE_avg" in d and "TCC_EA0_RDREQ_sum_avg" in d and d["TCC_EA0_RDREQ_sum_avg"]:
             d["fetch_kib_per_rdreq"] = d["FETCH_SIZE_avg"] / d["TCC_EA0_RDREQ_sum_avg"]
+    # multi-counter passes (pmc_A+B+..._counter_collection.csv): per kernel and counter
+    for p in sorted(src.glob("pmc_*+*_counter_collection.csv")):
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            agg[(r["Kernel_Name"].split("(")[0].replace("void ", ""), r["Counter_Name"])].append(float(r["Counter_Value"]))
+        for (name, ctr), vals in agg.items():
+            out["kernels"].setdefault(name, {})[f"{ctr}_avg"] = sum(vals) / len(vals)
+    for name, d in out["kernels"].items():
+        # VALU issue: a wave64 VALU instruction issues over 2 cycles on its SIMD (MI355X guide);
+        # GRBM_GUI_ACTIVE of a dispatch sums the 8 XCDs' active cycles; 1024 SIMDs
+        if d.get("SQ_INSTS_VALU_avg") and d.get("GRBM_GUI_ACTIVE_avg"):
+            cyc = d["GRBM_GUI_ACTIVE_avg"] / 8.0
+            d["valu_issue_frac"] = d["SQ_INSTS_VALU_avg"] * 2.0 / (cyc * 1024.0)
+            if d.get("avg_us"):
+                d["implied_clock_ghz"] = cyc / (d["avg_us"] * 1e3)
     # the timed ray-cast launch: the merged cast_kernel, else (DCRT_SPLIT_CASTS=1) the EXT kernel
     ext = next((v for k, v in out["kernels"].items() if k.startswith("dcrt::dev::cast_kernel<false")), None) or \
         next((v for k, v in out["kernels"].items() if k.startswith("dcrt::dev::extension_kernel<false")), {})
     out["ext_hbm_bytes_per_launch"] = ext.get("hbm_bytes_per_launch")
+    out["ext_valu_issue_frac"] = ext.get("valu_issue_frac")
+    out["ext_valu_insts_per_launch"] = ext.get("SQ_INSTS_VALU_avg")
+    out["ext_implied_clock_ghz"] = ext.get("implied_clock_ghz")
     # the workload the PMC passes profiled (bench.py matches its own run against it)
     log = src / "pmc_FETCH_SIZE.log"
     line = next((l for l in (log.read_text().splitlines() if log.exists() else []) if l.startswith("{")), None)

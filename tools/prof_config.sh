@@ -18,7 +18,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT" -o trace -- 
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 [ -n "${NO_PMC:-}" ] && exit 0
 # FETCH_SIZE (3 TCC), WRITE_SIZE (2 TCC), TCC_EA0_RDREQ_sum, L2 hit / miss: separate passes
-for ctr in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum "TCC_HIT_sum TCC_MISS_sum" ${EXTRA_PMC:-}; do
+# (the SQ + GRBM pass: VALU issue per cast launch for the bench's compute statement)
+for ctr in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES GRBM_GUI_ACTIVE" ${EXTRA_PMC:-}; do
   tag=$(echo "$ctr" | tr ' ' '+')
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -f csv -d "$OUT" -o "pmc_$tag" -- \
       python3 "$ROOTDIR/bench.py" $ARGS > "$OUT/pmc_${tag}.log" 2>&1
