@@ -127,7 +127,8 @@ class FilmPartition(C.Structure):
 class TraversalStats(C.Structure):
     _fields_ = [("ext_node_visits", C.c_uint64), ("ext_triangle_tests", C.c_uint64), ("ext_blas_entries", C.c_uint64),
                 ("shadow_node_visits", C.c_uint64), ("shadow_triangle_tests", C.c_uint64),
-                ("shadow_blas_entries", C.c_uint64), ("ext_launches", C.c_uint64), ("ext_kernel_ms", C.c_double)]
+                ("shadow_blas_entries", C.c_uint64), ("ext_launches", C.c_uint64), ("ext_kernel_ms", C.c_double),
+                ("ext_max_node_visits", C.c_uint64), ("shadow_max_node_visits", C.c_uint64)]
 
 
 class TracerInfo(C.Structure):

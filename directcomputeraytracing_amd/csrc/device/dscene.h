@@ -277,6 +277,7 @@ struct TraversalStats {
     uint32_t nodes;   // iterationCounter (BVHAccel.inc.hlsl:121)
     uint32_t tris;    // triangle tests
     uint32_t blas;    // TLAS -> BLAS entries
+    uint32_t maxNodes;   // (merged cast, per ray kind) the longest ray's node visits
 #ifdef DCRT_PHASE_CLOCKS
     // diagnostic build: node visits served by the LDS scene cache; pushes onto a stack
     // already 4 / 8 / 12 entries deep

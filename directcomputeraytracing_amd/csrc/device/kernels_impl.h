@@ -728,6 +728,13 @@ __device__ __forceinline__ void flush_stats(const TraversalStats& st, unsigned l
     if ((threadIdx.x & 63u) == 0 && (a | b | c)) { atomicAdd(&dst[0], a); atomicAdd(&dst[1], b); atomicAdd(&dst[2], c); }
 }
 
+// the wave's largest value into *dst (the longest ray's node visits)
+__device__ __forceinline__ void flush_max(uint32_t v, unsigned long long* dst)
+{
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    if ((threadIdx.x & 63u) == 0 && v) atomicMax(dst, (unsigned long long)v);
+}
+
 // The extension cast's result at the ray's queue item: the hit and, for MATERIAL, the
 // ray's direction and instance (so MATERIAL reads nothing of the ray record)
 __device__ __forceinline__ void emit_hit(const PathPool& pool, uint32_t item, const TravState& s)
@@ -872,13 +879,19 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
             if (INSTR) {
                 TraversalStats& dst = s.anyHit ? stShadow : stExt;
                 dst.nodes += st.nodes; dst.tris += st.tris; dst.blas += st.blas;
+                dst.maxNodes = max(dst.maxNodes, st.nodes);
 #ifdef DCRT_PHASE_CLOCKS
                 dst.cached += st.cached; dst.deep4 += st.deep4; dst.deep8 += st.deep8; dst.deep12 += st.deep12;
 #endif
             }
         },
         st, DCRT_WAVE_TAG(g));
-    if (INSTR) { flush_stats(stExt, instr); flush_stats(stShadow, instr + 3); }
+    if (INSTR) {
+        flush_stats(stExt, instr);
+        flush_stats(stShadow, instr + 3);
+        flush_max(stExt.maxNodes, instr + 6);
+        flush_max(stShadow.maxNodes, instr + 7);
+    }
 #ifdef DCRT_PHASE_CLOCKS
     if (INSTR) {
         const unsigned long long c = wave_sum(stExt.cached + stShadow.cached), d4 = wave_sum(stExt.deep4 + stShadow.deep4),

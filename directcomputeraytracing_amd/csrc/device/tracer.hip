@@ -1358,6 +1358,7 @@ DCRT_API int dcrt_tracer_traversal_stats(dcrt_tracer* t, dcrt_traversal_stats* o
     out->shadow_node_visits = v[3]; out->shadow_triangle_tests = v[4]; out->shadow_blas_entries = v[5];
     out->ext_launches = launches;
     out->ext_kernel_ms = ms;
+    out->ext_max_node_visits = v[6]; out->shadow_max_node_visits = v[7];
     return DCRT_OK;
 }
 

@@ -264,6 +264,8 @@ typedef struct dcrt_traversal_stats {
     uint64_t shadow_node_visits, shadow_triangle_tests, shadow_blas_entries;
     uint64_t ext_launches;
     double ext_kernel_ms;         /* summed HIP-event time of the timed EXTENSION_RAY_CAST launches */
+    uint64_t ext_max_node_visits, shadow_max_node_visits;   /* the longest ray of each kind since
+                                     the last reset (merged cast kernel, instrumented)      */
 } dcrt_traversal_stats;
 
 /* What the tracer chose for the uploaded scene (diagnostics; bench.py reports it). */

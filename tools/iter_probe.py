@@ -23,6 +23,8 @@ def run(tr, images, instrument):
         tr.reset_image()
         it = 0
         while True:
+            if instrument:
+                tr.reset_stats()            # per-iteration maxima
             c0 = tr.counters()
             s0 = tr.traversal_stats() if instrument else None
             t0 = time.perf_counter()
@@ -36,7 +38,7 @@ def run(tr, images, instrument):
             if instrument:
                 s1 = tr.traversal_stats()
                 for k in s1:
-                    row[k] = s1[k] - s0[k]
+                    row[k] = s1[k] if "max" in k else s1[k] - s0[k]
             rows.append(row)
             it += 1
             if tr.is_image_complete() or it > 64:
