@@ -135,7 +135,29 @@ def cpu_baseline(scene, luts_arrays, seconds: float, label: str = "1920x1080 8-b
             break
     done_rows = band * images
     mrays = rays / elapsed / 1e6
-    return {"value": round(mrays, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    # BASELINE configs[0], reported in full: the Cornell OBJ at 128x128,
+    # 1 spp, maxBounce 2 -- the host scene load + BVH build (C++, this package) and the scalar
+    # megakernel on the same threads; median of 5 after one warm-up
+    from directcomputeraytracing_amd import Scene, scenes
+    builds, renders, c0_rays = [], [], 0
+    for rep in range(6):
+        t0 = time.perf_counter()
+        s0 = Scene((128, 128))
+        scenes.setup_cornell(s0, 128, 128, 2)
+        f0 = s0.flat()
+        t1 = time.perf_counter()
+        _, _, _, c = oracle.render(f0, luts, s0.frame_params(0), oracle.MEGAKERNEL, threads=threads)
+        t2 = time.perf_counter()
+        if rep:
+            builds.append(t1 - t0)
+            renders.append(t2 - t1)
+        c0_rays = c["extension_rays"] + c["shadow_rays"]
+    r0 = float(np.median(renders))
+    config0 = {"workload": "configs[0]: Cornell box OBJ 128x128, 1 spp, maxBounce 2, CPU BVH build + scalar megakernel",
+               "mrays_per_s": round(c0_rays / r0 / 1e6, 3), "ms_per_spp": round(r0 * 1e3, 3),
+               "scene_load_and_bvh_ms": round(float(np.median(builds)) * 1e3, 3), "rays": int(c0_rays),
+               "threads": threads}
+    return {"value": round(mrays, 3), "unit": "Mrays/s", "cores": threads, "kind": "port", "config0": config0,
             "nproc": host["nproc"], "cpu_model": host["model"], "affinity_cpus": host["affinity"],
             "cgroup_cpus": host["cgroup_cpus"],
             "sample": f"oracle megakernel (scalar C restatement of MegakernelPathTracing.hlsl), {W}x{done_rows} "

@@ -527,3 +527,16 @@ def test_bvh_structure_invariants():
     lf = np.flatnonzero(leaf)
     t = tri[right[lf]]
     assert np.all(t.min(1) >= bmin[lf] - 1e-5) and np.all(t.max(1) <= bmax[lf] + 1e-5)
+
+
+def test_bench_cpu_baseline_reports_config0(oracle_mod):
+    """bench.py's cpu_baseline leg: the bounded Cornell sample plus BASELINE configs[0] in full
+    (128x128, 1 spp, maxBounce 2, the host BVH build + the scalar megakernel), with the host
+    description SURVEY 8(d) asks for."""
+    import bench
+    s = cornell(64, 48, 2)
+    r = bench.cpu_baseline(s, dict(np.load(GOLDEN / "bxdf_luts.npz")), 0.05, "64x48 2-bounce Cornell")
+    assert r["value"] > 0 and r["kind"] == "port" and r["cores"] >= 1 and r["nproc"] >= 1
+    c0 = r["config0"]
+    assert c0["rays"] > 128 * 128 and c0["ms_per_spp"] > 0 and c0["mrays_per_s"] > 0
+    assert c0["threads"] == r["cores"]
