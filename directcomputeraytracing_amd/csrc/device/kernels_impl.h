@@ -510,7 +510,9 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         // where the shadow cast writes the result: the continuing path's next state, or its
         // finish record
         r[1] = make_float4(sD.x, sD.y, sD.z, asf(terminate ? (fPos | kDestFinish) : qNext));
-        slot(pool.shadowQueue, sq) = path;
+        // the path slot beside it: only ALLOW_ANYHIT_SHADER's cast reads it (the shadow ray's
+        // opacity sample is per slot)
+        if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) slot(pool.shadowQueue, sq) = path;
     }
     if (ends) {
         sample_at(outPos, pix) = pixel_sample(*fc, pix);
