@@ -104,6 +104,8 @@ def test_bench_default_line_fields(tmp_path):
     assert d["pipeline_roofline"]["bound"].startswith("algorithmic")
     cb = d["cpu_baseline"]
     assert cb["cores"] >= 1 and cb["nproc"] >= cb["cores"] and cb["cpu_model"]
+    assert cb["config0"]["rays"] > 128 * 128 and cb["config0"]["ms_per_spp"] > 0   # BASELINE configs[0] in full
+    assert "compute" in roof   # the VALU statement (null without a PMC profile of this workload)
     sp = d["spaceship"]
     assert sp["ms_per_spp"] > 0 and sp["roofline"]["per_shadow_ray"]["nodes"] > 0
     assert sp["roofline"]["bound"].startswith("memory latency") and not sp["roofline"]["scene_in_lds"]
