@@ -289,13 +289,12 @@ struct SampleOut {
     uint4* debugRng;
 };
 
-// Pixel of lane `lane` in claimed block `block` of the batch: image, then 8-row group,
-// then 8-column block. False for lanes outside the film or past the last rendered row.
 // A path's sub-pixel position (NEW_PATH's first two draws, WavefrontPathTracing.hlsl:213-214)
 // recomputed from its sample index p = image * W*H + y * W + x when WriteSample needs it:
 // the same rng_init and the same two draws, so the same bits as storing them per slot -- a
 // 4-B pixel read per ending path instead of a 12-B one (two partly read sectors). Valid
-// while the path's batch is live (fc's frame seed advances only once the batch completed).
+// while the path's batch is live (fc's frame seed advances only once the batch completed);
+// fc.resolution is the film's (EnsureFilm follows SetFrame).
 DEV float2 pixel_sample(const FrameConstants& fc, uint32_t p)
 {
     const uint32_t W = fc.resolution[0], wh = W * fc.resolution[1];
@@ -307,6 +306,8 @@ DEV float2 pixel_sample(const FrameConstants& fc, uint32_t p)
     return make_float2(psx, psy);
 }
 
+// Pixel of lane `lane` in claimed block `block` of the batch: image, then 8-row group,
+// then 8-column block. False for lanes outside the film or past the last rendered row.
 DEV bool block_pixel(const FrameConstants& fc, const Film& film, uint32_t block, uint32_t lane, uint32_t* px, uint32_t* py,
                      uint32_t* image)
 {
