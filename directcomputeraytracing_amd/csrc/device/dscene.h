@@ -82,13 +82,35 @@ struct DeviceScene {
     uint32_t cachedTris;          // triVerts of triangles [0, cachedTris) likewise, after the nodes
     uint32_t cachedInstances;     // 0, or instanceCount: every inverse transform + identity flag, after the triangles
     uint32_t singlePrimLeaves;    // 1: every BLAS leaf holds exactly one triangle (BVHAccel.cpp's builder always does)
+    uint32_t pairLayout;          // node order: 0 PackBVH's (flat scene), 1 child pairs (children())
 };
+
+// Node orders on the device. kLayoutFlat is PackBVH's depth-first order, as in the flat
+// scene: an interior node's left child is node + 1 and its `right` field the right child.
+// kLayoutPairs (tracer.hip PairLayout, taken for scenes beyond an XCD's L2: the pair
+// traversal's kernels) puts the two children side by side -- one 64-B line, fetched together
+// when trav_visit_pair expands a node -- with `right` holding the left child's index, and the
+// levels nearest the roots first (the prefix the LDS scene cache holds). kLayoutScene reads
+// the order from the scene (kernels that serve either). The order changes no result.
+enum : int { kLayoutFlat = 0, kLayoutPairs = 1, kLayoutScene = 2 };
+// An interior node's children as packed references (with the node's BLAS bit); `right` is
+// its record's `right` field (or the packed reference to it)
+template <int LAYOUT>
+DEV void node_children(const DeviceScene& sc, uint32_t node, uint32_t right, uint32_t* left, uint32_t* rightChild)
+{
+    const uint32_t r = right | (node & 0x80000000u);
+    const bool pairs = LAYOUT == kLayoutPairs || (LAYOUT == kLayoutScene && sc.pairLayout != 0u);
+    *left = pairs ? r : node + 1u;
+    *rightChild = pairs ? r + 1u : r;
+}
 
 // LDS scene cache of the traversal kernels: after the per-lane stacks ([stackSize + 2]
 // x blockDim words, see stack_at) the block holds a copy of the first cachedNodes BVH nodes and the
-// first cachedTris pre-gathered triangles (the whole BVH and mesh of a small scene, the
-// TLAS and the first BLAS nodes of a large one), so most node and triangle fetches are
-// ds_read_b128 instead of vector-memory gathers through the texture path.
+// first cachedTris pre-gathered triangles (the whole BVH and mesh of a small scene; the
+// levels nearest the TLAS and BLAS roots of a large one, which the device node order puts
+// first), so most node and triangle fetches are ds_read_b128 instead of vector-memory
+// gathers through the texture path.
+
 DEV float4* scene_cache(const DeviceScene& sc, uint32_t* stackMem, uint32_t shift)
 {
     return (float4*)(stackMem + ((sc.stackSize + 2u) << shift));
@@ -399,7 +421,7 @@ DEV bool trav_pop(TravState& s, uint32_t* lds, uint32_t stride)
 // the top, and selects pick the outcome; the lanes of a wave stay convergent.
 // ALL_CACHED: the whole BVH and every triangle sit in the LDS scene cache (small scenes),
 // so node and triangle fetches are plain ds_read_b128 (no FLAT select, no global path).
-template <bool INSTR, bool ALL_CACHED = false>
+template <bool INSTR, bool ALL_CACHED = false, int LAYOUT = kLayoutScene>
 DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
@@ -437,8 +459,8 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     // (v_bfe takes its offset from the low 5 bits of misc: the split axis for an interior
     // node; for a leaf, whose neg is unused, a bit of negMask above bit 3, i.e. 0)
     const bool neg = __builtin_amdgcn_ubfe(s.negMask, misc, 1u) != 0u;
-    const uint32_t next = s.node + 1u;
-    const uint32_t rightRef = right | (s.node & 0x80000000u);
+    uint32_t next, rightRef;
+    node_children<LAYOUT>(sc, s.node, right, &next, &rightRef);
     const uint32_t nearChild = neg ? rightRef : next;
     const uint32_t farChild = neg ? next : rightRef;
     stack_at(lds, s.sp + stride) = farChild;
@@ -486,17 +508,19 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
 // * a far child that hits at the parent is pushed and tested again when popped (visit).
 // The stack holds a subset of the reference's entries (a push needs both children to hit),
 // so the uploaded stack size bounds it too.
-template <bool ALL_CACHED = false>
+template <bool ALL_CACHED = false, int LAYOUT = kLayoutScene>
 DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift)
 {
     const uint32_t stride = stack_stride<ALL_CACHED>(shift);
     const uint32_t top = stack_at(lds, s.sp);
     const uint32_t blasBit = s.node & 0x80000000u;
-    const uint32_t nextRef = s.node + 1u;
     // record A: the node itself (visit) or its near child (expand); record B: the far child
     // (expand only)
-    const uint32_t aRef = s.expand ? (s.expNeg ? s.expRight : nextRef) : s.node;
-    const uint32_t bRef = s.expNeg ? nextRef : s.expRight;
+    // (expanding: s.node is the expanded node, s.expRight its `right` field with the BLAS bit)
+    uint32_t nextRef, rightRef;
+    node_children<LAYOUT>(sc, s.node, s.expRight, &nextRef, &rightRef);
+    const uint32_t aRef = s.expand ? (s.expNeg ? rightRef : nextRef) : s.node;
+    const uint32_t bRef = s.expNeg ? nextRef : rightRef;
     auto fetch = [&](uint32_t ref, float4& a, float4& b) __attribute__((always_inline)) {
         const uint32_t idx = ref & 0x7FFFFFFFu;
         if (ALL_CACHED || idx < sc.cachedNodes) {

@@ -582,8 +582,8 @@ __device__ uint32_t g_waveItems[2][16][8192];
 #endif
 
 
-template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, bool PAIR = false, typename Lookup,
-          typename Fetch, typename Emit>
+template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, bool PAIR = false,
+          int LAYOUT = kLayoutScene, typename Lookup, typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
                                                  uint32_t kParkLanes, uint32_t* lds, uint32_t shift, Lookup lookup, Fetch fetch,
                                                  Emit emit, TraversalStats& st, int waveTag = -1)
@@ -668,8 +668,8 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
 #pragma unroll
             for (int k = 0; k < kVisitsPerCheck; ++k) {
                 if (ls == kRun) {
-                    const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair(sc, s, lds, shift)
-                                                                   : trav_visit<INSTR, ALL_CACHED>(sc, s, lds, shift, st);
+                    const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair<false, LAYOUT>(sc, s, lds, shift)
+                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT>(sc, s, lds, shift, st);
                     if (fin) ls = kFin;
                     else if (s.parked) ls = kPark;
                 }
@@ -852,7 +852,9 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     const float4* shRec = sgpr_ptr((const float4*)pool.shRec);
     TraversalStats st = {};
     TraversalStats stExt = {}, stShadow = {};
-    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR>(
+    // (node order: the pair kernels run on pair-ordered scenes, the other non-counting ones on
+    // PackBVH-ordered ones -- tracer.hip takes both from castPair -- the counting ones on either)
+    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, PAIR ? kLayoutPairs : (!INSTR || ALL_CACHED ? kLayoutFlat : kLayoutScene)>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
             // either kind: its record's position in its queue (no load)

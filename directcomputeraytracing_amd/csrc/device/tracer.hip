@@ -171,6 +171,71 @@ bool RequiredTraversalStack(const dcrt_flat_scene& s, uint32_t* out)
     return walk(0, true, out);
 }
 
+// The device node order (dscene.h, DCRT_PAIR_LAYOUT): an interior node's two children
+// adjacent, its `right` field the first child's device index, a TLAS leaf's the BLAS root's.
+// The levels nearest the roots come first -- the TLAS root and every BLAS root, breadth-first
+// until at least `topNodes` nodes are placed: what the LDS scene cache (a prefix) and the L2
+// hold -- then every subtree below them depth-first by child pairs. Each root gets a padded
+// slot, so every pair starts at an even index (one 64-B aligned line). Traversal follows the
+// tree, not the indices: hits, node counts and stack depths are those of the flat order.
+// Call after RequiredTraversalStack (which checks every reference); false if a node would be
+// placed twice (a child shared between parents).
+bool PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bvh_node>* out)
+{
+    constexpr uint32_t kNone = UINT32_MAX;
+    const dcrt_bvh_node* nd = s.bvh_nodes;
+    std::vector<uint32_t> pos(s.bvh_node_count, kNone);   // flat index -> device index
+    std::vector<uint32_t> order;                          // device index -> flat index (kNone: padding)
+    order.reserve((size_t)s.bvh_node_count + 64);
+    auto isLeaf = [&](uint32_t i) { return nd[i].misc >= 4u; };
+    auto place = [&](uint32_t i) {
+        if (pos[i] != kNone) return false;
+        pos[i] = (uint32_t)order.size();
+        order.push_back(i);
+        return true;
+    };
+    // an interior node's children, left then right, at the next (even) device index
+    auto placeChildren = [&](uint32_t p) { return place(p + 1) && place(nd[p].right_child_or_prim_index); };
+    std::vector<uint32_t> level, next, stack;
+    auto addRoot = [&](uint32_t r) {
+        if (pos[r] != kNone) return;   // a BLAS shared by several instances
+        place(r);
+        order.push_back(kNone);
+        if (!isLeaf(r)) level.push_back(r);
+    };
+    addRoot(0);
+    for (uint32_t i = 0; i < std::min(s.tlas_node_count, s.bvh_node_count); ++i)
+        if ((nd[i].misc & 4u) && nd[i].misc >= 4u) addRoot(nd[i].right_child_or_prim_index);
+    while (!level.empty() && order.size() < topNodes) {
+        next.clear();
+        for (const uint32_t p : level) {
+            if (!placeChildren(p)) return false;
+            if (!isLeaf(p + 1)) next.push_back(p + 1);
+            if (!isLeaf(nd[p].right_child_or_prim_index)) next.push_back(nd[p].right_child_or_prim_index);
+        }
+        level.swap(next);
+    }
+    for (const uint32_t root : level) {
+        stack.assign(1, root);
+        while (!stack.empty()) {
+            const uint32_t p = stack.back();
+            stack.pop_back();
+            if (!placeChildren(p)) return false;
+            if (!isLeaf(nd[p].right_child_or_prim_index)) stack.push_back(nd[p].right_child_or_prim_index);
+            if (!isLeaf(p + 1)) stack.push_back(p + 1);   // the left subtree's pairs first
+        }
+    }
+    out->assign(order.size(), dcrt_bvh_node{});
+    for (size_t k = 0; k < order.size(); ++k) {
+        if (order[k] == kNone) continue;
+        dcrt_bvh_node v = nd[order[k]];
+        if (v.misc < 4u) v.right_child_or_prim_index = pos[order[k] + 1];
+        else if (v.misc & 4u) v.right_child_or_prim_index = pos[v.right_child_or_prim_index];
+        (*out)[k] = v;
+    }
+    return true;
+}
+
 }  // namespace
 
 struct dcrt_tracer {
@@ -502,7 +567,6 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
                      " is below the uploaded BVH's depth " + std::to_string(stackNeed));
         return DCRT_E_INVALID_ARG;
     }
-    CHECKED(upload(&nodes, s.bvh_nodes, s.bvh_node_count));
     uint32_t* mids = nullptr; uint32_t* lidx = nullptr; uint32_t* iflags = nullptr; uint32_t* ovr = nullptr;
     dcrt_material* mats = nullptr; dcrt_light* lights = nullptr;
     CHECKED(upload(&mids, s.material_ids, s.triangle_count));
@@ -557,7 +621,6 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     CHECKED(upload(&dSrgb, srgb, 256));
     float* dEnv = nullptr;
     if (s.env_cube_rgb && s.env_cube_size) CHECKED(upload(&dEnv, s.env_cube_rgb, (size_t)6 * s.env_cube_size * s.env_cube_size * 3));
-    d.nodes = (const float4*)nodes;
     d.triVerts = triVerts;
     d.triShade = triShade;
     d.vertices = vtx;
@@ -582,7 +645,6 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     d.lutBsdf = dLuts->bsdf;
     d.lutBsdfAvg = dLuts->bsdf_avg;
     d.instanceCount = s.instance_count;
-    d.nodeCount = s.bvh_node_count;
     d.triangleCount = s.triangle_count;
     d.stackSize = std::max<uint32_t>(s.bvh_traversal_stack_size, 1u);
     // BLAS leaves (no TLAS-leaf bit, a primitive count) all with one triangle
@@ -620,20 +682,40 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, extension_kernel<false, false>, (int)castBlock, castLds));
         const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
         const size_t budget = castLds < perBlock ? perBlock - castLds : 0;
-        d.cachedNodes = (uint32_t)std::min<size_t>(s.bvh_node_count, budget / 32);
+        uint32_t nodeCount = s.bvh_node_count;
+        d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
         d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
         if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {   // A/B experiments
             if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
         }
         // (the LDS-only variant assumes 256-thread workgroups: its stack stride is a constant)
         // (the cache-only variant keeps three permuted copies of every triangle: 144 B each)
-        castAllCached = castBlock == 256 && d.cachedNodes == s.bvh_node_count && d.cachedTris == s.triangle_count &&
+        castAllCached = castBlock == 256 && d.cachedNodes == nodeCount && d.cachedTris == s.triangle_count &&
                         (size_t)d.cachedNodes * 32 + (size_t)s.triangle_count * 144 + (size_t)s.instance_count * 64 <= budget;
         d.cachedInstances = castAllCached ? s.instance_count : 0u;
         // trav_visit_pair where the traversal's fetches miss L2: nodes + triangles beyond an
         // XCD's 4 MiB L2 (DCRT_PAIR_TRAVERSAL=0/1 forces it off / on, A/B and tests)
-        castPair = !castAllCached && (size_t)s.bvh_node_count * 32 + (size_t)s.triangle_count * 48 > ((size_t)4 << 20);
+        castPair = !castAllCached && (size_t)nodeCount * 32 + (size_t)s.triangle_count * 48 > ((size_t)4 << 20);
         if (const char* pv = std::getenv("DCRT_PAIR_TRAVERSAL")) castPair = !castAllCached && std::atoi(pv) != 0;
+        // the node order goes with it (dscene.h kLayoutPairs: the pair kernels assume it, the
+        // other non-counting cast kernels assume PackBVH's)
+        std::vector<dcrt_bvh_node> pairNodes;
+        if (castPair) {
+            uint32_t topNodes = 4096;
+            if (const char* e = std::getenv("DCRT_TOP_NODES")) topNodes = (uint32_t)std::atoi(e);   // A/B experiments
+            if (!PairLayout(s, topNodes, &pairNodes)) { SetLastError("malformed BVH: a node with two parents"); return DCRT_E_INVALID_ARG; }
+            nodeCount = (uint32_t)pairNodes.size();
+            d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
+            d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
+            if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {
+                if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
+            }
+        }
+        CHECKED(upload(&nodes, castPair ? pairNodes.data() : s.bvh_nodes, nodeCount));
+        HIPCHECK(hipStreamSynchronize(stream));   // (pairNodes ends with this block)
+        d.nodes = (const float4*)nodes;
+        d.nodeCount = nodeCount;
+        d.pairLayout = castPair ? 1u : 0u;
         castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * (castAllCached ? 144 : 48) + (size_t)d.cachedInstances * 64;
         scene = d;
     }

@@ -277,7 +277,8 @@ typedef struct dcrt_tracer_info {
     uint32_t cast_block;          /* cast-kernel workgroup size                          */
     uint32_t traversal_stack;     /* LDS stack rows per lane                             */
     uint32_t material_generic;    /* 1: the any-scene MATERIAL variant                   */
-    uint32_t pair_traversal;      /* 1: the cast kernel expands node pairs (scene beyond L2) */
+    uint32_t pair_traversal;      /* 1: the cast kernel expands node pairs (scene beyond L2), over the device
+                                     child-pair node order */
     uint32_t control_grid, material_grid;   /* CONTROL / MATERIAL workgroups per launch  */
 } dcrt_tracer_info;
 

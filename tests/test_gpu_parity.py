@@ -385,14 +385,26 @@ def test_partition_rejects_filter_wider_than_halo(native_lib, golden_luts):
         t.destroy()
 
 
-def test_traversal_counters_match_oracle(native_lib, golden_luts, oracle_mod):
-    """Instrumented casts count the same AABB/triangle/BLAS work as the oracle (bytes/ray basis)."""
-    from directcomputeraytracing_amd import WavefrontPathTracer
+@pytest.mark.parametrize("scene_name,order", [("cornell", "flat"), ("cornell", "pairs"), ("xml_mix", "pairs")])
+def test_traversal_counters_match_oracle(native_lib, golden_luts, oracle_mod, monkeypatch, scene_name, order):
+    """Instrumented casts count the same AABB/triangle/BLAS work as the oracle (bytes/ray basis),
+    on PackBVH's node order and on the device's child-pair order (the pair traversal's scenes:
+    forced here with the LDS cache off; the counting kernel reads the order from the scene)."""
+    from conftest import GOLDEN
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer
+    if order == "pairs":
+        monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+        monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1")
     t = WavefrontPathTracer(path_pool_size=1 << 16)
     try:
-        s = cornell(128, 96, 4)
+        if scene_name == "cornell":
+            s = cornell(128, 96, 4)
+        else:
+            s = Scene((64, 48))
+            s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
         t.set_luts(golden_luts)
         t.on_scene_loaded(s)
+        assert t.info()["pair_traversal"] == (1 if order == "pairs" else 0)
         t.set_instrumentation(True, True)
         t.reset_stats()
         t.render_images(2, 1)
