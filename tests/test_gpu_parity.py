@@ -514,6 +514,42 @@ def test_full_size_spaceship_mesh_bit_exact(gpu_tracer, golden_luts, oracle_mod,
     assert gpu_tracer.info()["pair_traversal"] == 1   # (beyond an XCD's L2: trav_visit_pair)
 
 
+@pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
+def test_pair_order_trace_rays_and_megakernel_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, scene_name):
+    """The kernels that read the node order from the scene (trace_rays' batch kernel, the
+    megakernel) on the child-pair order (tracer.hip PairLayout: forced here with the LDS cache
+    off), against the oracle on PackBVH's order."""
+    from conftest import GOLDEN
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer
+    monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+    monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1")
+    if scene_name == "cornell":
+        s = cornell(48, 40, 6)
+    else:
+        s = Scene((32, 32))
+        s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
+    t = WavefrontPathTracer(path_pool_size=1 << 14, debug_rng=True)
+    try:
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        assert t.info()["pair_traversal"] == 1
+        flat = oracle_mod.flat_with_own_bvh(s)
+        for features in (0x0D, 0x07):
+            rays = _rays(20000, 5 + features, scene_name == "cornell")
+            assert np.array_equal(t.trace_rays(rays, features).view(np.uint8), oracle_mod.trace_rays(flat, rays, features)[0].view(np.uint8))
+            assert np.array_equal(t.occluded(rays, features), oracle_mod.occluded(flat, rays, features)[0])
+        t.set_mode("megakernel")
+        t.clear_film()
+        t.render_images(4, 1)
+        pos, val = t.read_samples()
+        p_ref, v_ref, r_ref, _ = oracle_mod.render(flat, golden_luts, s.frame_params(4), oracle_mod.MEGAKERNEL, rng=True)
+        assert np.array_equal(t.read_rng(), r_ref)
+        assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
+        assert same_bits(val, v_ref).all()
+    finally:
+        t.destroy()
+
+
 def test_cpp_host_example_matches_python_host(native_lib, tmp_path):
     """examples/dcrt_render (C++ host over the C ABI, the reference's frame loop: Render /
     IsImageComplete / SampleConvolution per image) and its --batch mode (render_images)
