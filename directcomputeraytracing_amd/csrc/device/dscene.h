@@ -82,7 +82,7 @@ struct DeviceScene {
     uint32_t cachedTris;          // triVerts of triangles [0, cachedTris) likewise, after the nodes
     uint32_t cachedInstances;     // 0, or instanceCount: every inverse transform + identity flag, after the triangles
     uint32_t singlePrimLeaves;    // 1: every BLAS leaf holds exactly one triangle (BVHAccel.cpp's builder always does)
-    uint32_t pairLayout;          // node order: 0 PackBVH's (flat scene), 1 child pairs (children())
+    uint32_t pairLayout;          // node order: 0 PackBVH's (flat scene), 1 child pairs (kLayoutPairs)
 };
 
 // Node orders on the device. kLayoutFlat is PackBVH's depth-first order, as in the flat

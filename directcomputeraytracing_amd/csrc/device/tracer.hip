@@ -171,7 +171,7 @@ bool RequiredTraversalStack(const dcrt_flat_scene& s, uint32_t* out)
     return walk(0, true, out);
 }
 
-// The device node order (dscene.h, DCRT_PAIR_LAYOUT): an interior node's two children
+// The child-pair node order (dscene.h kLayoutPairs): an interior node's two children
 // adjacent, its `right` field the first child's device index, a TLAS leaf's the BLAS root's.
 // The levels nearest the roots come first -- the TLAS root and every BLAS root, breadth-first
 // until at least `topNodes` nodes are placed: what the LDS scene cache (a prefix) and the L2
