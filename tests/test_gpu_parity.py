@@ -550,6 +550,24 @@ def test_pair_order_trace_rays_and_megakernel_bit_exact(native_lib, golden_luts,
         t.destroy()
 
 
+@pytest.mark.parametrize("name", ["mask_xml", "spaceship"])
+def test_pair_order_wavefront_anyhit_and_instancing_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, name):
+    """The pair kernels on the child-pair order, forced on small scenes: the any-hit shader's
+    variant (mask_xml, ALLOW_ANYHIT_SHADER) and a BLAS shared by several instances (the
+    spaceship fixture: four ships, one hull BLAS)."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    from test_oracle import load_fixture_scene
+    monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+    monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1")
+    s = _anyhit_scenes()["mask_xml"] if name == "mask_xml" else load_fixture_scene("spaceship")
+    t = WavefrontPathTracer(path_pool_size=1 << 14, debug_rng=True)
+    try:
+        list(_render_and_compare(t, oracle_mod, golden_luts, s, [0, 2]))
+        assert t.info()["pair_traversal"] == 1
+    finally:
+        t.destroy()
+
+
 def test_cpp_host_example_matches_python_host(native_lib, tmp_path):
     """examples/dcrt_render (C++ host over the C ABI, the reference's frame loop: Render /
     IsImageComplete / SampleConvolution per image) and its --batch mode (render_images)
