@@ -16,7 +16,7 @@ constexpr uint32_t kFlagIdle = 0x80000000u;           // WavefrontPathTracing.hl
 constexpr uint32_t kFlagShadowRayHit = 0x40000000u;
 constexpr uint32_t kFlagTerminate = 0x20000000u;
 constexpr uint32_t kFlagDelta = 0x10000000u;           // the path's last BSDF lobe was a delta (SPathAccumulation.isDelta)
-constexpr uint32_t kFlagFirst = 0x08000000u;           // a new path's state record holds NEW_PATH's rng only (PathState)
+constexpr uint32_t kFlagFirst = 0x08000000u;           // a new path's state record holds NEW_PATH's rng only (PathStateA)
 constexpr uint32_t kBlockW = 8, kBlockH = 8;           // one wave64 = one 8x8 pixel block
 #ifndef DCRT_CONTROL_BLOCK
 #define DCRT_CONTROL_BLOCK 256
@@ -204,13 +204,17 @@ DEV T& sample_at(T* base, uint32_t i)
 // (CONTROL for a new path, MATERIAL for a continuing one) and read densely by the next
 // MATERIAL pass at the same position -- no slot-indexed state, so no access to a 128-B
 // line half of which belongs to an ended path, and no load that waits for the slot.
-// xoshiro state, (lsr.y, lsr.z, flags, path slot), throughput + bsdfPdf, Li + lsr.x. A new
-// path's record is its first 32 B only (CONTROL: rng and the misc word with kFlagFirst; one
-// whole 32-B sector): its T = 1, bsdfPdf = 0, Li = 0, lsr = 0 are NEW_PATH's constants,
-// which its first MATERIAL pass takes instead of the unwritten half.
-struct PathState {
+// xoshiro state, (lsr.y, lsr.z, flags, path slot), throughput + bsdfPdf, Li + lsr.x, as two
+// dense 32-B halves (two arrays, same positions). A new path writes half A only (CONTROL: rng
+// and the misc word with kFlagFirst): its T = 1, bsdfPdf = 0, Li = 0, lsr = 0 are NEW_PATH's
+// constants, which its first MATERIAL pass takes instead of half B. (As one 64-B record, a
+// new path's half-written record cost a 32-B write request each: 33 M of a 4K batch start's
+// 54 M, PMC.)
+struct PathStateA {
     uint4 rng;
     float4 lsrMisc;  // lsr.y, lsr.z, asfloat(flags: first, delta, bounce), asfloat(path slot)
+};
+struct PathStateB {
     float4 thr;      // T.xyz, bsdfPdf
     float4 liLsr;    // Li.xyz, lsr.x
 };
@@ -251,8 +255,10 @@ struct PathPool {
     // without an index load.
     float4* extRec;
     const float4* extPrevRec;
-    PathState* state;            // kShards x recCap, 64-bit offsets (state_at)
-    const PathState* statePrev;
+    PathStateA* stateA;          // kShards x recCap each (state_at: 32-bit offsets, as ext_rec)
+    PathStateB* stateB;
+    const PathStateA* stateAPrev;
+    const PathStateB* stateBPrev;
     uint32_t* shadowHit;         // the shadow cast's result for ext position q (1 = occluded)
     const uint32_t* shadowHitPrev;
     uint32_t* shadowQueue;
@@ -264,10 +270,10 @@ struct PathPool {
     uint32_t recCap;           // entries per extension-queue shard
     uint32_t finCap;           // entries per finish-queue shard
 };
-// State record of extension-queue position q: a 64-bit byte offset (one parity's records
-// pass 4 GiB at 2^26 slots)
-DEV PathState& state_at(PathState* base, uint32_t q) { return *(PathState*)((char*)base + (uint64_t)q * 64u); }
-DEV const PathState& state_at(const PathState* base, uint32_t q) { return *(const PathState*)((const char*)base + (uint64_t)q * 64u); }
+// State half of extension-queue position q (32 B: one parity's halves stay below 4 GiB like
+// the extension records, dcrt_tracer::Create)
+template <typename T>
+DEV T& state_at(T* base, uint32_t q) { static_assert(sizeof(T) == 32, "state halves are 32 B"); return *(T*)((char*)base + (uint64_t)(q * 32u)); }
 
 // Sample textures (m_SamplePositionTexture / m_SampleValueTexture) for every image of a
 // batch: image b's sample of pixel (x, y) sits at b * W*H + y * W + x.

@@ -287,7 +287,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
         // NEW_PATH's state (:227-237) beside the ray: the rng, isDelta = true, bounce 0, the
         // slot (32 B); Li = 0, light sampling result = 0, T = 1, bsdfPdf = 0 are implicit
         // (kFlagFirst: writing all 64 B cost the 4K batches' first passes 3 GB of writes)
-        PathState& st = state_at(pool.state, q);
+        PathStateA& st = state_at(pool.stateA, q);
         st.rng = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
         st.lsrMisc = make_float4(0.0f, 0.0f, asf(kFlagDelta | kFlagFirst), asf(tid));
     }
@@ -346,7 +346,8 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         // the path's state record at its extension-queue position q, the cast's hit record
         // (with the ray's direction) at item i, the result of the path's last shadow ray at q
         const uint32_t q = qpos(pool.recCap, qm, i);
-        const PathState& ps = state_at(pool.statePrev, q);
+        const PathStateA& ps = state_at(pool.stateAPrev, q);
+        const PathStateB& psB = state_at(pool.stateBPrev, q);
         const float4 h4 = pool.hit[2 * i], hd = pool.hit[2 * i + 1];
         const bool shadowHit = pool.shadowHitPrev[q] != 0u;
         HitRecord hit;
@@ -360,8 +361,8 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         // a new path's first pass: NEW_PATH's constants, not the record's unwritten half
         const bool first = (flags & kFlagFirst) != 0u;
         flags &= ~kFlagFirst;
-        float4 thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : ps.thr;
-        const float4 l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : ps.liLsr;
+        float4 thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : psB.thr;
+        const float4 l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : psB.liLsr;
         F3 li{l4.x, l4.y, l4.z};
         {
             // CONTROL's Li += light sampling result (:520-528), done here for live paths (a
@@ -492,10 +493,11 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         float4* r = ext_rec(pool.extRec, qNext);
         r[0] = make_float4(nO.x, nO.y, nO.z, 0.0f);
         r[1] = make_float4(nD.x, nD.y, nD.z, asf(path));
-        PathState& st = state_at(pool.state, qNext);
+        PathStateA& st = state_at(pool.stateA, qNext);
+        PathStateB& stB = state_at(pool.stateB, qNext);
         st.rng = sRng;
-        st.thr = make_float4(sT.x, sT.y, sT.z, sThr.w);
-        st.liLsr = make_float4(sL.x, sL.y, sL.z, sLsr.x);
+        stB.thr = make_float4(sT.x, sT.y, sT.z, sThr.w);
+        stB.liLsr = make_float4(sL.x, sL.y, sL.z, sLsr.x);
         st.lsrMisc = make_float4(sLsr.y, sLsr.z, asf(pathFlags), asf(path));
     }
     if (fin) {

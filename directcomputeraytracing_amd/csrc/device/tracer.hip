@@ -259,7 +259,8 @@ struct dcrt_tracer {
     std::vector<void*> poolAllocs, sceneAllocs, filmAllocs, sampleAllocs, rowAllocs;
     PathPool pool{};                   // (queue pointers set per launch: LaunchIteration)
     float4* extRecs = nullptr;         // 2 parities x kShards x recCap extension-ray records (2 float4)
-    PathState* stateRecs = nullptr;    // 2 parities x kShards x recCap path state records
+    PathStateA* stateRecsA = nullptr;  // 2 parities x kShards x recCap path state halves
+    PathStateB* stateRecsB = nullptr;
     uint32_t* shadowHits = nullptr;    // 2 parities x kShards x recCap shadow results
     FinishRec* finRecs = nullptr;      // 2 parities x kFinShards x pool.finCap
     uint32_t* finHits = nullptr;       // 2 parities x kFinShards x pool.finCap
@@ -460,7 +461,8 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     if ((uint64_t)pool.recCap * kShards * 32u > (1ull << 32)) { SetLastError("path pool too large for the extension-queue records"); return DCRT_E_LIMIT; }
     CHECKED(DeviceAlloc(&extRecs, (size_t)pool.recCap * kShards * 2 * 2, &poolAllocs));
     // the paths' state records and their shadow rays' results, at the same positions
-    CHECKED(DeviceAlloc(&stateRecs, (size_t)pool.recCap * kShards * 2, &poolAllocs));
+    CHECKED(DeviceAlloc(&stateRecsA, (size_t)pool.recCap * kShards * 2, &poolAllocs));
+    CHECKED(DeviceAlloc(&stateRecsB, (size_t)pool.recCap * kShards * 2, &poolAllocs));
     CHECKED(DeviceAlloc(&shadowHits, (size_t)pool.recCap * kShards * 2, &poolAllocs));
     // the shadow queue (filled and cast within one iteration): records + path slots
     CHECKED(DeviceAlloc(&pool.shRec, (size_t)pool.recCap * kShards * 2, &poolAllocs));
@@ -937,8 +939,10 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     PathPool pool = this->pool;
     pool.extRec = extRecs + (size_t)par * kShards * pool.recCap * 2;
     pool.extPrevRec = extRecs + (size_t)(par ^ 1u) * kShards * pool.recCap * 2;
-    pool.state = stateRecs + (size_t)par * kShards * pool.recCap;
-    pool.statePrev = stateRecs + (size_t)(par ^ 1u) * kShards * pool.recCap;
+    pool.stateA = stateRecsA + (size_t)par * kShards * pool.recCap;
+    pool.stateB = stateRecsB + (size_t)par * kShards * pool.recCap;
+    pool.stateAPrev = stateRecsA + (size_t)(par ^ 1u) * kShards * pool.recCap;
+    pool.stateBPrev = stateRecsB + (size_t)(par ^ 1u) * kShards * pool.recCap;
     pool.shadowHit = shadowHits + (size_t)par * kShards * pool.recCap;
     pool.shadowHitPrev = shadowHits + (size_t)(par ^ 1u) * kShards * pool.recCap;
     pool.finRec = finRecs + (size_t)par * kFinShards * pool.finCap;
