@@ -377,7 +377,8 @@ def main():
         tracer = make_tracer(args.pool, (world, rank, args.stripe) if world > 1 else None)
     roof = cast_roofline(tracer, R, filt, {"config": args.config, "resolution": [args.width, args.height], "images": R,
                                            "path_pool": args.pool, "world": world}, args.traffic_json)
-    st, cr = roof.pop("_stats"), roof.pop("_counters")
+    st, cr, tm = roof.pop("_stats"), roof.pop("_counters"), roof.pop("_timing")
+    pmc, pmc_src = roof.pop("_pmc")
     # whole-pipeline figure ("and for the whole pipeline"): the reference's
     # algorithmic bytes of every stage for the timed images (cast terms, CONTROL + MATERIAL
     # per path-iteration = per extension ray, NEW_PATH per new path, the film pass per pixel
@@ -414,13 +415,8 @@ def main():
                                   + (f", {K} concurrent pipelines per GPU" if K > 1 else ""),
                    "rays": int(rays)},
         "roofline": roof,
-        "pipeline_roofline": {"bound": "algorithmic (not an HBM measurement)", "achieved_algorithmic": round(pipe_achieved, 1),
-                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac_algorithmic": round(pipe_achieved / HBM_PEAK_GBS, 4),
-                              "bytes_per_spp": int(pipe_bytes_R / R),
-                              "basis": "per GPU: algorithmic bytes of cast + CONTROL (92 B) + MATERIAL (600 B) per "
-                                       "path-iteration + NEW_PATH (88 B) per new path + film pass per pixel-image "
-                                       "(SURVEY 8(d)) over the timed region's wall time; mostly LDS / cache served"},
+        "pipeline_roofline": pipeline_roofline(pmc, pmc_src, images / world / elapsed, pipe_achieved, pipe_bytes_R / R),
+        "material": material_roofline(tm, pmc, pmc_src),
         "cpu_baseline": None,
     }
     if per_rank is not None:
@@ -475,26 +471,19 @@ def cast_roofline(tracer, R, filt, workload_key, traffic_json=None) -> dict:
     avg_ms = tm["ext_kernel_ms"] / launches
     bytes_per_launch = cast_bytes / launches
     alg = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    pmc, pmc_src = find_pmc_profile(workload_key, traffic_json)
     traffic, traffic_src, valu = None, "no committed PMC profile of this workload", None
-    cands = [Path(traffic_json)] if traffic_json else sorted((ROOT / "profiles").glob("r*_pmc_traffic*.json"), reverse=True)
-    for tj in cands:
-        try:
-            d = json.loads(tj.read_text())
-        except Exception:
-            continue
-        if d.get("workload") == workload_key and d.get("ext_hbm_bytes_per_launch"):
-            traffic = d["ext_hbm_bytes_per_launch"]
-            traffic_src = (f"{tj.relative_to(ROOT) if tj.is_relative_to(ROOT) else tj}: rocprofv3 PMC, "
-                           f"FETCH_SIZE x2 + WRITE_SIZE per cast launch, same workload")
-            if d.get("ext_valu_issue_frac"):
-                # what the launch does bound: the VALU issue slots (a wave64 instruction takes 2
-                # cycles of its SIMD) used over the launch's active cycles, the tail included
-                valu = {"valu_issue_frac": round(d["ext_valu_issue_frac"], 4),
-                        "valu_insts_per_launch": d.get("ext_valu_insts_per_launch"),
-                        "implied_clock_ghz": None if d.get("ext_implied_clock_ghz") is None else round(d["ext_implied_clock_ghz"], 3),
-                        "basis": "SQ_INSTS_VALU x 2 cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) per cast launch, "
-                                 "same PMC profile"}
-            break
+    if pmc is not None and pmc.get("ext_hbm_bytes_per_launch"):
+        traffic = pmc["ext_hbm_bytes_per_launch"]
+        traffic_src = f"{pmc_src}: rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE per cast launch, same workload"
+        if pmc.get("ext_valu_issue_frac"):
+            # what the launch does bound: the VALU issue slots (a wave64 instruction takes 2
+            # cycles of its SIMD) used over the launch's active cycles, the tail included
+            valu = {"valu_issue_frac": round(pmc["ext_valu_issue_frac"], 4),
+                    "valu_insts_per_launch": pmc.get("ext_valu_insts_per_launch"),
+                    "implied_clock_ghz": None if pmc.get("ext_implied_clock_ghz") is None else round(pmc["ext_implied_clock_ghz"], 3),
+                    "basis": "SQ_INSTS_VALU x 2 cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) per cast launch, "
+                             "same PMC profile"}
     hbm = None if traffic is None else traffic / (avg_ms * 1e-3) / 1e9
     # what bounds the launch, from the evidence: a scene resident in the LDS scene cache
     # (Cornell) runs node / triangle fetches from LDS and is VALU-issue bound;
@@ -521,7 +510,71 @@ def cast_roofline(tracer, R, filt, workload_key, traffic_json=None) -> dict:
             "per_shadow_ray": {"nodes": st["shadow_node_visits"] / max(1, cr["shadow_rays"]),
                                "tris": st["shadow_triangle_tests"] / max(1, cr["shadow_rays"]),
                                "blas": st["shadow_blas_entries"] / max(1, cr["shadow_rays"])},
-            "_stats": st, "_counters": cr}
+            "_stats": st, "_counters": cr, "_timing": tm, "_pmc": (pmc, pmc_src)}
+
+
+def pipeline_roofline(pmc, pmc_src, images_per_s, alg_achieved, alg_bytes_per_image) -> dict:
+    """The whole pipeline on one GPU ("and for the whole pipeline"): the HBM bytes
+    per image that the committed PMC profile of this workload measured over every per-image
+    kernel (tools/pmc_traffic.py pipeline_hbm_bytes_per_image: cast, MATERIAL, CONTROL, film,
+    image sequencing), times the images this GPU renders per second in the timed region. The
+    reference's algorithmic bytes (largely served from LDS / L2 / MALL, so above the HBM peak
+    on cache-resident scenes) stay beside it as achieved_algorithmic."""
+    out = {"peak": HBM_PEAK_GBS, "unit": "GB/s", "achieved": None, "frac": None, "traffic": None}
+    if alg_achieved is not None:
+        out.update(achieved_algorithmic=round(alg_achieved, 1), frac_algorithmic=round(alg_achieved / HBM_PEAK_GBS, 4),
+                   bytes_per_spp_algorithmic=int(alg_bytes_per_image),
+                   algorithmic_basis="per GPU: algorithmic bytes of cast + CONTROL (92 B) + MATERIAL (600 B) per "
+                                     "path-iteration + NEW_PATH (88 B) per new path + film pass per pixel-image (SURVEY "
+                                     "8(d)) over the timed region's wall time; mostly LDS / cache served")
+    if pmc is None or not pmc.get("pipeline_hbm_bytes_per_image"):
+        out["bound"] = "unmeasured (no committed PMC profile of this workload)"
+        return out
+    t = pmc["pipeline_hbm_bytes_per_image"]
+    achieved = t * images_per_s / 1e9
+    out.update(bound="measured HBM", achieved=round(achieved, 1), frac=round(achieved / HBM_PEAK_GBS, 4), traffic=t,
+               traffic_by_kernel={k: int(v) for k, v in sorted(pmc.get("pipeline_hbm_bytes_per_image_by_kernel", {}).items())},
+               basis="rocprofv3 PMC HBM bytes per image summed over every per-image kernel (FETCH_SIZE x2 + WRITE_SIZE) "
+                     "x the images this GPU rendered per second of the timed region",
+               traffic_source=f"{pmc_src}: pipeline_hbm_bytes_per_image")
+    return out
+
+
+def find_pmc_profile(workload_key, traffic_json=None):
+    """The newest committed tools/pmc_traffic.py summary (profiles/r*_pmc_traffic*.json) whose
+    recorded workload is this run's: (dict, path) or (None, None)."""
+    cands = [Path(traffic_json)] if traffic_json else sorted((ROOT / "profiles").glob("r*_pmc_traffic*.json"), reverse=True)
+    for tj in cands:
+        try:
+            d = json.loads(tj.read_text())
+        except Exception:
+            continue
+        if d.get("workload") == workload_key and d.get("ext_hbm_bytes_per_launch"):
+            return d, str(tj.relative_to(ROOT) if tj.is_relative_to(ROOT) else tj)
+    return None, None
+
+
+def material_roofline(tm, pmc, pmc_src) -> dict:
+    """MATERIAL's own statement: the PMC-measured HBM bytes per launch of the same workload over
+    its average HIP-event launch time (the roofline leg's timed launches), plus VALU issue."""
+    launches = tm.get("material_launches", 0)
+    avg_ms = tm["material_kernel_ms"] / launches if launches else None
+    out = {"kernel": "material_kernel (MATERIAL)", "avg_launch_us": None if avg_ms is None else round(avg_ms * 1e3, 2),
+           "launches": int(launches), "peak": HBM_PEAK_GBS, "unit": "GB/s", "achieved": None, "frac": None,
+           "traffic": None, "compute": None}
+    if pmc is None or not pmc.get("material_hbm_bytes_per_launch") or avg_ms is None:
+        out["traffic_source"] = "no committed PMC profile of this workload"
+        return out
+    b = pmc["material_hbm_bytes_per_launch"]
+    achieved = b / (avg_ms * 1e-3) / 1e9
+    out.update(achieved=round(achieved, 1), frac=round(achieved / HBM_PEAK_GBS, 4), traffic=b,
+               read_bytes=pmc.get("material_read_bytes_per_launch"), write_bytes=pmc.get("material_write_bytes_per_launch"),
+               traffic_source=f"{pmc_src}: rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE per MATERIAL launch, same workload",
+               bound="memory latency (dependent hit -> triangle -> material fetches; DESIGN section 4)")
+    if pmc.get("material_valu_issue_frac"):
+        out["compute"] = {"valu_issue_frac": round(pmc["material_valu_issue_frac"], 4),
+                          "basis": "SQ_INSTS_VALU x 2 cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) per MATERIAL launch"}
+    return out
 
 
 def spaceship_leg(args, luts_arrays) -> dict:
@@ -572,10 +625,13 @@ def spaceship_leg(args, luts_arrays) -> dict:
                                            "path_pool": pool, "world": 1})
     finally:
         tr.destroy()
+    tm = roof.pop("_timing")
+    pmc, pmc_src = roof.pop("_pmc")
     roof.pop("_stats"), roof.pop("_counters")
     return {"workload": f"{desc}, {n} spp, 1 GPU, {K} concurrent pipelines", "ms_per_spp": round(el * 1e3 / n, 3),
             "repeat_ms_per_spp": [round(w * 1e3 / n, 3) for w in walls], "mrays_per_s": round(rays / el / 1e6, 2),
-            "path_pool": pool, "roofline": roof}
+            "path_pool": pool, "roofline": roof, "material": material_roofline(tm, pmc, pmc_src),
+            "pipeline_roofline": pipeline_roofline(pmc, pmc_src, n / el, None, None)}
 
 
 if __name__ == "__main__":

@@ -128,7 +128,9 @@ class TraversalStats(C.Structure):
     _fields_ = [("ext_node_visits", C.c_uint64), ("ext_triangle_tests", C.c_uint64), ("ext_blas_entries", C.c_uint64),
                 ("shadow_node_visits", C.c_uint64), ("shadow_triangle_tests", C.c_uint64),
                 ("shadow_blas_entries", C.c_uint64), ("ext_launches", C.c_uint64), ("ext_kernel_ms", C.c_double),
-                ("ext_max_node_visits", C.c_uint64), ("shadow_max_node_visits", C.c_uint64)]
+                ("ext_max_node_visits", C.c_uint64), ("shadow_max_node_visits", C.c_uint64),
+                ("material_launches", C.c_uint64), ("material_kernel_ms", C.c_double),
+                ("control_launches", C.c_uint64), ("control_kernel_ms", C.c_double)]
 
 
 class TracerInfo(C.Structure):
@@ -136,6 +138,25 @@ class TracerInfo(C.Structure):
                 ("cached_triangles", C.c_uint32), ("cast_block", C.c_uint32), ("traversal_stack", C.c_uint32),
                 ("material_generic", C.c_uint32), ("pair_traversal", C.c_uint32), ("control_grid", C.c_uint32),
                 ("material_grid", C.c_uint32)]
+
+
+class MaterialSetting(C.Structure):
+    _fields_ = [("albedo", C.c_float * 3), ("roughness", C.c_float), ("ior", C.c_float * 3), ("opacity", C.c_float),
+                ("k", C.c_float * 3), ("tiling", C.c_float * 2), ("material_type", C.c_uint32),
+                ("albedo_texture_index", C.c_int32), ("opacity_texture_index", C.c_int32),
+                ("internal_scattering_mode", C.c_uint32), ("multiscattering", C.c_uint32),
+                ("is_two_sided", C.c_uint32), ("has_roughness_texture", C.c_uint32)]
+
+
+class SceneSettings(C.Structure):
+    _fields_ = [("resolution", C.c_uint32 * 2), ("max_bounce_count", C.c_uint32), ("camera_type", C.c_uint32),
+                ("fov_x", C.c_float), ("focal_length", C.c_float), ("focal_distance", C.c_float),
+                ("relative_aperture", C.c_float), ("aperture_blade_count", C.c_uint32), ("aperture_rotation", C.c_float),
+                ("film_size", C.c_float * 2), ("camera_position", C.c_float * 3), ("camera_euler_angles", C.c_float * 3),
+                ("features", C.c_uint32), ("has_environment_light", C.c_uint32), ("environment_color", C.c_float * 3),
+                ("env_cube_rgb", C.POINTER(C.c_float)), ("env_cube_size", C.c_uint32),
+                ("mesh_light_count", C.c_uint32), ("punctual_light_count", C.c_uint32),
+                ("material_count", C.c_uint32), ("texture_count", C.c_uint32)]
 
 
 class ObjMesh(C.Structure):
@@ -174,6 +195,12 @@ SIGNATURES = [
     ("dcrt_scene_get_material_count", _I, [_P, C.POINTER(C.c_uint32)]),
     ("dcrt_scene_set_material", _I, [_P, _U, _I, _FP, C.c_float, _FP, _FP, _I, _I]),
     ("dcrt_scene_set_material_opacity", _I, [_P, _U, C.c_float, C.c_int32]),
+    ("dcrt_scene_get_material_setting", _I, [_P, _U, C.POINTER(MaterialSetting)]),
+    ("dcrt_scene_set_material_multiscattering", _I, [_P, _U, _I]),
+    ("dcrt_scene_get_settings", _I, [_P, C.POINTER(SceneSettings)]),
+    ("dcrt_scene_get_mesh_light", _I, [_P, _U, C.POINTER(C.c_uint32), _FP]),
+    ("dcrt_scene_get_punctual_light", _I, [_P, _U, _FP, _FP, _FP, C.POINTER(C.c_int)]),
+    ("dcrt_scene_get_instance_material_override", _I, [_P, _U, C.POINTER(C.c_uint32)]),
     ("dcrt_scene_set_features", _I, [_P, _U]),
     ("dcrt_scene_get_features", _I, [_P, C.POINTER(C.c_uint32)]),
     ("dcrt_scene_get_flat", _I, [_P, C.POINTER(FlatScene)]),

@@ -312,10 +312,37 @@ struct dcrt_tracer {
     hipEvent_t stopEvents[4] = {};
     bool instrCounters = false;
     bool extTiming = false;
+    // timed launches (ext_timing): start / stop event pairs and the kernel each pair timed
+    enum TimedKind : uint8_t { kTimedCast = 0, kTimedMaterial = 1, kTimedControl = 2, kTimedKinds = 3 };
     std::vector<hipEvent_t> events;
+    std::vector<uint8_t> eventKinds;   // per pair
     size_t eventsUsed = 0;
-    double extMs = 0.0;
-    uint64_t extLaunches = 0;
+    double kindMs[kTimedKinds] = {};
+    uint64_t kindLaunches[kTimedKinds] = {};
+    int TimedPair(TimedKind kind, hipEvent_t* e0, hipEvent_t* e1)
+    {
+        while (events.size() < eventsUsed + 2) {
+            hipEvent_t e;
+            HIPCHECK(hipEventCreate(&e));
+            events.push_back(e);
+        }
+        eventKinds.resize(events.size() / 2);
+        eventKinds[eventsUsed / 2] = kind;
+        *e0 = events[eventsUsed++];
+        *e1 = events[eventsUsed++];
+        return DCRT_OK;
+    }
+    int CollectTimes()   // fold the recorded pairs into kindMs / kindLaunches
+    {
+        for (size_t i = 0; i + 1 < eventsUsed; i += 2) {
+            float e = 0.0f;
+            HIPCHECK(hipEventElapsedTime(&e, events[i], events[i + 1]));
+            kindMs[eventKinds[i / 2]] += e;
+            ++kindLaunches[eventKinds[i / 2]];
+        }
+        eventsUsed = 0;
+        return DCRT_OK;
+    }
 
     ~dcrt_tracer();
     int Create(const dcrt_tracer_config& cfg);
@@ -951,23 +978,17 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     pool.finHitPrev = finHits + (size_t)(par ^ 1u) * kFinShards * pool.finCap;
     const bool opacity = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) != 0;
     const uint32_t castGrid = CastGrid(castBlock, opacity);
-    hipLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, pool, film, (const FrameConstants*)dFrame, cnt,
-                       (const Counters*)next, dGlobals, (uint32_t)(film.debugRng != nullptr));
-    auto material = materialCaps == kCapOpaqueDelta ? material_kernel<kCapOpaqueDelta> : material_kernel<kCapAll>;
-    hipLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
-                       (const Counters*)next, (const SampleOut*)dSampleOut);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (timed) {
-        while (events.size() < eventsUsed + 2) {
-            hipEvent_t e;
-            HIPCHECK(hipEventCreate(&e));
-            events.push_back(e);
-        }
-        e0 = events[eventsUsed++];
-        e1 = events[eventsUsed++];
-    }
     // Timed launches take their start/stop timestamps from the dispatch itself
     // (hipExtLaunchKernelGGL), so the duration is the kernel's, as rocprofv3 reports it.
+    hipEvent_t c0 = nullptr, c1 = nullptr, m0 = nullptr, m1 = nullptr, e0 = nullptr, e1 = nullptr;
+    if (timed) CHECKED(TimedPair(kTimedControl, &c0, &c1));
+    hipExtLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, c0, c1, 0, pool, film,
+                          (const FrameConstants*)dFrame, cnt, (const Counters*)next, dGlobals, (uint32_t)(film.debugRng != nullptr));
+    auto material = materialCaps == kCapOpaqueDelta ? material_kernel<kCapOpaqueDelta> : material_kernel<kCapAll>;
+    if (timed) CHECKED(TimedPair(kTimedMaterial, &m0, &m1));
+    hipExtLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), 0, stream, m0, m1, 0, pool, scene,
+                          (const FrameConstants*)dFrame, cnt, (const Counters*)next, (const SampleOut*)dSampleOut);
+    if (timed) CHECKED(TimedPair(kTimedCast, &e0, &e1));
     // kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER
     if (mergedCasts) {
         auto cast = CastKernel(instrCounters, opacity, castAllCached, castPair);
@@ -1125,15 +1146,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
             frame.frame_seed = firstSeed + img;
             CHECKED(BeginImage());
             hipEvent_t e0 = nullptr, e1 = nullptr;
-            if (extTiming) {
-                while (events.size() < eventsUsed + 2) {
-                    hipEvent_t e;
-                    HIPCHECK(hipEventCreate(&e));
-                    events.push_back(e);
-                }
-                e0 = events[eventsUsed++];
-                e1 = events[eventsUsed++];
-            }
+            if (extTiming) CHECKED(TimedPair(kTimedCast, &e0, &e1));
             auto mk = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) ? megakernel<true> : megakernel<false>;
             hipExtLaunchKernelGGL(mk, dim3(megaResident), dim3(castBlock), castLds, stream, e0, e1, 0, scene,
                                   (const FrameConstants*)dFrame, film, dGlobals, (uint32_t)(film.debugRng != nullptr));
@@ -1429,22 +1442,16 @@ DCRT_API int dcrt_tracer_traversal_stats(dcrt_tracer* t, dcrt_traversal_stats* o
     unsigned long long v[8];
     HIPCHECK(hipMemcpyAsync(v, t->dInstr, sizeof(v), hipMemcpyDeviceToHost, t->stream));
     HIPCHECK(hipStreamSynchronize(t->stream));
-    double ms = t->extMs;
-    uint64_t launches = t->extLaunches;
-    for (size_t i = 0; i + 1 < t->eventsUsed; i += 2) {
-        float e = 0.0f;
-        HIPCHECK(hipEventElapsedTime(&e, t->events[i], t->events[i + 1]));
-        ms += e;
-        ++launches;
-    }
-    t->extMs = ms;
-    t->extLaunches = launches;
-    t->eventsUsed = 0;
+    CHECKED(t->CollectTimes());
     out->ext_node_visits = v[0]; out->ext_triangle_tests = v[1]; out->ext_blas_entries = v[2];
     out->shadow_node_visits = v[3]; out->shadow_triangle_tests = v[4]; out->shadow_blas_entries = v[5];
-    out->ext_launches = launches;
-    out->ext_kernel_ms = ms;
+    out->ext_launches = t->kindLaunches[dcrt_tracer::kTimedCast];
+    out->ext_kernel_ms = t->kindMs[dcrt_tracer::kTimedCast];
     out->ext_max_node_visits = v[6]; out->shadow_max_node_visits = v[7];
+    out->material_launches = t->kindLaunches[dcrt_tracer::kTimedMaterial];
+    out->material_kernel_ms = t->kindMs[dcrt_tracer::kTimedMaterial];
+    out->control_launches = t->kindLaunches[dcrt_tracer::kTimedControl];
+    out->control_kernel_ms = t->kindMs[dcrt_tracer::kTimedControl];
     return DCRT_OK;
 }
 
@@ -1461,8 +1468,10 @@ DCRT_API int dcrt_tracer_reset_stats(dcrt_tracer* t)
     HIPCHECK(hipMemcpyAsync(t->dGlobals, &g, sizeof(Globals), hipMemcpyHostToDevice, t->stream));
     HIPCHECK(hipStreamSynchronize(t->stream));
     t->eventsUsed = 0;
-    t->extMs = 0.0;
-    t->extLaunches = 0;
+    for (int k = 0; k < dcrt_tracer::kTimedKinds; ++k) {
+        t->kindMs[k] = 0.0;
+        t->kindLaunches[k] = 0;
+    }
     return DCRT_OK;
 }
 

@@ -17,7 +17,10 @@ void SetLastError(const std::string& s) { g_lastError = s; }
 
 struct dcrt_scene {
     dcrt::CScene scene;
-    std::vector<uint32_t> loadedIndices, loadedMaterialIds;   // dcrt_scene_get_loaded_mesh's buffers
+    // dcrt_scene_get_loaded_mesh's buffers, one pair per mesh, kept until the scene is
+    // reset or loads more content (the pointers handed out stay valid until then)
+    std::vector<std::vector<uint32_t>> loadedIndices, loadedMaterialIds;
+    void DropLoadedBuffers() { loadedIndices.clear(); loadedMaterialIds.clear(); }
 };
 
 using dcrt::SetLastError;
@@ -56,6 +59,7 @@ DCRT_API void dcrt_scene_destroy(dcrt_scene* s) { delete s; }
 DCRT_API int dcrt_scene_reset(dcrt_scene* s, uint32_t w, uint32_t h)
 {
     if (!s || !w || !h) return DCRT_E_INVALID_ARG;
+    s->DropLoadedBuffers();
     s->scene.Reset(w, h);
     return DCRT_OK;
 }
@@ -65,6 +69,7 @@ DCRT_API int dcrt_scene_load_from_file(dcrt_scene* s, const char* path)
     if (!s || !path) return DCRT_E_INVALID_ARG;
     DCRT_GUARD_BEGIN
     SetLastError("");
+    s->DropLoadedBuffers();
     if (!s->scene.LoadFromFile(path)) {
         const std::string detail = dcrt_last_error();
         SetLastError(std::string("failed to load scene ") + path + (detail.empty() ? "" : ": " + detail));
@@ -197,6 +202,40 @@ DCRT_API int dcrt_scene_set_material(dcrt_scene* s, uint32_t index, int type, co
     return DCRT_OK;
 }
 
+DCRT_API int dcrt_scene_get_material_setting(const dcrt_scene* s, uint32_t index, dcrt_material_setting* out)
+{
+    if (!s || !out || index >= s->scene.materials.size()) return DCRT_E_INVALID_ARG;
+    const dcrt::SMaterial& m = s->scene.materials[index];
+    *out = dcrt_material_setting{};
+    out->albedo[0] = m.albedo.x; out->albedo[1] = m.albedo.y; out->albedo[2] = m.albedo.z;
+    out->roughness = m.roughness;
+    out->ior[0] = m.ior.x; out->ior[1] = m.ior.y; out->ior[2] = m.ior.z;
+    out->opacity = m.opacity;
+    out->k[0] = m.k.x; out->k[1] = m.k.y; out->k[2] = m.k.z;
+    out->tiling[0] = m.tiling.x; out->tiling[1] = m.tiling.y;
+    out->material_type = (uint32_t)m.type;
+    out->albedo_texture_index = m.albedoTextureIndex;
+    out->opacity_texture_index = m.opacityTextureIndex;
+    out->internal_scattering_mode = m.internalScatteringMode;
+    out->multiscattering = m.multiscattering;
+    out->is_two_sided = m.isTwoSided;
+    out->has_roughness_texture = m.hasRoughnessTexture;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_set_material_multiscattering(dcrt_scene* s, uint32_t index, int enable)
+{
+    if (!s || index >= s->scene.materials.size()) return DCRT_E_INVALID_ARG;
+    dcrt::SMaterial& m = s->scene.materials[index];
+    if (m.type == dcrt::EMaterialType::Diffuse || m.type == dcrt::EMaterialType::ThinDielectric) {
+        SetLastError("multiscattering applies to plastic, conductor and dielectric materials (ImGui.cpp:620)");
+        return DCRT_E_INVALID_ARG;
+    }
+    m.multiscattering = enable != 0;
+    RefreshMaterials(s);
+    return DCRT_OK;
+}
+
 DCRT_API int dcrt_scene_set_material_opacity(dcrt_scene* s, uint32_t index, float opacity, int32_t opacity_texture_index)
 {
     if (!s || index >= s->scene.materials.size()) return DCRT_E_INVALID_ARG;
@@ -283,17 +322,25 @@ DCRT_API int dcrt_scene_get_loaded_mesh(dcrt_scene* s, uint32_t index, dcrt_obj_
     const dcrt::Mesh& m = s->scene.meshes[index];
     const uint32_t n = m.GetTriangleCount();
     if (m.bvhTriangleOrder.size() != n) { SetLastError("mesh has no BVH yet"); return DCRT_E_NO_SCENE; }
-    s->loadedIndices.assign((size_t)n * 3, 0);
-    s->loadedMaterialIds.assign(n, 0);
-    for (uint32_t t = 0; t < n; ++t) {   // BVH position t holds load-order triangle order[t]
-        const uint32_t src = m.bvhTriangleOrder[t];
-        for (int k = 0; k < 3; ++k) s->loadedIndices[(size_t)src * 3 + k] = m.indices[(size_t)t * 3 + k];
-        s->loadedMaterialIds[src] = m.materialIds[t];
+    if (s->loadedIndices.size() != s->scene.meshes.size()) {
+        s->loadedIndices.assign(s->scene.meshes.size(), {});
+        s->loadedMaterialIds.assign(s->scene.meshes.size(), {});
+    }
+    std::vector<uint32_t>& idx = s->loadedIndices[index];
+    std::vector<uint32_t>& ids = s->loadedMaterialIds[index];
+    if (idx.size() != (size_t)n * 3 || ids.size() != n) {
+        idx.assign((size_t)n * 3, 0);
+        ids.assign(n, 0);
+        for (uint32_t t = 0; t < n; ++t) {   // BVH position t holds load-order triangle order[t]
+            const uint32_t src = m.bvhTriangleOrder[t];
+            for (int k = 0; k < 3; ++k) idx[(size_t)src * 3 + k] = m.indices[(size_t)t * 3 + k];
+            ids[src] = m.materialIds[t];
+        }
     }
     out->vertices = m.vertices.data();
     out->vertex_count = (uint32_t)m.vertices.size();
-    out->indices = s->loadedIndices.data();
-    out->material_ids = s->loadedMaterialIds.data();
+    out->indices = idx.data();
+    out->material_ids = ids.data();
     out->triangle_count = n;
     return DCRT_OK;
     DCRT_GUARD_END
@@ -306,6 +353,68 @@ DCRT_API int dcrt_scene_get_instance(const dcrt_scene* s, uint32_t index, uint32
     const dcrt::Float4x3& t = s->scene.instanceTransforms[index];
     for (int r = 0; r < 4; ++r)
         for (int c = 0; c < 3; ++c) transform[r * 3 + c] = t.m[r][c];
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_settings(const dcrt_scene* s, dcrt_scene_settings* out)
+{
+    if (!s || !out) return DCRT_E_INVALID_ARG;
+    const dcrt::CScene& sc = s->scene;
+    *out = dcrt_scene_settings{};
+    out->resolution[0] = sc.resolutionWidth;
+    out->resolution[1] = sc.resolutionHeight;
+    out->max_bounce_count = sc.maxBounceCount;
+    out->camera_type = (uint32_t)sc.cameraType;
+    out->fov_x = sc.fovX;
+    out->focal_length = sc.focalLength;
+    out->focal_distance = sc.focalDistance;
+    out->relative_aperture = sc.relativeAperture;
+    out->aperture_blade_count = sc.apertureBladeCount;
+    out->aperture_rotation = sc.apertureRotation;
+    out->film_size[0] = sc.filmSize.x;
+    out->film_size[1] = sc.filmSize.y;
+    const dcrt::Float3 p = sc.camera.position, e = sc.camera.eulerAngles;
+    out->camera_position[0] = p.x; out->camera_position[1] = p.y; out->camera_position[2] = p.z;
+    out->camera_euler_angles[0] = e.x; out->camera_euler_angles[1] = e.y; out->camera_euler_angles[2] = e.z;
+    out->features = sc.features;
+    out->has_environment_light = sc.hasEnvironmentLight;
+    const dcrt::Float3 c = sc.environmentLight.color;
+    out->environment_color[0] = c.x; out->environment_color[1] = c.y; out->environment_color[2] = c.z;
+    out->env_cube_rgb = sc.environmentLight.cubeSize ? sc.environmentLight.cubeRGB.data() : nullptr;
+    out->env_cube_size = sc.environmentLight.cubeSize;
+    out->mesh_light_count = (uint32_t)sc.meshLights.size();
+    out->punctual_light_count = (uint32_t)sc.punctualLights.size();
+    out->material_count = (uint32_t)sc.materials.size();
+    out->texture_count = (uint32_t)sc.textures.size();
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_mesh_light(const dcrt_scene* s, uint32_t index, uint32_t* instance, float color[3])
+{
+    if (!s || !instance || !color || index >= s->scene.meshLights.size()) return DCRT_E_INVALID_ARG;
+    const dcrt::SMeshLight& l = s->scene.meshLights[index];
+    *instance = l.instanceIndex;
+    color[0] = l.color.x; color[1] = l.color.y; color[2] = l.color.z;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_punctual_light(const dcrt_scene* s, uint32_t index, float position[3], float euler[3],
+                                           float color[3], int* is_directional)
+{
+    if (!s || !position || !euler || !color || !is_directional || index >= s->scene.punctualLights.size())
+        return DCRT_E_INVALID_ARG;
+    const dcrt::SPunctualLight& l = s->scene.punctualLights[index];
+    position[0] = l.position.x; position[1] = l.position.y; position[2] = l.position.z;
+    euler[0] = l.eulerAngles.x; euler[1] = l.eulerAngles.y; euler[2] = l.eulerAngles.z;
+    color[0] = l.color.x; color[1] = l.color.y; color[2] = l.color.z;
+    *is_directional = l.isDirectional;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_scene_get_instance_material_override(const dcrt_scene* s, uint32_t index, uint32_t* out)
+{
+    if (!s || !out || index >= s->scene.meshInstances.size()) return DCRT_E_INVALID_ARG;
+    *out = s->scene.meshInstances[index].materialIdOverride;
     return DCRT_OK;
 }
 

@@ -94,6 +94,61 @@ class Scene:
                                                 f3(k) if k is not None else None,
                                                 int(multiscattering), int(two_sided)), "SetMaterial")
 
+    def material_setting(self, index) -> _abi.MaterialSetting:   # SMaterial, Material.h:14-30
+        m = _abi.MaterialSetting()
+        check(self._lib.dcrt_scene_get_material_setting(self._h, int(index), C.byref(m)), "GetMaterialSetting")
+        return m
+
+    def set_multiscattering(self, index, enable: bool = True) -> None:   # ImGui.cpp:620-626
+        check(self._lib.dcrt_scene_set_material_multiscattering(self._h, int(index), int(bool(enable))),
+              "SetMultiscattering")
+
+    def enable_multiscattering(self) -> list:
+        """Tick the UI's "Multiscattering" box (ImGui.cpp:620-626) on every material that has
+        it -- plastic, conductor, dielectric; both loaders leave it off
+        (SceneXMLLoading.cpp:869). Returns the material indices changed."""
+        changed = []
+        for i in range(self.material_count):
+            if self.material_setting(i).material_type in (_abi.MATERIAL_PLASTIC, _abi.MATERIAL_CONDUCTOR,
+                                                          _abi.MATERIAL_DIELECTRIC):
+                self.set_multiscattering(i, True)
+                changed.append(i)
+        return changed
+
+    def settings(self) -> _abi.SceneSettings:
+        s = _abi.SceneSettings()
+        check(self._lib.dcrt_scene_get_settings(self._h, C.byref(s)), "GetSettings")
+        return s
+
+    def mesh_lights(self):
+        """[(instance index in load order, (r, g, b))] -- SMeshLight, Scene.h:42-46."""
+        out = []
+        for i in range(self.settings().mesh_light_count):
+            inst, col = C.c_uint32(), (C.c_float * 3)()
+            check(self._lib.dcrt_scene_get_mesh_light(self._h, i, C.byref(inst), col))
+            out.append((inst.value, tuple(col)))
+        return out
+
+    def punctual_lights(self):
+        """[(position, euler angles, color, is_directional)] -- SPunctualLight, Scene.h:27-40."""
+        out = []
+        for i in range(self.settings().punctual_light_count):
+            p, e, c, d = (C.c_float * 3)(), (C.c_float * 3)(), (C.c_float * 3)(), C.c_int()
+            check(self._lib.dcrt_scene_get_punctual_light(self._h, i, p, e, c, C.byref(d)))
+            out.append((tuple(p), tuple(e), tuple(c), bool(d.value)))
+        return out
+
+    def instance_material_overrides(self):
+        """SMeshInstance::m_MaterialIdOverride per instance, load order."""
+        _, ni = C.c_uint32(), C.c_uint32()
+        check(self._lib.dcrt_scene_get_content_counts(self._h, C.byref(_), C.byref(ni)))
+        out = []
+        for j in range(ni.value):
+            o = C.c_uint32()
+            check(self._lib.dcrt_scene_get_instance_material_override(self._h, j, C.byref(o)))
+            out.append(o.value)
+        return out
+
     def set_material_opacity(self, index, opacity=1.0, opacity_texture_index=-1) -> None:   # ImGui.cpp:630-650
         check(self._lib.dcrt_scene_set_material_opacity(self._h, int(index), float(opacity), int(opacity_texture_index)),
               "SetMaterialOpacity")

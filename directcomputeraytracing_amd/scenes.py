@@ -419,9 +419,15 @@ def write_anyhit(directory: Path | str, width: int = 64, height: int = 48) -> Pa
 CONFIGS = ("cornell", "coffee", "spaceship", "lamp")
 
 
-def setup_config(scene, name: str, scene_dir: Path | str, small: bool = False) -> str:
+def setup_config(scene, name: str, scene_dir: Path | str, small: bool = False, multiscattering: bool = True) -> str:
     """BASELINE.json configs[1..4] as procedural scenes (written into `scene_dir`), loaded
-    into `scene` at their resolutions; returns a workload description."""
+    into `scene` at their resolutions; returns a workload description.
+
+    configs[2] names "Cook-Torrance/Kulla-Conty": both reference loaders force
+    SMaterial::m_Multiscattering off (SceneXMLLoading.cpp:869) and only the UI's checkbox
+    turns it on (ImGui.cpp:620-626), so the coffee scene ticks it programmatically on every
+    plastic / conductor / dielectric material (``multiscattering=False`` keeps the loader's
+    state, for the A/B)."""
     d = Path(scene_dir)
     if name == "cornell":
         setup_cornell(scene, 1920, 1080, 8)
@@ -429,7 +435,9 @@ def setup_config(scene, name: str, scene_dir: Path | str, small: bool = False) -
     if name == "coffee":
         scene.load_from_file(write_coffee(d, 1920, 1080, segments=48 if small else 96))
         scene.set_environment_light((1.0, 1.0, 1.0), env_cube(64))
-        return "coffee-like Mitsuba XML 1920x1080, env cube + constant, max_depth 8 (configs[2])"
+        ms = scene.enable_multiscattering() if multiscattering else []
+        return ("coffee-like Mitsuba XML 1920x1080, env cube + constant, max_depth 8, Kulla-Conty multiscattering "
+                + (f"on ({len(ms)} materials)" if ms else "off") + " (configs[2])")
     if name == "spaceship":
         nu, nv = (64, 32) if small else (512, 256)
         scene.load_from_file(write_spaceship(d, 3840, 2160, nu=nu, nv=nv, ships=8))

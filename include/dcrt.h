@@ -266,6 +266,10 @@ typedef struct dcrt_traversal_stats {
     double ext_kernel_ms;         /* summed HIP-event time of the timed EXTENSION_RAY_CAST launches */
     uint64_t ext_max_node_visits, shadow_max_node_visits;   /* the longest ray of each kind since
                                      the last reset (merged cast kernel, instrumented)      */
+    uint64_t material_launches;   /* timed MATERIAL launches (ext_timing) and their summed   */
+    double material_kernel_ms;    /* HIP-event time                                          */
+    uint64_t control_launches;    /* timed CONTROL(+NEW_PATH) launches, likewise             */
+    double control_kernel_ms;
 } dcrt_traversal_stats;
 
 /* What the tracer chose for the uploaded scene (diagnostics; bench.py reports it). */
@@ -317,6 +321,28 @@ DCRT_API int dcrt_scene_get_material_count(const dcrt_scene* scene, uint32_t* ou
 DCRT_API int dcrt_scene_set_material(dcrt_scene* scene, uint32_t index, int material_type, const float albedo[3],
                                      float roughness, const float ior[3], const float k[3],
                                      int multiscattering, int two_sided);
+/* SMaterial as the scene holds it before UpdateMaterialGPUData translates it
+ * (Material.h:14-30, Scene.cpp:742-774): the oracle's own flattening reads this. */
+typedef struct dcrt_material_setting {
+    float albedo[3];
+    float roughness;
+    float ior[3];
+    float opacity;
+    float k[3];
+    float tiling[2];
+    uint32_t material_type;               /* DCRT_MATERIAL_TYPE_* */
+    int32_t albedo_texture_index;         /* -1 = INDEX_NONE */
+    int32_t opacity_texture_index;
+    uint32_t internal_scattering_mode;    /* DCRT_INTERNAL_SCATTERING_* */
+    uint32_t multiscattering;             /* m_Multiscattering */
+    uint32_t is_two_sided;
+    uint32_t has_roughness_texture;
+} dcrt_material_setting;
+DCRT_API int dcrt_scene_get_material_setting(const dcrt_scene* scene, uint32_t index, dcrt_material_setting* out_setting);
+/* The UI's "Multiscattering" checkbox (ImGui.cpp:620-626): only plastic, conductor and
+ * dielectric materials have it (DCRT_E_INVALID_ARG for diffuse / thin dielectric). Both
+ * loaders force the flag off (SceneXMLLoading.cpp:869, WavefrontOBJLoading.cpp:318). */
+DCRT_API int dcrt_scene_set_material_multiscattering(dcrt_scene* scene, uint32_t index, int enable);
 /* Material opacity and opacity texture (ImGui.cpp:630-650, SMaterial::m_Opacity /
  * m_OpacityTextureIndex); texture index -1 = none. Recomputes the instance OPAQUE flags
  * (Scene.cpp:57-80, 785-800). */
@@ -338,13 +364,44 @@ DCRT_API int dcrt_scene_get_bvh_info(const dcrt_scene* scene, uint32_t* tlas_nod
 /* The scene content as loaded, before BVHAccel reordered it -- the inputs of
  * Mesh::BuildBVH / BuildTLAS (Mesh.cpp:59-79, Scene.cpp:160-215): mesh i's vertices,
  * triangles (mesh-local vertex indices) and material ids in load order; instance j's
- * mesh index and XMFLOAT4X3 transform (4 rows of 3) in load order. Pointers stay valid
- * until the scene changes. Used to check the BVH build against an independent one. */
+ * mesh index and XMFLOAT4X3 transform (4 rows of 3) in load order. Each mesh's pointers
+ * stay valid until the scene is reset, loads more content or is destroyed. Used to check the BVH build against an independent one. */
 typedef struct dcrt_obj_mesh dcrt_obj_mesh;
 DCRT_API int dcrt_scene_get_content_counts(const dcrt_scene* scene, uint32_t* out_meshes, uint32_t* out_instances);
 DCRT_API int dcrt_scene_get_loaded_mesh(dcrt_scene* scene, uint32_t mesh, dcrt_obj_mesh* out_mesh);
 DCRT_API int dcrt_scene_get_instance(const dcrt_scene* scene, uint32_t instance, uint32_t* out_mesh_index,
                                      float out_transform[12]);
+
+/* The rest of CScene's state before UpdateLight/Material/InstanceFlagsGPUData and
+ * Render() flatten it (Scene.h:118-160, Camera.h, Scene.cpp:570-584, 672-807,
+ * WavefrontPathTracer.cpp:372-428): what the oracle's own flattening is driven from. */
+typedef struct dcrt_scene_settings {
+    uint32_t resolution[2];
+    uint32_t max_bounce_count;
+    uint32_t camera_type;                 /* 0 = pinhole, 1 = thin lens */
+    float fov_x, focal_length, focal_distance, relative_aperture;
+    uint32_t aperture_blade_count;
+    float aperture_rotation;
+    float film_size[2];
+    float camera_position[3];             /* CCamera::m_Position */
+    float camera_euler_angles[3];         /* CCamera::m_EulerAngles (pitch, yaw, roll) */
+    uint32_t features;                    /* DCRT_FEATURE_* */
+    uint32_t has_environment_light;
+    float environment_color[3];           /* SEnvironmentLight::m_Color */
+    const float* env_cube_rgb;            /* the environment texture (NULL = none) */
+    uint32_t env_cube_size;
+    uint32_t mesh_light_count, punctual_light_count, material_count, texture_count;
+} dcrt_scene_settings;
+DCRT_API int dcrt_scene_get_settings(const dcrt_scene* scene, dcrt_scene_settings* out_settings);
+/* SMeshLight i (Scene.h:42-46): the instance it lights (load order) and its radiance. */
+DCRT_API int dcrt_scene_get_mesh_light(const dcrt_scene* scene, uint32_t index, uint32_t* out_instance,
+                                       float out_color[3]);
+/* SPunctualLight i (Scene.h:27-40). */
+DCRT_API int dcrt_scene_get_punctual_light(const dcrt_scene* scene, uint32_t index, float out_position[3],
+                                           float out_euler_angles[3], float out_color[3], int* out_is_directional);
+/* SMeshInstance::m_MaterialIdOverride of instance j (load order; 0xFFFFFFFF = none). */
+DCRT_API int dcrt_scene_get_instance_material_override(const dcrt_scene* scene, uint32_t instance,
+                                                       uint32_t* out_override);
 
 /* Standalone BVHAccel::BuildBLAS + PackBVH over one triangle soup
  * (BVHAccel.cpp:376-447). out_nodes holds 2*triangle_count-1 entries at most;
@@ -427,7 +484,8 @@ DCRT_API int dcrt_tracer_copy_film_device(dcrt_tracer* tracer, void* d_dst);
 DCRT_API int dcrt_tracer_add_film_device(dcrt_tracer* tracer, const void* d_src);
 DCRT_API int dcrt_tracer_counters(dcrt_tracer* tracer, dcrt_ray_stats* out_stats);
 /* counters != 0: traversal work counters in the cast kernels; ext_timing != 0: plain
- * (non-graph) launches with HIP events around every EXTENSION_RAY_CAST launch. */
+ * (non-graph) launches with HIP events around every EXTENSION_RAY_CAST, MATERIAL and
+ * CONTROL launch. */
 DCRT_API int dcrt_tracer_set_instrumentation(dcrt_tracer* tracer, int counters, int ext_timing);
 DCRT_API int dcrt_tracer_traversal_stats(dcrt_tracer* tracer, dcrt_traversal_stats* out_stats);
 DCRT_API int dcrt_tracer_reset_stats(dcrt_tracer* tracer);

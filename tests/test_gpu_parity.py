@@ -495,11 +495,14 @@ def test_traversal_variants_wavefront_bit_exact(native_lib, golden_luts, oracle_
         t.destroy()
 
 
-@pytest.mark.parametrize("name,cube", [("coffee", True), ("spaceship", False), ("lamp", False)])
-def test_config_scenes_bit_exact(gpu_tracer, golden_luts, oracle_mod, name, cube):
-    """configs[2..4] (coffee / spaceship / lamp, procedural XML fixtures) at 160x90, 8 bounces."""
+@pytest.mark.parametrize("name,cube,ms", [("coffee", True, True), ("coffee", True, False), ("spaceship", False, False),
+                                          ("lamp", False, False)])
+def test_config_scenes_bit_exact(gpu_tracer, golden_luts, oracle_mod, name, cube, ms):
+    """configs[2..4] (coffee / spaceship / lamp, procedural XML fixtures) at 160x90, 8 bounces;
+    coffee as configs[2] names it (Kulla-Conty multiscattering on every plastic, conductor and
+    dielectric material) and as the loader leaves it (off)."""
     from test_oracle import load_fixture_scene
-    s = load_fixture_scene(name, env_cube=cube)
+    s = load_fixture_scene(name, env_cube=cube, multiscattering=ms)
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 1]))
 
 

@@ -309,13 +309,34 @@ def test_xml_scene_oracle_renders(oracle_mod, golden_luts):
 SCENE_FIXTURES = {"coffee": "coffee.xml", "spaceship": "spaceship_64x32.xml", "lamp": "lamp.xml"}
 
 
-def load_fixture_scene(name, env_cube=False):
+def load_fixture_scene(name, env_cube=False, multiscattering=False):
+    """A configs[2..4] fixture; ``multiscattering`` ticks the UI's Kulla-Conty box
+    (ImGui.cpp:620-626) on every material that has it, as configs[2] names it."""
     from directcomputeraytracing_amd import Scene, scenes
     s = Scene((8, 8))
     s.load_from_file(GOLDEN / "scenes" / SCENE_FIXTURES[name])
     if env_cube:
         s.set_environment_light((1.0, 1.0, 1.0), scenes.env_cube(16))
+    if multiscattering:
+        assert s.enable_multiscattering()
     return s
+
+
+def test_multiscattering_checkbox():
+    """Scene.set_multiscattering = the UI checkbox (ImGui.cpp:620-626): plastic, conductor and
+    dielectric only; the flag reaches the material's GPU flags (Scene.cpp:763)."""
+    from directcomputeraytracing_amd import DCRTError, _abi
+    s = load_fixture_scene("coffee")
+    before = s.arrays()["materials"][:, 11].copy()
+    assert not (before & 0x80).any()                  # the XML loader leaves it off (SceneXMLLoading.cpp:869)
+    changed = s.enable_multiscattering()
+    types = [s.material_setting(i).material_type for i in range(s.material_count)]
+    assert changed == [i for i, t in enumerate(types) if t in (1, 2, 3)] and len(changed) >= 4
+    after = s.arrays()["materials"][:, 11]
+    assert np.array_equal(after, before | np.where(np.isin(np.arange(len(types)), changed), 0x80, 0).astype(np.uint32))
+    diffuse = types.index(_abi.MATERIAL_DIFFUSE)
+    with pytest.raises(DCRTError):
+        s.set_multiscattering(diffuse, True)
 
 
 def test_scene_fixtures_are_reproducible(tmp_path):

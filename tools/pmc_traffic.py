@@ -72,6 +72,12 @@ def main(src, dst_prefix):
     out["ext_valu_issue_frac"] = ext.get("valu_issue_frac")
     out["ext_valu_insts_per_launch"] = ext.get("SQ_INSTS_VALU_avg")
     out["ext_implied_clock_ghz"] = ext.get("implied_clock_ghz")
+    # MATERIAL's own statement (the second-heaviest kernel)
+    mat = next((v for k, v in out["kernels"].items() if k.startswith("dcrt::dev::material_kernel")), {})
+    out["material_hbm_bytes_per_launch"] = mat.get("hbm_bytes_per_launch")
+    out["material_valu_issue_frac"] = mat.get("valu_issue_frac")
+    out["material_read_bytes_per_launch"] = mat.get("hbm_read_bytes_per_launch")
+    out["material_write_bytes_per_launch"] = mat.get("hbm_write_bytes_per_launch")
     # the workload the PMC passes profiled (bench.py matches its own run against it)
     log = src / "pmc_FETCH_SIZE.log"
     line = next((l for l in (log.read_text().splitlines() if log.exists() else []) if l.startswith("{")), None)
@@ -81,6 +87,24 @@ def main(src, dst_prefix):
         out["workload"] = {"config": cfg["name"], "resolution": cfg["resolution"], "images": roof["images"],
                            "path_pool": cfg["path_pool"], "world": b["n_gpus"]}
         out["bench_avg_launch_us"] = roof["avg_launch_us"]
+        # Whole-pipeline HBM bytes per image. The profiled command (tools/prof_config.sh: one
+        # pipeline, one repeat, no warm-up) renders the same images three times -- the timed
+        # run, the roofline leg's counting pass (instrumented cast kernel) and its timing pass
+        # -- so a per-iteration kernel's launches cover 3 x images, the plain cast kernel's 2 x
+        # images and the instrumented cast's (a diagnostic variant, left out) 1 x images.
+        # One-time scene set-up kernels (LUT integration, triangle gathers) are not per image.
+        images = roof["images"]
+        per_image = {}
+        for name, d in out["kernels"].items():
+            if not name.startswith("dcrt::dev::") or "hbm_bytes_per_launch" not in d or "calls" not in d:
+                continue
+            short = name.split("::")[-1]
+            if short.startswith(("lut_", "build_tri_verts")) or short.startswith("cast_kernel<true"):
+                continue
+            legs = 2 if short.startswith(("cast_kernel", "extension_kernel", "shadow_kernel")) else 3
+            per_image[short] = d["hbm_bytes_per_launch"] * d["calls"] / (legs * images)
+        out["pipeline_hbm_bytes_per_image"] = sum(per_image.values())
+        out["pipeline_hbm_bytes_per_image_by_kernel"] = per_image
     Path(dst_prefix + "_pmc_traffic.json").write_text(json.dumps(out, indent=1, sort_keys=True))
     print(json.dumps({"ext_hbm_bytes_per_launch": out["ext_hbm_bytes_per_launch"]}))
 
