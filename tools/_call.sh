@@ -1,11 +1,8 @@
 set -u
-cd $GRAFT_REPO_ROOT
+cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-for i in 1 2; do
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_$i.log 2>&1 || exit $?
-python -c "import json;d=json.load(open('gpurun_out/bench_$i.log'));print('bench', d['ms_per_spp'], d['value'], d['roofline']['avg_launch_us'], d['roofline']['frac'])"
-DCRT_MATERIAL_GENERIC=1 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_g$i.log 2>&1 || exit $?
-python -c "import json;d=json.load(open('gpurun_out/bench_g$i.log'));print('generic', d['ms_per_spp'], d['value'], d['roofline']['avg_launch_us'])"
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+CONFIG=cornell STEPS=20 OUT=gpurun_out/prof_c20 bash tools/prof_config.sh || exit $?
+python tools/pmc_traffic.py gpurun_out/prof_c20 gpurun_out/r04pre_c20 || exit $?
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --traffic-json gpurun_out/r04pre_c20_pmc_traffic.json --spaceship-spp 0 > gpurun_out/bench_s20.json 2> gpurun_out/bench_s20.err; echo "bench rc=$?"
