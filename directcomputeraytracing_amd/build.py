@@ -125,7 +125,8 @@ def build_examples(force: bool = False) -> Path:
 
 def build_oracle(force: bool = False) -> Path:
     """TEST INFRASTRUCTURE: compile the CPU restatement (gcc, no contraction)."""
-    src = [ORACLE_DIR / "dcrt_oracle.c", ORACLE_DIR / "dcrt_oracle_bvh.c", ORACLE_DIR / "dcrt_oracle.h",
+    src = [ORACLE_DIR / "dcrt_oracle.c", ORACLE_DIR / "dcrt_oracle_bvh.c", ORACLE_DIR / "dcrt_oracle_scene.c",
+           ORACLE_DIR / "dcrt_oracle.h",
            ORACLE_DIR / "Makefile", ROOT / "include" / "dcrt.h"]
     digest = _digest(src)
     stamp = ORACLE_LIB.with_suffix(".so.sha256")

@@ -86,6 +86,10 @@ def load():
     lib.oracle_bvh_build_tlas.argtypes = [P(C.c_float), P(C.c_float), U, P(OracleBVHNode), P(U), P(U), P(U), P(U), P(U)]
     lib.oracle_bvh_pack.restype = None
     lib.oracle_bvh_pack.argtypes = [P(OracleBVHNode), U, C.c_int, P(A.BVHNode), U, U]
+    lib.oracle_frame_params.restype = None
+    lib.oracle_frame_params.argtypes = [P(A.SceneSettings), U, P(A.FrameParams)]
+    lib.oracle_punctual_direction.restype = None
+    lib.oracle_punctual_direction.argtypes = [P(C.c_float), P(C.c_float)]
     _lib = lib
     return lib
 
@@ -321,32 +325,209 @@ def sum_log_luminance(film):
     return load().oracle_sum_log_luminance(_fp(film), film.shape[1], film.shape[0])
 
 
-def flat_with_own_bvh(scene):
-    """The product's flat scene with the BVH half replaced by the oracle's own build
-    (build_scene_bvh over the scene's loaded meshes and instances): nodes, triangles,
-    material ids, stack size. Per-instance arrays (inverse transforms -- DirectXMath's
-    XMMatrixInverse is parity unpinned -- flags, overrides, light indices) are taken from
-    the product after checking that both builds order the instances identically. The
-    returned FlatScene keeps its arrays alive."""
+# ---- the oracle's own CScene flattening (Scene.cpp:423-552, 672-807; WavefrontPathTracer.cpp:372-428) ----
+# Driven from the scene state the loaders produced (dcrt_scene_get_settings / _material_setting /
+# _mesh_light / _punctual_light / _instance_material_override, dcrt_scene_get_loaded_mesh /
+# _instance): everything the reference's flattening derives from it is restated here, separately
+# from csrc/host/scene.cpp. The texture texels and the environment cube are loader outputs and are
+# taken as loaded.
+
+def f32_from_fraction(x) -> np.float32:
+    """An exact rational rounded to the nearest float32 (ties to even), as one IEEE operation
+    would round it (no double rounding through float64)."""
+    import math
+    from fractions import Fraction
+    x = Fraction(x)
+    if x == 0:
+        return np.float32(0.0)
+    neg = x < 0
+    n, d = abs(x.numerator), x.denominator
+    e = n.bit_length() - d.bit_length()          # 2^e <= |x| < 2^(e+1) after the correction
+    if (n << max(0, -e)) < (d << max(0, e)):
+        e -= 1
+    e = max(e, -126)                              # subnormals share the minimum exponent
+    shift = 23 - e                                # |x| * 2^shift: the 24-bit significand
+    num, den = (n << shift, d) if shift >= 0 else (n, d << -shift)
+    m, r = divmod(num, den)
+    if 2 * r > den or (2 * r == den and m & 1):
+        m += 1
+    v = math.ldexp(m, e - 23)
+    if v >= 2.0 ** 128:
+        v = math.inf
+    return np.float32(-v if neg else v)
+
+
+def inverse_affine_exact(t43) -> np.ndarray:
+    """XMMatrixInverse of an XMFLOAT4X3 instance transform (row vectors: rows 0-2 the linear
+    part A, row 3 the translation t), as the exactly rounded inverse [[A^-1, 0], [-t A^-1, 1]]:
+    (4, 3) float32. DirectXMath's own float arithmetic is not available here: parity unpinned;
+    this is the exactly rounded value of what it approximates."""
+    from fractions import Fraction
+    M = [[Fraction(float(v)) for v in row] for row in np.asarray(t43, np.float32).reshape(4, 3)]
+    a = M[:3]
+    det = (a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) - a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0])
+           + a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]))
+    out = np.zeros((4, 3), np.float32)
+    if det == 0:
+        return out
+    inv = [[None] * 3 for _ in range(3)]
+    for r in range(3):
+        for c in range(3):
+            rows = [i for i in range(3) if i != c]
+            cols = [j for j in range(3) if j != r]
+            minor = a[rows[0]][cols[0]] * a[rows[1]][cols[1]] - a[rows[0]][cols[1]] * a[rows[1]][cols[0]]
+            inv[r][c] = (minor if (r + c) % 2 == 0 else -minor) / det
+    t = M[3]
+    for r in range(3):
+        for c in range(3):
+            out[r, c] = f32_from_fraction(inv[r][c])
+    for c in range(3):
+        out[3, c] = f32_from_fraction(-(t[0] * inv[0][c] + t[1] * inv[1][c] + t[2] * inv[2][c]))
+    return out
+
+
+def _clamp01(v) -> np.float32:   # std::clamp(v, 0.f, 1.f): NaN passes through
+    v = np.float32(v)
+    return np.float32(0.0) if v < 0 else (np.float32(1.0) if v > 1 else v)
+
+
+def frame_params(scene, frame_seed: int = 0):
+    """The frame constants Render() uploads (WavefrontPathTracer.cpp:372-428), from the scene
+    state: camera matrix, film distance, aperture, blade vertex, light count (C restatement,
+    dcrt_oracle_scene.c)."""
     from directcomputeraytracing_amd import _abi as A
+    out = A.FrameParams()
+    settings = scene.settings()
+    load().oracle_frame_params(C.byref(settings), int(frame_seed), C.byref(out))
+    return out
+
+
+def flatten_scene(scene):
+    """The flattened scene (dcrt_flat_scene: Scene.cpp:273-608 uploads plus UpdateLight /
+    Material / InstanceFlagsGPUData, Scene.cpp:672-807), built by the oracle from the scene
+    state alone: its own BVHAccel build (build_scene_bvh), its own light array, material
+    translation, instance arrays and inverse transforms. The returned FlatScene keeps its
+    arrays alive."""
+    from directcomputeraytracing_amd import _abi as A
+    lib = load()
     meshes, instances = scene.loaded_content()
     own = build_scene_bvh(meshes, instances)
-    src = scene.flat()
-    n = src.instance_count
-    fwd = np.ctypeslib.as_array(C.cast(src.instance_transforms, C.POINTER(C.c_float)), (n * 12,)).reshape(n, 12)
-    if not np.array_equal(fwd.view(np.uint32), own["forward_transforms"].view(np.uint32)):
-        raise AssertionError("instance order differs between the product and the oracle BVH build")
-    keep = {"nodes": np.ascontiguousarray(own["nodes"], np.uint32),
+    settings = scene.settings()
+    order = [int(i) for i in own["instance_order"]]               # reordered -> original
+    reordered = {orig: r for r, orig in enumerate(order)}          # original -> reordered
+    overrides = scene.instance_material_overrides()
+    mats = [scene.material_setting(i) for i in range(settings.material_count)]
+
+    # materials (UpdateMaterialGPUData, Scene.cpp:742-774): a conductor's albedo slot carries k
+    materials = np.zeros((len(mats), 13), np.uint32)
+    mf = materials.view(np.float32)
+    for i, m in enumerate(mats):
+        albedo = m.k if m.material_type == A.MATERIAL_CONDUCTOR else m.albedo
+        mf[i, 0:3] = np.array(albedo[:], np.float32)
+        tex = -1 if m.material_type in (A.MATERIAL_CONDUCTOR, A.MATERIAL_DIELECTRIC) else m.albedo_texture_index
+        materials[i, 3] = np.uint32(tex & 0xFFFFFFFF)
+        mf[i, 4:7] = np.array(m.ior[:], np.float32)
+        mf[i, 7] = _clamp01(m.roughness)
+        mf[i, 8:10] = np.array(m.tiling[:], np.float32)
+        mf[i, 10] = np.float32(m.opacity)
+        flags = m.material_type & 0xF
+        flags |= 0x80 if m.multiscattering else 0
+        flags |= 0x40 if m.is_two_sided else 0
+        flags |= 0x20 if m.has_roughness_texture else 0
+        flags |= (m.internal_scattering_mode << 8) & 0x300
+        materials[i, 11] = flags
+        materials[i, 12] = np.uint32(m.opacity_texture_index & 0xFFFFFFFF)
+
+    def is_opaque(i):   # SMaterial::IsOpaque (Scene.cpp:57-60)
+        return np.float32(mats[i].opacity) == np.float32(1.0) and mats[i].opacity_texture_index == -1
+
+    # mesh flags (Scene.cpp:62-90): opaque when every triangle's material is
+    mesh_opaque = [all(is_opaque(int(i)) for i in m["material_ids"]) for m in meshes]
+    ni = len(instances)
+    # instance arrays in TLAS (reordered) order (Scene.cpp:423-552, 776-807)
+    transforms = np.zeros((2 * ni, 12), np.float32)
+    flags = np.zeros(ni, np.uint32)
+    ovr = np.zeros(ni, np.uint32)
+    for r, orig in enumerate(order):
+        mesh, t = instances[orig]
+        t = np.asarray(t, np.float32).reshape(4, 3)
+        inv = inverse_affine_exact(t)
+        transforms[r] = t.T.reshape(12)          # XMFLOAT4X3(_11, _21, _31, _41, _12, ...)
+        transforms[ni + r] = inv.T.reshape(12)
+        o = overrides[orig]
+        opaque = is_opaque(o) if o != 0xFFFFFFFF else mesh_opaque[mesh]
+        flags[r] = 1 if opaque else 0
+        ovr[r] = o
+    # mesh lights, then the environment light, then the punctual lights (Scene.cpp:672-735);
+    # each instance's light index (Scene.cpp:467-499)
+    mesh_lights = scene.mesh_lights()
+    tri_offsets = np.concatenate([[0], np.cumsum([len(m["indices"]) for m in meshes])]).astype(np.uint32)
+    lights = []
+    light_index = np.full(ni, 0xFFFFFFFF, np.uint32)
+    for li, (inst, color) in enumerate(mesh_lights):
+        mesh = instances[inst][0]
+        rec = np.zeros(7, np.uint32)
+        rec[0:3] = np.array(color, np.float32).view(np.uint32)
+        rec[3] = tri_offsets[mesh]
+        rec[4] = len(meshes[mesh]["indices"])
+        rec[5] = reordered[inst]
+        rec[6] = 0x2
+        lights.append(rec)
+        light_index[reordered[inst]] = li
+    if settings.has_environment_light:
+        rec = np.zeros(7, np.uint32)
+        rec[0:3] = np.array(settings.environment_color[:], np.float32).view(np.uint32)
+        rec[6] = 0x8
+        lights.append(rec)
+    for pos, euler, color, directional in scene.punctual_lights():
+        rec = np.zeros(7, np.uint32)
+        rec[0:3] = np.array(color, np.float32).view(np.uint32)
+        if directional:
+            e = (C.c_float * 3)(*euler)
+            d = (C.c_float * 3)()
+            lib.oracle_punctual_direction(e, d)
+            rec[3:6] = np.array(d[:], np.float32).view(np.uint32)
+        else:
+            rec[3:6] = np.array(pos, np.float32).view(np.uint32)
+        rec[6] = 0x4 if directional else 0x1
+        lights.append(rec)
+    lights = np.array(lights, np.uint32).reshape(-1, 7)
+    vertices = np.ascontiguousarray(np.concatenate([m["vertices"] for m in meshes]), np.float32)
+    keep = {"vertices": vertices, "nodes": np.ascontiguousarray(own["nodes"], np.uint32),
             "triangles": np.ascontiguousarray(own["triangles"], np.uint32),
-            "material_ids": np.ascontiguousarray(own["material_ids"], np.uint32)}
+            "material_ids": np.ascontiguousarray(own["material_ids"], np.uint32),
+            "transforms": transforms, "light_index": light_index, "flags": flags, "overrides": ovr,
+            "materials": materials, "lights": lights if len(lights) else np.zeros((1, 7), np.uint32)}
+    src = scene.flat()   # only for the loaders' texture texels
     f = A.FlatScene()
-    C.pointer(f)[0] = src
+    f.vertices = keep["vertices"].ctypes.data_as(C.POINTER(A.Vertex))
+    f.vertex_count = vertices.shape[0]
     f.triangles = keep["triangles"].ctypes.data_as(C.POINTER(C.c_uint32))
     f.triangle_count = keep["triangles"].shape[0]
     f.bvh_nodes = keep["nodes"].ctypes.data_as(C.POINTER(A.BVHNode))
     f.bvh_node_count = keep["nodes"].shape[0]
     f.tlas_node_count = own["tlas_node_count"]
     f.material_ids = keep["material_ids"].ctypes.data_as(C.POINTER(C.c_uint32))
+    f.instance_transforms = keep["transforms"].ctypes.data_as(C.POINTER(A.Float4x3))
+    f.instance_count = ni
+    f.instance_light_indices = keep["light_index"].ctypes.data_as(C.POINTER(C.c_uint32))
+    f.instance_flags = keep["flags"].ctypes.data_as(C.POINTER(C.c_uint32))
+    f.instance_material_overrides = keep["overrides"].ctypes.data_as(C.POINTER(C.c_uint32))
+    f.materials = keep["materials"].ctypes.data_as(C.POINTER(A.Material))
+    f.material_count = len(mats)
+    f.lights = keep["lights"].ctypes.data_as(C.POINTER(A.Light))
+    f.light_count = len(lights)
+    f.environment_light_index = len(mesh_lights) if settings.has_environment_light else 0xFFFFFFFF
+    f.textures = src.textures
+    f.texture_count = src.texture_count
+    f.env_cube_rgb = settings.env_cube_rgb if settings.env_cube_size else None
+    f.env_cube_size = settings.env_cube_size
     f.bvh_traversal_stack_size = own["stack_size"]
     f._keep = (keep, scene)
     return f
+
+
+def flat_with_own_bvh(scene):
+    """The oracle side of every GPU parity test: the scene flattened by the oracle alone
+    (flatten_scene -- its own BVHAccel build, lights, materials, instance arrays)."""
+    return flatten_scene(scene)

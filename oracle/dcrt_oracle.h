@@ -102,6 +102,11 @@ int oracle_bvh_build_tlas(const float* blas_root_boxes, const float* transforms,
 void oracle_bvh_pack(const oracle_bvh_node* nodes, uint32_t count, int is_blas, dcrt_bvh_node* out, uint32_t node_offset,
                      uint32_t prim_offset);
 
+/* dcrt_oracle_scene.c: the float half of CScene's flattening (frame constants,
+ * WavefrontPathTracer.cpp:372-428; directional light direction, Scene.cpp:946-955). */
+void oracle_frame_params(const dcrt_scene_settings* settings, uint32_t frame_seed, dcrt_frame_params* out);
+void oracle_punctual_direction(const float euler[3], float out[3]);
+
 #ifdef __cplusplus
 }
 #endif

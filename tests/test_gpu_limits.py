@@ -39,7 +39,7 @@ def test_2p26_pool_renders_4k_strip_bit_exact(native_lib, golden_luts, oracle_mo
         t.render_images(11, 2)
         pos, val = t.read_samples()
         rng = t.read_rng()
-        p_ref, v_ref, r_ref, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(12),
+        p_ref, v_ref, r_ref, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, oracle_mod.frame_params(s, 12),
                                                    oracle_mod.WAVEFRONT, rng=True)
         assert np.array_equal(rng, r_ref)
         assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
@@ -68,7 +68,7 @@ def test_4k_batch_past_2p32_sample_bytes(native_lib, golden_luts, oracle_mod):
     finally:
         t.destroy()
     flat = oracle_mod.flat_with_own_bvh(s)
-    fr = s.frame_params(n - 1)
+    fr = oracle_mod.frame_params(s, n - 1)
     for y0 in (0, H // 2, H - 3):
         p_ref, v_ref, r_ref, _ = oracle_mod.render(flat, golden_luts, fr, oracle_mod.WAVEFRONT, rect=(0, y0, W, 3), rng=True)
         rows = slice(y0, y0 + 3)

@@ -6,9 +6,10 @@ sides compile without contraction and with IEEE div/sqrt and share the same
 deterministic transcendentals (DESIGN.md "Numerics"). Where a float
 comparison is not bit-exact the tolerance is stated in the assertion.
 
-The oracle side renders the scene with its OWN BVH (oracle.flat_with_own_bvh: the
-oracle's independent BVHAccel restatement over the scene's loaded meshes, see
-tests/test_bvh_pin.py), not with the product's flattened nodes and triangles.
+The oracle side renders the scene flattened by the oracle ALONE (oracle.flat_with_own_bvh =
+oracle.flatten_scene: its independent BVHAccel restatement over the scene's loaded meshes,
+tests/test_bvh_pin.py, and its own lights, materials and instance arrays, tests/test_scene_pin.py)
+with the oracle's own frame constants (oracle.frame_params), not with the product's flat scene.
 """
 import numpy as np
 import pytest
@@ -93,7 +94,8 @@ def _render_and_compare(tracer, oracle_mod, luts, scene, seeds):
         assert tracer.is_image_complete()
         pos, val = tracer.read_samples()
         rng = tracer.read_rng()
-        p_ref, v_ref, r_ref, c_ref = oracle_mod.render(flat, luts, fr, oracle_mod.WAVEFRONT, rng=True)
+        p_ref, v_ref, r_ref, c_ref = oracle_mod.render(flat, luts, oracle_mod.frame_params(scene, seed), oracle_mod.WAVEFRONT,
+                                                        rng=True)
         assert np.array_equal(rng, r_ref), f"seed {seed}: RNG state differs at {np.count_nonzero((rng != r_ref).any(-1))} px"
         assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32)), f"seed {seed}: sample positions"
         bad = np.count_nonzero(~same_bits(val, v_ref).all(-1))
@@ -180,7 +182,7 @@ def test_film_accumulation_matches_oracle(native_lib, golden_luts, oracle_mod):
             film = t.read_film()
             ref = np.zeros_like(film)
             for seed in range(3):
-                p, v, _, _ = oracle_mod.render(flat, golden_luts, s.frame_params(seed), oracle_mod.WAVEFRONT)
+                p, v, _, _ = oracle_mod.render(flat, golden_luts, oracle_mod.frame_params(s, seed), oracle_mod.WAVEFRONT)
                 oracle_mod.sample_convolution(filt, p, v, ref)
             assert same_bits(film, ref).all(), \
                 f"filter {filt.filter}: max |d| {np.abs(film - ref).max()}"
@@ -210,7 +212,7 @@ def test_film_radius_just_below_half_integer(native_lib, golden_luts, oracle_mod
             film = t.read_film()
             ref = np.zeros_like(film)
             for seed in range(2):
-                p, v, _, _ = oracle_mod.render(flat, golden_luts, s.frame_params(seed), oracle_mod.WAVEFRONT)
+                p, v, _, _ = oracle_mod.render(flat, golden_luts, oracle_mod.frame_params(s, seed), oracle_mod.WAVEFRONT)
                 oracle_mod.sample_convolution(filt, p, v, ref)
             assert same_bits(film, ref).all(), f"filter {filt.filter} r={filt.radius!r}"
     finally:
@@ -314,7 +316,7 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
             t.destroy()
     for f in films[1:]:
         assert same_bits(f, films[0]).all()
-    p_ref, v_ref, _, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(7), oracle_mod.WAVEFRONT)
+    p_ref, v_ref, _, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, oracle_mod.frame_params(s, 7), oracle_mod.WAVEFRONT)
     for pos, val in samples:
         assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
@@ -366,7 +368,7 @@ def test_tiny_pool_renders_every_pixel(native_lib, golden_luts, oracle_mod):
         pos, val = t.read_samples()
     finally:
         t.destroy()
-    p_ref, v_ref, _, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(4), oracle_mod.WAVEFRONT)
+    p_ref, v_ref, _, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, oracle_mod.frame_params(s, 4), oracle_mod.WAVEFRONT)
     assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
 
@@ -410,7 +412,7 @@ def test_traversal_counters_match_oracle(native_lib, golden_luts, oracle_mod, mo
         t.render_images(2, 1)
         st = t.traversal_stats()
         c = t.counters()
-        _, _, _, ref = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(2), oracle_mod.WAVEFRONT)
+        _, _, _, ref = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, oracle_mod.frame_params(s, 2), oracle_mod.WAVEFRONT)
         assert c["extension_rays"] == ref["extension_rays"]
         assert c["shadow_rays"] == ref["shadow_rays"]
         assert st["ext_node_visits"] == ref["node_visits"]
@@ -545,7 +547,7 @@ def test_pair_order_trace_rays_and_megakernel_bit_exact(native_lib, golden_luts,
         t.clear_film()
         t.render_images(4, 1)
         pos, val = t.read_samples()
-        p_ref, v_ref, r_ref, _ = oracle_mod.render(flat, golden_luts, s.frame_params(4), oracle_mod.MEGAKERNEL, rng=True)
+        p_ref, v_ref, r_ref, _ = oracle_mod.render(flat, golden_luts, oracle_mod.frame_params(s, 4), oracle_mod.MEGAKERNEL, rng=True)
         assert np.array_equal(t.read_rng(), r_ref)
         assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
         assert same_bits(val, v_ref).all()
@@ -647,7 +649,7 @@ def test_megakernel_matches_oracle_megakernel(native_lib, golden_luts, oracle_mo
             t.render_images(seed, 1)
             pos, val = t.read_samples()
             rng = t.read_rng()
-            p_ref, v_ref, r_ref, c_ref = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(seed), oracle_mod.MEGAKERNEL,
+            p_ref, v_ref, r_ref, c_ref = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, oracle_mod.frame_params(s, seed), oracle_mod.MEGAKERNEL,
                                                            rng=True)
             assert np.array_equal(rng, r_ref)
             assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
@@ -691,7 +693,7 @@ def test_anyhit_megakernel_bit_exact(native_lib, golden_luts, oracle_mod, name):
         t.clear_film()
         t.render_images(2, 1)
         pos, val = t.read_samples()
-        p_ref, v_ref, r_ref, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, s.frame_params(2), oracle_mod.MEGAKERNEL, rng=True)
+        p_ref, v_ref, r_ref, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, oracle_mod.frame_params(s, 2), oracle_mod.MEGAKERNEL, rng=True)
         assert np.array_equal(t.read_rng(), r_ref)
         assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
         assert same_bits(val, v_ref).all()
