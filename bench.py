@@ -48,9 +48,11 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--bounces", type=int, default=8)
-    ap.add_argument("--config", default="cornell", choices=["cornell", "coffee", "spaceship", "lamp"],
+    ap.add_argument("--config", default="cornell", choices=["cornell", "coffee", "spaceship", "lamp", "spaceship_close"],
                     help="BASELINE.json configs[1..4]; the headline (and default) is cornell = configs[1]")
     ap.add_argument("--scene-dir", default="/tmp/dcrt_scenes", help="where the procedural config scenes are written")
+    ap.add_argument("--no-multiscattering", action="store_true",
+                    help="coffee: keep the loaders' Kulla-Conty flag (off) instead of configs[2]'s multiscattering (A/B)")
     ap.add_argument("--snapshot-spp", type=int, default=0,
                     help="progressive: reduce the film onto rank 0 every K images (configs[4]); 0 = once at the end")
     ap.add_argument("--pool", type=int, default=0,
@@ -198,10 +200,12 @@ def main():
         workload = (f"cornell_box_obj {args.width}x{args.height}, {{spp}} spp ({world} spp/step, film stripes across "
                     f"{world} GPU(s)), {args.bounces} bounces, wavefront, point light")
     else:
-        desc = scenes.setup_config(scene, args.config, args.scene_dir)
+        desc = scenes.setup_config(scene, args.config, args.scene_dir, multiscattering=not args.no_multiscattering)
         args.width, args.height = scene.resolution
         workload = f"{desc}, {{spp}} spp ({world} spp/step, film stripes across {world} GPU(s)), wavefront"
     args.pool = args.pool or scenes.default_pool(args.width, args.height)
+    # (the coffee scene without configs[2]'s multiscattering is its own workload)
+    config_name = args.config + ("_noms" if args.config == "coffee" and args.no_multiscattering else "")
     filt = scene.filter_params()
     from directcomputeraytracing_amd.partition import halo_for_radius, pipeline_pool, render_rows, stream_partition
     halo = max(1, halo_for_radius(filt.radius, args.height))
@@ -375,7 +379,7 @@ def main():
         for t in tracers:
             t.destroy()
         tracer = make_tracer(args.pool, (world, rank, args.stripe) if world > 1 else None)
-    roof = cast_roofline(tracer, R, filt, {"config": args.config, "resolution": [args.width, args.height], "images": R,
+    roof = cast_roofline(tracer, R, filt, {"config": config_name, "resolution": [args.width, args.height], "images": R,
                                            "path_pool": args.pool, "world": world}, args.traffic_json)
     st, cr, tm = roof.pop("_stats"), roof.pop("_counters"), roof.pop("_timing")
     pmc, pmc_src = roof.pop("_pmc")
@@ -392,7 +396,7 @@ def main():
 
     result = {
         "metric": ("Mrays/s and ms/spp at 1920x1080, 8-bounce wavefront" if args.config == "cornell"
-                   else f"Mrays/s and ms/spp at {args.width}x{args.height}, {args.config} config, wavefront"),
+                   else f"Mrays/s and ms/spp at {args.width}x{args.height}, {config_name} config, wavefront"),
         "value": round(rays / elapsed / 1e6, 2),
         "unit": "Mrays/s",
         "n_gpus": world,
@@ -407,7 +411,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": workload.format(spp=images), "name": args.config,
+        "config": {"workload": workload.format(spp=images), "name": config_name,
                    "resolution": [args.width, args.height], "spp": images,
                    "max_bounce": args.bounces if args.config == "cornell" else scene.frame_params(0).max_bounce_count,
                    "path_pool": args.pool, "streams_per_gpu": K, "snapshot_spp": args.snapshot_spp or images,

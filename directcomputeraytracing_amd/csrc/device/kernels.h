@@ -17,6 +17,7 @@ constexpr uint32_t kFlagShadowRayHit = 0x40000000u;
 constexpr uint32_t kFlagTerminate = 0x20000000u;
 constexpr uint32_t kFlagDelta = 0x10000000u;           // the path's last BSDF lobe was a delta (SPathAccumulation.isDelta)
 constexpr uint32_t kFlagFirst = 0x08000000u;           // a new path's state record holds NEW_PATH's rng only (PathStateA)
+constexpr uint32_t kFlagShadowPending = 0x04000000u;   // the path cast a shadow ray last pass: its result is at its position
 constexpr uint32_t kBlockW = 8, kBlockH = 8;           // one wave64 = one 8x8 pixel block
 #ifndef DCRT_CONTROL_BLOCK
 #define DCRT_CONTROL_BLOCK 256
@@ -41,13 +42,24 @@ constexpr uint32_t kQExt = 0, kQShadow = 1, kQFinish = 2, kQueues = 3;
 #endif
 constexpr uint32_t kFinShards = DCRT_FIN_SHARDS;
 constexpr uint32_t kCounterWords = 2 * kShards + kFinShards;   // ext, shadow, then finish shards
+// One more word per parity (its own 256-B line): nonzero = this iteration's extension queue is
+// a batch start's VIRTUAL queue -- item i is path slot i, whose camera ray the cast generates
+// and whose NEW_PATH state the next MATERIAL pass recomputes (see control_kernel); its value is
+// the number of items (the pool size; slots without a pixel are holes)
+constexpr uint32_t kVirtualWord = kCounterWords;
+constexpr uint32_t kNoPixel = 0xFFFFFFFFu;             // a virtual item (path slot) without a pixel
+// And one more: nonzero = drain_kernel completed every path this iteration's queues held (the
+// next MATERIAL / CONTROL pass has nothing to take from them)
+constexpr uint32_t kDrainedWord = kCounterWords + 1;
 // Extension-queue entry bit: the path's first MATERIAL pass follows (set by NEW_PATH), whose
 // Li, light sampling result and throughput are the NEW_PATH constants, not stored or loaded
 constexpr uint32_t kEntryFirst = 0x80000000u;
 
 struct Counters {        // one set per iteration parity
-    uint32_t w[kCounterWords * kShardStride];
+    uint32_t w[(kCounterWords + 2) * kShardStride];
 };
+DEV uint32_t virtual_items(const Counters* c) { return c->w[kVirtualWord * kShardStride]; }
+DEV bool drained(const Counters* c) { return c->w[kDrainedWord * kShardStride] != 0u; }
 struct Globals {
     uint32_t nextBlock[kShards * kShardStride];        // per-shard pixel-block cursors
     uint32_t totalBlocks;
@@ -134,6 +146,8 @@ struct FrameConstants {
     uint32_t blocksX, bandCount;     // blocks per row, number of 8-row groups of the rendered rows
     uint32_t blocksPerImage;         // blocksX * bandCount
     uint32_t refillLanes, parkLanes; // persistent traversal thresholds (lanes of a wave64)
+    uint32_t virtualStart;           // batch starts use the virtual extension queue (kVirtualWord)
+    uint32_t drainPaths;             // drain_kernel completes the live paths once at most this many remain (0: off)
 };
 
 // SampleAperture + GenerateRay (RayTracingCommon.inc.hlsl:38-86).
@@ -310,6 +324,28 @@ DEV float2 pixel_sample(const FrameConstants& fc, uint32_t p)
     const float psx = next1(r);
     const float psy = next1(r);
     return make_float2(psx, psy);
+}
+
+// NEW_PATH (WavefrontPathTracing.hlsl:211-237) of the path of sample index p = image * W*H + y *
+// W + x: its rng after the pixel-sample and aperture draws and (RAY) its camera ray -- the same
+// arithmetic control_kernel runs for a claimed pixel, so the same bits. A virtual batch start
+// (kVirtualWord) runs it in the cast kernel (the ray) and in the path's first MATERIAL pass
+// (the rng) instead of writing and reading them back.
+template <bool RAY>
+DEV Rng new_path(const FrameConstants& fc, uint32_t p, V3* o, V3* d)
+{
+    const uint32_t W = fc.resolution[0], wh = W * fc.resolution[1];
+    const uint32_t image = p / wh, local = p - image * wh;
+    const uint32_t py = local / W, px = local - py * W;
+    Rng rng = rng_init(px, py, fc.frameSeed + image);
+    const float psx = next1(rng), psy = next1(rng);
+    const float a0 = next1(rng), a1 = next1(rng), a2 = next1(rng);
+    if (RAY) {
+        const float fsx = (psx + (float)px) / (float)fc.resolution[0];
+        const float fsy = (psy + (float)py) / (float)fc.resolution[1];
+        generate_ray(fc, fsx, fsy, a0, a1, a2, o, d);
+    }
+    return rng;
 }
 
 // Pixel of lane `lane` in claimed block `block` of the batch: image, then 8-row group,

@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     {
         QueueMapN<kFinShards> fm;
         qmap(prev, kQFinish, &fm);
-        const uint32_t nFin = fm.prefix[kFinShards];
+        const uint32_t nFin = drained(prev) ? 0u : fm.prefix[kFinShards];   // (drain_kernel completed them)
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nFin; i += gridDim.x * blockDim.x) {
             // the path's finish record and its shadow ray's result, both at its finish-queue
             // position (dense); only the pixel is per slot
@@ -222,6 +222,27 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     // pixel blocks of this shard: shard, shard + kShards, ...
     const uint32_t shardBlocks = g->totalBlocks > shard ? (g->totalBlocks - shard + kShards - 1) / kShards : 0u;
     const bool staticFill = g->staticFill != 0u;
+    if (staticFill && fc->virtualStart) {
+        // Virtual batch start: every slot is idle (the previous batch drained), wave j of the
+        // shard takes the shard's block j, and NEW_PATH is deferred -- the cast generates slot
+        // i's camera ray from its pixel (new_path<true>) and the path's first MATERIAL pass
+        // recomputes its rng (new_path<false>), so the only per-slot writes are the pixel (or
+        // kNoPixel: a hole in the virtual queue) and the busy flag. A 4K batch's start wrote
+        // 72 B per path here and read 64 of them back.
+        for (uint32_t base = blockIdx.x * blockDim.x; base < pool.size; base += gridDim.x * blockDim.x) {
+            const uint32_t tid = base + threadIdx.x;
+            const uint32_t vb = base / kControlBlock;
+            const uint32_t claimed = (vb / kShards) * (kControlBlock >> 6) + (threadIdx.x >> 6);
+            uint32_t pixel = kNoPixel, px = 0, py = 0, image = 0;
+            if (claimed < shardBlocks && block_pixel(*fc, film, shard + claimed * kShards, lane, &px, &py, &image)) {
+                pixel = image * (film.width * film.height) + py * film.width + px;
+                pool.flags[tid] = 0u;   // busy
+            }
+            pool.pixel[tid] = pixel;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) cnt->w[kVirtualWord * kShardStride] = pool.size;
+        return;
+    }
     if (!staticFill) {
         // (one read for the workgroup: the scan below holds barriers, so the exit must be uniform)
         __shared__ uint32_t exhausted;
@@ -294,6 +315,88 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     }
 }
 
+// MATERIAL's shading of one path at its hit (WavefrontPathTracing.hlsl:302-441): emission with
+// MIS, termination, next-event estimation (the shadow ray and its light sampling result), the
+// BSDF sample (the next extension ray), the new throughput, bsdfPdf (thr.w) and flags. `li` is
+// the path's Li after CONTROL's `Li += light sampling result`. Shared by material_kernel and
+// the drain kernel (drain_kernel), so both run the same arithmetic in the same order.
+template <uint32_t CAPS>
+__device__ __forceinline__ void shade_path(const DeviceScene& sc, const FrameConstants& fc, const HitRecord& hit, V3 dir, Rng& rng,
+                                           uint32_t& flags, float4& thr, const F3& li, V3& T, V3& L, V3& lsr, bool& terminate,
+                                           bool& hasShadow, V3& nO, V3& nD, float4& sO, V3& sD, float& extOpacity,
+                                           float& shadowOpacity)
+{
+    const uint32_t bounce = flags & 0xFFu;
+    const uint32_t features = fc.features;
+    const bool vndf = (features & DCRT_FEATURE_GGX_SAMPLE_VNDF) != 0;
+    const bool hasHit = hit.t != inf();
+    Intersection it;
+    it.lightIndex = DCRT_LIGHT_INDEX_INVALID; it.triangleIndex = 0;
+    it.geometryNormal = mk(0.0f, 0.0f, 0.0f);
+    if (hasHit) hit_to_intersection<CAPS>(sc, hit, it);
+    T = mk(thr.x, thr.y, thr.z);
+    L = mk(li.x, li.y, li.z);
+    // Evaluate light :331-349
+    {
+        const uint32_t lightIndex = hasHit ? it.lightIndex : fc.envLightIndex;
+        const bool visible = (features & DCRT_FEATURE_LIGHT_VISIBLE) != 0;
+        if (visible ? lightIndex != DCRT_LIGHT_INDEX_INVALID : (bounce > 0 && lightIndex != DCRT_LIGHT_INDEX_INVALID)) {
+            V3 radiance; float lightPdf;
+            evaluate_light<CAPS>(sc, lightIndex, it.triangleIndex, it.geometryNormal, dir, hit.t, fc.lightCount, &radiance, &lightPdf);
+            if (lightPdf > 0.0f) {
+                const float weight = !(flags & kFlagDelta) ? power_heuristic(thr.w, lightPdf) : 1.0f;
+                L = L + T * radiance * weight;
+            }
+        }
+    }
+    lsr = mk(0.0f, 0.0f, 0.0f);
+    if (bounce > fc.maxBounce || !hasHit) {
+        flags |= kFlagTerminate;
+        terminate = true;
+    } else {
+        const V3 wo = -dir;
+        const BsdfFrame bf = bsdf_frame(sc, wo, it);
+        if (fc.lightCount != 0) {
+            const LightSample ls = sample_light<CAPS>(sc, it.position, fc.lightCount, rng);
+            if (any_pos(ls.radiance) && ls.pdf > 0.0f) {
+                const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, bf, it);
+                const float NdotWI = fabsf(dot(it.normal, ls.wi));
+                const float bsdfPdf = evaluate_bsdf_pdf(sc, vndf, ls.wi, bf, it);
+                const float weight = ls.isDelta ? 1.0f : power_heuristic(ls.pdf, bsdfPdf);
+                lsr = T * ls.radiance * bsdf * NdotWI * weight / ls.pdf;
+                const V3 so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
+                sO = make_float4(so.x, so.y, so.z, ls.distance);   // (written into the shadow
+                sD = ls.wi;                                         //  queue after the append)
+                hasShadow = true;
+            }
+        }
+        float bsdfPdf = 0.0f;
+        bool isDelta = false;
+        {
+            const float sel = next1(rng);
+            const float sx = next1(rng), sy = next1(rng);
+            V3 wi, bsdf;
+            sample_bsdf(sc, vndf, bf, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
+            if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
+                const float NdotWI = fabsf(dot(it.normal, wi));
+                T = T * bsdf * NdotWI / bsdfPdf;
+                nO = offset_ray_origin(it.position, it.geometryNormal, wi);
+                nD = wi;   // (written into the extension queue after the append)
+                flags = (flags & 0xFFFFFF00u) | ((bounce + 1) & 0xFFu);
+            } else {
+                flags |= kFlagTerminate;
+                terminate = true;
+            }
+        }
+        thr.w = bsdfPdf;
+        flags = isDelta ? flags | kFlagDelta : flags & ~kFlagDelta;
+        if (features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430 (the caller stores them)
+            if (!terminate) extOpacity = next1(rng);
+            if (hasShadow) shadowOpacity = next1(rng);
+        }
+    }
+}
+
 // ---- MATERIAL -----------------------------------------------------------------------
 #ifndef DCRT_MATERIAL_BLOCK
 #define DCRT_MATERIAL_BLOCK 256
@@ -315,10 +418,13 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
                                                                              const Counters* prev, const SampleOut* sampleOut)
 {
     __shared__ uint32_t sm[96];
-    // the work list: the previous iteration's extension queue (its rays have been cast)
+    // the work list: the previous iteration's extension queue (its rays have been cast) -- or
+    // a batch start's virtual queue (item i = path slot i, kVirtualWord)
     QueueMap qm;
     qmap(prev, kQExt, &qm);
-    const uint32_t count = qm.prefix[kShards];
+    const uint32_t virt = virtual_items(prev);
+    // (a work list drain_kernel already completed holds nothing)
+    const uint32_t count = drained(prev) ? 0u : (virt ? virt : qm.prefix[kShards]);
     const uint32_t shard = blockIdx.x % kShards;
     const uint32_t fshard = blockIdx.x % kFinShards;
     DCRT_MCLK_INIT;
@@ -326,7 +432,12 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     uint32_t round = 0;   // grid-stride round: alternates block_append2's sm halves
     for (uint32_t base = blockIdx.x * blockDim.x; base < count; base += gridDim.x * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
-    const bool active = i < count;
+    bool active = i < count;
+    uint32_t newPixel = kNoPixel;   // a virtual item's pixel (a hole of the virtual queue has none)
+    if (virt && active) {
+        newPixel = slot(pool.pixel, i);
+        active = newPixel != kNoPixel;
+    }
     bool terminate = false, hasShadow = false, ends = false;
     uint32_t path = 0, pix = 0;
     float4 sample = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -345,24 +456,44 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         // Everything this pass reads is indexed by the item (no load waits for another):
         // the path's state record at its extension-queue position q, the cast's hit record
         // (with the ray's direction) at item i, the result of the path's last shadow ray at q
-        const uint32_t q = qpos(pool.recCap, qm, i);
-        const PathStateA& ps = state_at(pool.stateAPrev, q);
-        const PathStateB& psB = state_at(pool.stateBPrev, q);
+        // (only when it cast one: kFlagShadowPending)
         const float4 h4 = pool.hit[2 * i], hd = pool.hit[2 * i + 1];
-        const bool shadowHit = pool.shadowHitPrev[q] != 0u;
         HitRecord hit;
         hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = asu(hd.w);
         const V3 dir = mk(hd.x, hd.y, hd.z);
-        const uint4 r4 = ps.rng;
-        Rng rng; rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
-        const float4 l2 = ps.lsrMisc;
-        path = asu(l2.w);
-        uint32_t flags = asu(l2.z);
-        // a new path's first pass: NEW_PATH's constants, not the record's unwritten half
-        const bool first = (flags & kFlagFirst) != 0u;
-        flags &= ~kFlagFirst;
-        float4 thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : psB.thr;
-        const float4 l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : psB.liLsr;
+        Rng rng;
+        uint32_t flags;
+        float4 thr, l4, l2;
+        bool shadowHit = false;
+        if (virt) {
+            // a virtual batch start's path (slot i): NEW_PATH's state (:227-237) recomputed from
+            // its pixel -- the rng after the five camera draws, isDelta, bounce 0, T = 1,
+            // bsdfPdf = 0, Li = 0, no light sampling result
+            V3 unusedO, unusedD;
+            rng = new_path<false>(*fc, newPixel, &unusedO, &unusedD);
+            path = i;
+            flags = kFlagDelta;
+            thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+            l4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            l2 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        } else {
+            const uint32_t q = qpos(pool.recCap, qm, i);
+            const PathStateA& ps = state_at(pool.stateAPrev, q);
+            const PathStateB& psB = state_at(pool.stateBPrev, q);
+            const uint4 r4 = ps.rng;
+            rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
+            l2 = ps.lsrMisc;
+            path = asu(l2.w);
+            flags = asu(l2.z);
+            // a new path's first pass: NEW_PATH's constants, not the record's unwritten half
+            const bool first = (flags & kFlagFirst) != 0u;
+            thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : psB.thr;
+            l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : psB.liLsr;
+            // the last shadow ray's result exists only if the path cast one (a position nothing
+            // wrote this batch holds a stale value; its lsr is 0 then, but it is not read)
+            if (flags & kFlagShadowPending) shadowHit = pool.shadowHitPrev[q] != 0u;
+            flags &= ~(kFlagFirst | kFlagShadowPending);
+        }
         F3 li{l4.x, l4.y, l4.z};
         {
             // CONTROL's Li += light sampling result (:520-528), done here for live paths (a
@@ -377,79 +508,15 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         // live in VGPR pairs across the whole shading code
         uint32_t out = path;
         asm volatile("" : "+v"(out));
-        const uint32_t bounce = flags & 0xFFu;
-        const uint32_t features = fc->features;
-        const bool vndf = (features & DCRT_FEATURE_GGX_SAMPLE_VNDF) != 0;
-        const bool hasHit = hit.t != inf();
-        Intersection it;
-        it.lightIndex = DCRT_LIGHT_INDEX_INVALID; it.triangleIndex = 0;
-        it.geometryNormal = mk(0.0f, 0.0f, 0.0f);
+        float extOpacity = 0.0f, shadowOpacity = 0.0f;
+        V3 T, L, lsr;
         DCRT_MCLK(0);
-        if (hasHit) hit_to_intersection<CAPS>(sc, hit, it);
-        DCRT_MCLK(1);
-        V3 T = mk(thr.x, thr.y, thr.z);
-        V3 L = mk(li.x, li.y, li.z);
-        // Evaluate light :331-349
-        {
-            const uint32_t lightIndex = hasHit ? it.lightIndex : fc->envLightIndex;
-            const bool visible = (features & DCRT_FEATURE_LIGHT_VISIBLE) != 0;
-            if (visible ? lightIndex != DCRT_LIGHT_INDEX_INVALID : (bounce > 0 && lightIndex != DCRT_LIGHT_INDEX_INVALID)) {
-                V3 radiance; float lightPdf;
-                evaluate_light<CAPS>(sc, lightIndex, it.triangleIndex, it.geometryNormal, dir, hit.t, fc->lightCount, &radiance, &lightPdf);
-                if (lightPdf > 0.0f) {
-                    const float weight = !(flags & kFlagDelta) ? power_heuristic(thr.w, lightPdf) : 1.0f;
-                    L = L + T * radiance * weight;
-                }
-            }
-        }
-        DCRT_MCLK(2);
-        V3 lsr = mk(0.0f, 0.0f, 0.0f);
-        if (bounce > fc->maxBounce || !hasHit) {
-            flags |= kFlagTerminate;
-            terminate = true;
-        } else {
-            const V3 wo = -dir;
-            const BsdfFrame bf = bsdf_frame(sc, wo, it);
-            if (fc->lightCount != 0) {
-                const LightSample ls = sample_light<CAPS>(sc, it.position, fc->lightCount, rng);
-                if (any_pos(ls.radiance) && ls.pdf > 0.0f) {
-                    const V3 bsdf = evaluate_bsdf(sc, vndf, ls.wi, bf, it);
-                    const float NdotWI = fabsf(dot(it.normal, ls.wi));
-                    const float bsdfPdf = evaluate_bsdf_pdf(sc, vndf, ls.wi, bf, it);
-                    const float weight = ls.isDelta ? 1.0f : power_heuristic(ls.pdf, bsdfPdf);
-                    lsr = T * ls.radiance * bsdf * NdotWI * weight / ls.pdf;
-                    const V3 so = offset_ray_origin(it.position, it.geometryNormal, ls.wi);
-                    sO = make_float4(so.x, so.y, so.z, ls.distance);   // (written into the shadow
-                    sD = ls.wi;                                         //  queue after the append)
-                    hasShadow = true;
-                }
-            }
-            DCRT_MCLK(3);
-            float bsdfPdf = 0.0f;
-            bool isDelta = false;
-            {
-                const float sel = next1(rng);
-                const float sx = next1(rng), sy = next1(rng);
-                V3 wi, bsdf;
-                sample_bsdf(sc, vndf, bf, sx, sy, sel, it, &wi, &bsdf, &bsdfPdf, &isDelta);
-                if ((bsdf.x != 0.0f || bsdf.y != 0.0f || bsdf.z != 0.0f) && bsdfPdf != 0.0f) {
-                    const float NdotWI = fabsf(dot(it.normal, wi));
-                    T = T * bsdf * NdotWI / bsdfPdf;
-                    nO = offset_ray_origin(it.position, it.geometryNormal, wi);
-                    nD = wi;   // (written into the extension queue after the append)
-                    flags = (flags & 0xFFFFFF00u) | ((bounce + 1) & 0xFFu);
-                } else {
-                    flags |= kFlagTerminate;
-                    terminate = true;
-                }
-            }
-            DCRT_MCLK(4);
-            thr.w = bsdfPdf;
-            flags = isDelta ? flags | kFlagDelta : flags & ~kFlagDelta;
-            if (features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430
-                if (!terminate) slot(pool.extOpacity, out) = next1(rng);
-                if (hasShadow) slot(pool.shadowOpacity, out) = next1(rng);
-            }
+        shade_path<CAPS>(sc, *fc, hit, dir, rng, flags, thr, li, T, L, lsr, terminate, hasShadow, nO, nD, sO, sD,
+                         extOpacity, shadowOpacity);
+        DCRT_MCLK(4);
+        if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430
+            if (!terminate) slot(pool.extOpacity, out) = extOpacity;
+            if (hasShadow) slot(pool.shadowOpacity, out) = shadowOpacity;
         }
         ends = terminate && !hasShadow;
         // (the state written below goes to the queue positions the appends return)
@@ -498,7 +565,7 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         st.rng = sRng;
         stB.thr = make_float4(sT.x, sT.y, sT.z, sThr.w);
         stB.liLsr = make_float4(sL.x, sL.y, sL.z, sLsr.x);
-        st.lsrMisc = make_float4(sLsr.y, sLsr.z, asf(pathFlags), asf(path));
+        st.lsrMisc = make_float4(sLsr.y, sLsr.z, asf(pathFlags | (hasShadow ? kFlagShadowPending : 0u)), asf(path));
     }
     if (fin) {
         FinishRec& fr = pool.finRec[fPos];
@@ -584,6 +651,8 @@ __device__ uint32_t g_waveItems[2][16][8192];
 #endif
 
 
+constexpr uint32_t kNoItem = 0xFFFFFFFFu;   // a fetch's "no ray for this item"
+
 template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, bool PAIR = false,
           int LAYOUT = kLayoutScene, typename Lookup, typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
@@ -656,7 +725,8 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             if (free && k < end && idx < n) {
                 item = fetch(idx, lookup(idx), s);
                 if (!f2b) s.negMask = 0u;
-                ls = kRun;
+                // (kNoItem: the queue item has no ray -- a hole of a virtual batch start)
+                ls = item != kNoItem ? kRun : kIdle;
             }
             cursor += min(nNeed, end - cursor);
         }
@@ -789,8 +859,10 @@ __device__ __forceinline__ void end_iteration(const Counters* cnt, Counters* nex
         if (threadIdx.x == 0) {
             uint32_t fin = 0;
             for (uint32_t sh = 0; sh < kFinShards; ++sh) fin += qctr_load(cnt, kQFinish, sh);
-            const uint32_t ext = qtotal(cnt, kQExt);
-            g->extRays += ext;
+            // (a virtual batch start's items: its cast counted the rays, holes excluded)
+            const uint32_t virt = virtual_items(cnt);
+            const uint32_t ext = virt ? virt : qtotal(cnt, kQExt);
+            if (!virt) g->extRays += ext;
             g->shadowRays += shadowRays;
             g->iterations += 1ull;
             g->staticFill = 0u;   // only a batch's first CONTROL pass claims statically
@@ -802,7 +874,7 @@ __device__ __forceinline__ void end_iteration(const Counters* cnt, Counters* nex
             g->imageComplete = (idle && !g->stopped) ? 1u : 0u;
             g->prevLive = ext + fin;
         }
-        if (threadIdx.x < kCounterWords) nextCnt->w[threadIdx.x * kShardStride] = 0u;
+        if (threadIdx.x < kCounterWords + 2) nextCnt->w[threadIdx.x * kShardStride] = 0u;   // (with kVirtual/kDrainedWord)
     }
 }
 
@@ -854,9 +926,44 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     const float4* shRec = sgpr_ptr((const float4*)pool.shRec);
     TraversalStats st = {};
     TraversalStats stExt = {}, stShadow = {};
+    constexpr int kLayout = PAIR ? kLayoutPairs : (!INSTR || ALL_CACHED ? kLayoutFlat : kLayoutScene);
+    const uint32_t virt = !ALL_CACHED && !OPACITY ? virtual_items(cnt) : 0u;
+    if (!ALL_CACHED && !OPACITY && virt) {
+        // A virtual batch start (control_kernel): item i is path slot i; its camera ray is
+        // NEW_PATH's (new_path<true>) from the slot's pixel, its hit goes to item i. (The
+        // shadow queue is empty: the previous batch drained.) The rays traced are counted
+        // here -- the queue's holes are not rays.
+        const FrameConstants& f = *fc;
+        const uint32_t* pixels = sgpr_ptr((const uint32_t*)pool.pixel);
+        uint32_t rays = 0;
+        persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout>(
+            sc, virt, f.features, f.refillLanes, f.parkLanes, stackMem + threadIdx.x, block_shift(),
+            [&](uint32_t i) __attribute__((always_inline)) { return i; },
+            [&](uint32_t i, uint32_t v, TravState& s) __attribute__((always_inline)) {
+                const uint32_t p = slot(pixels, v);
+                if (p == kNoPixel) return kNoItem;
+                V3 o, d;
+                (void)new_path<true>(f, p, &o, &d);
+                trav_init(s, o, d, 0.0f, inf());
+                s.anyHit = false;
+                if (INSTR) st = TraversalStats{};
+                ++rays;
+                return i;
+            },
+            [&](uint32_t item, const TravState& s) __attribute__((always_inline)) {
+                emit_hit(pool, item, s);
+                if (INSTR) {
+                    stExt.nodes += st.nodes; stExt.tris += st.tris; stExt.blas += st.blas;
+                    stExt.maxNodes = max(stExt.maxNodes, st.nodes);
+                }
+            },
+            st, DCRT_WAVE_TAG(g));
+        const unsigned long long r = wave_sum(rays);
+        if ((threadIdx.x & 63u) == 0 && r) atomicAdd(&g->extRays, r);
+    } else {
     // (node order: the pair kernels run on pair-ordered scenes, the other non-counting ones on
     // PackBVH-ordered ones -- tracer.hip takes both from castPair -- the counting ones on either)
-    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, PAIR ? kLayoutPairs : (!INSTR || ALL_CACHED ? kLayoutFlat : kLayoutScene)>(
+    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
             // either kind: its record's position in its queue (no load)
@@ -892,6 +999,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
             }
         },
         st, DCRT_WAVE_TAG(g));
+    }
     if (INSTR) {
         flush_stats(stExt, instr);
         flush_stats(stShadow, instr + 3);
@@ -1061,6 +1169,132 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
     }
     const unsigned long long e = wave_sum((uint32_t)extRays), sh = wave_sum((uint32_t)shadowRays);
     if (lane == 0) { atomicAdd(&g->extRays, e); atomicAdd(&g->shadowRays, sh); }
+}
+
+// ---- drain completion ----------------------------------------------------------------------
+// Launched after every iteration's cast. Once a batch has no pixel block left to claim and
+// at most fc.drainPaths paths are live, it runs each of them to its end in one lane, as the
+// megakernel does, with the wavefront's arithmetic: the MATERIAL pass (shade_path) at the hit
+// the cast just wrote, then the shadow ray, then the next extension ray, and so on, and the
+// finish list's completion (CONTROL :520-528 + WriteSample) -- the same operations in the same
+// order per path, so the same bits as the remaining iterations. A batch's drain iterations
+// each took as long as their longest ray (a few thousand rays with 100-500 dependent node
+// visits on the spaceship scene, 3 launches each); here a path's remaining rays follow each
+// other in its lane and different paths overlap. The next iteration then finds the queues
+// empty (kDrainedWord) and the batch complete.
+template <uint32_t CAPS>
+__global__ __launch_bounds__(256) void drain_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fcp, Counters* cnt,
+                                                    Globals* g, const SampleOut* sampleOut)
+{
+    const FrameConstants& fc = *fcp;
+    if (!fc.drainPaths || g->stopped || virtual_items(cnt)) return;
+    QueueMap qe;
+    qmap(cnt, kQExt, &qe);
+    QueueMapN<kFinShards> fm;
+    qmap(cnt, kQFinish, &fm);
+    const uint32_t nExt = qe.prefix[kShards], nFin = fm.prefix[kFinShards];
+    if (nExt + nFin == 0u || nExt + nFin > fc.drainPaths) return;
+    for (uint32_t sh = 0; sh < kShards; ++sh) {   // a block still to claim: new paths will follow
+        const uint32_t blocks = g->totalBlocks > sh ? (g->totalBlocks - sh + kShards - 1) / kShards : 0u;
+        if (__hip_atomic_load(&g->nextBlock[sh * kShardStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < blocks) return;
+    }
+    extern __shared__ uint32_t stackMem[];
+    scene_cache_load(sc, stackMem, block_shift());
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        cnt->w[kDrainedWord * kShardStride] = 1u;   // the next MATERIAL / CONTROL pass: nothing to take
+        g->prevLive = 0u;                           // (so the next iteration completes the batch)
+    }
+    const bool watertight = (fc.features & DCRT_FEATURE_WATERTIGHT) != 0;
+    const bool f2b = (fc.features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
+    uint32_t* lds = stackMem + threadIdx.x;
+    const uint32_t shift = block_shift();
+    const SampleOut so = *sampleOut;
+    uint32_t extRays = 0, shadowRays = 0;
+    const uint32_t lanes = gridDim.x * blockDim.x;
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nExt + nFin; w += lanes) {
+        if (w >= nExt) {
+            // a path MATERIAL ended with its shadow ray pending (cast this iteration): CONTROL's
+            // completion, as control_kernel does it
+            const uint32_t f = qpos(pool.finCap, fm, w - nExt);
+            const FinishRec fr = pool.finRec[f];
+            const bool shadowHit = pool.finHit[f] != 0u;
+            const uint32_t path = asu(fr.lsrSlot.z);
+            F3 li{fr.liLsr.x, fr.liLsr.y, fr.liLsr.z};
+            const F3 lsr{fr.liLsr.w, fr.lsrSlot.x, fr.lsrSlot.y};
+            li.x = li.x + (!shadowHit ? lsr.x : 0.0f);
+            li.y = li.y + (!shadowHit ? lsr.y : 0.0f);
+            li.z = li.z + (!shadowHit ? lsr.z : 0.0f);
+            const uint32_t p = slot(pool.pixel, path);
+            sample_at(so.samplePosition, p) = pixel_sample(fc, p);
+            sample_at(so.sampleValue, p) = make_float4(li.x, li.y, li.z, 0.0f);
+            slot(pool.flags, path) = kFlagIdle;
+            continue;
+        }
+        // a continuing path: its state at its extension-queue position, the hit at its item
+        const uint32_t q = qpos(pool.recCap, qe, w);
+        const PathStateA ps = state_at(pool.stateA, q);
+        const float4 h4 = pool.hit[2 * w], hd = pool.hit[2 * w + 1];
+        HitRecord hit;
+        hit.t = h4.x; hit.u = h4.y; hit.v = h4.z; hit.tri = asu(h4.w); hit.inst = asu(hd.w);
+        V3 dir = mk(hd.x, hd.y, hd.z);
+        Rng rng;
+        rng.s0 = ps.rng.x; rng.s1 = ps.rng.y; rng.s2 = ps.rng.z; rng.s3 = ps.rng.w;
+        const uint32_t path = asu(ps.lsrMisc.w);
+        uint32_t flags = asu(ps.lsrMisc.z);
+        const bool first = (flags & kFlagFirst) != 0u;
+        float4 thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f), l4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (!first) {
+            const PathStateB psB = state_at(pool.stateB, q);
+            thr = psB.thr;
+            l4 = psB.liLsr;
+        }
+        bool shadowHit = (flags & kFlagShadowPending) ? pool.shadowHit[q] != 0u : false;
+        flags &= ~(kFlagFirst | kFlagShadowPending);
+        F3 li{l4.x, l4.y, l4.z};
+        V3 lsr0 = mk(l4.w, ps.lsrMisc.x, ps.lsrMisc.y);
+        for (;;) {
+            li.x = li.x + (!shadowHit ? lsr0.x : 0.0f);
+            li.y = li.y + (!shadowHit ? lsr0.y : 0.0f);
+            li.z = li.z + (!shadowHit ? lsr0.z : 0.0f);
+            bool terminate = false, hasShadow = false;
+            V3 T, L, lsr, nO = mk(0.0f, 0.0f, 0.0f), nD = nO, sD = nO;
+            float4 sO = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            float extOpacity = 0.0f, shadowOpacity = 0.0f;
+            shade_path<CAPS>(sc, fc, hit, dir, rng, flags, thr, li, T, L, lsr, terminate, hasShadow, nO, nD, sO, sD,
+                             extOpacity, shadowOpacity);
+            shadowHit = false;
+            if (hasShadow) {   // SHADOW_RAY_CAST
+                HitRecord sh;
+                shadowHit = trace_full<true, false>(sc, mk(sO.x, sO.y, sO.z), sD, sO.w, watertight, f2b, 0.0f, lds, shift, &sh);
+                ++shadowRays;
+            }
+            if (terminate) {
+                // MATERIAL's WriteSample (no shadow ray: L + 0) or CONTROL's (Li += lsr unless
+                // the shadow ray hit)
+                const uint32_t p = slot(pool.pixel, path);
+                sample_at(so.samplePosition, p) = pixel_sample(fc, p);
+                sample_at(so.sampleValue, p) = make_float4(L.x + (!shadowHit ? lsr.x : 0.0f), L.y + (!shadowHit ? lsr.y : 0.0f),
+                                                           L.z + (!shadowHit ? lsr.z : 0.0f), 0.0f);
+                if (so.debugRng) sample_at(so.debugRng, p) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
+                slot(pool.flags, path) = kFlagIdle;
+                break;
+            }
+            // EXTENSION_RAY_CAST of the next ray; the next MATERIAL pass's inputs
+            if (!trace_full<false, false>(sc, nO, nD, inf(), watertight, f2b, 0.0f, lds, shift, &hit)) {
+                hit.t = inf(); hit.u = 0.0f; hit.v = 0.0f; hit.tri = 0u; hit.inst = 0u;
+            }
+            ++extRays;
+            dir = nD;
+            thr = make_float4(T.x, T.y, T.z, thr.w);
+            li = F3{L.x, L.y, L.z};
+            lsr0 = lsr;
+        }
+    }
+    const unsigned long long e = wave_sum(extRays), sr = wave_sum(shadowRays);
+    if ((threadIdx.x & 63u) == 0) {
+        if (e) atomicAdd(&g->extRays, e);
+        if (sr) atomicAdd(&g->shadowRays, sr);
+    }
 }
 
 // ---- kernel-level batch entry points (tests / roofline) -----------------------------------

@@ -131,14 +131,21 @@ bool RequiredTraversalStack(const dcrt_flat_scene& s, uint32_t* out)
     *out = 0;
     if (n == 0) return true;
     std::vector<uint32_t> blasDepth(n, UINT32_MAX);   // memo: deepest path below a BLAS root
+    // every node is reached at most once per walk: a tree. A node reached twice (a child
+    // shared between parents, a cycle) is malformed -- and would make the walk exponential
+    std::vector<uint32_t> seen(n, UINT32_MAX);        // the walk that last reached the node
+    uint32_t walkId = 0;
     struct Item { uint32_t node, depth; };
     std::vector<Item> todo;
     auto walk = [&](uint32_t root, bool tlas, uint32_t* deepest) {
+        ++walkId;
         todo.assign(1, { root, 0u });
         *deepest = 0;
         while (!todo.empty()) {
             const Item it = todo.back();
             todo.pop_back();
+            if (seen[it.node] == walkId) return false;
+            seen[it.node] = walkId;
             const dcrt_bvh_node& nd = s.bvh_nodes[it.node];
             if (nd.misc >= 4u) {   // a leaf
                 uint32_t d = it.depth;
@@ -271,6 +278,7 @@ struct dcrt_tracer {
     bool castAllCached = false;        // the scene fits the LDS cache: cast_kernel<., ., true, .>
     bool castPair = false;             // trav_visit_pair: the scene outgrows an XCD's L2 (UploadScene)
     bool mergedCasts = true;           // one cast_kernel per iteration (DCRT_SPLIT_CASTS=1: EXT then SHADOW)
+    bool virtualStart = true;          // virtual batch starts where the cast kernel has them (DCRT_VIRTUAL_START=0: off)
     uint32_t sceneCaps = kCapAll;      // what the uploaded scene uses (kCap* of dscene.h)
     uint32_t materialCaps = kCapAll;   // the MATERIAL variant launched for it
 
@@ -378,6 +386,8 @@ struct dcrt_tracer {
     uint32_t castResident = 0;         // persistent cast grid: resident workgroups on the whole chip
     uint32_t castResidentOpacity = 0;  // the same for the ALLOW_ANYHIT_SHADER variant
     uint32_t megaResident = 0;         // persistent megakernel grid
+    uint32_t drainResident = 0;        // drain_kernel grid (resident workgroups)
+    uint32_t drainPaths = 32768;       // drain_kernel threshold (DCRT_DRAIN_PATHS; 0: no drain launches)
     int mode = 0;                      // 0 wavefront (WavefrontPathTracer), 1 megakernel (MegakernelPathTracer)
     uint32_t CastGrid(uint32_t block, bool opacity) const
     {
@@ -427,6 +437,8 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
     iterationsPerRender = cfg.iterations_per_render ? cfg.iterations_per_render : kDefaultIterations;
     debugRng = cfg.debug_rng != 0;
     if (const char* split = std::getenv("DCRT_SPLIT_CASTS")) mergedCasts = std::atoi(split) == 0;
+    if (const char* vs = std::getenv("DCRT_VIRTUAL_START")) virtualStart = std::atoi(vs) != 0;
+    if (const char* dp = std::getenv("DCRT_DRAIN_PATHS")) drainPaths = (uint32_t)std::max(0, std::atoi(dp));
     if (const char* tune = std::getenv("DCRT_TRAVERSAL_TUNE")) {
         unsigned r = 0, p = 0;
         if (std::sscanf(tune, "%u,%u", &r, &p) == 2 && r >= 1 && r <= 64 && p >= 1 && p <= 64) {
@@ -435,9 +447,10 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
             tuneOverride = true;
         }
     }
-    // pool arrays and queue records are addressed through 32-bit byte offsets (slot(),
-    // ext_rec()): an extension-queue parity holds up to 2 records of 32 B per slot, which
-    // bounds the pool at 2^26 slots (the state records, 64 B, use 64-bit offsets)
+    // pool arrays are addressed through 32-bit byte offsets (slot(): at most 16 B per slot), and
+    // one parity's extension-ray records and path-state halves (ext_rec(), state_at(): 32 B at
+    // position q = shard * recCap + entry) as well; this check bounds the pool at 2^26 slots,
+    // the recCap check below keeps recCap * kShards * 32 B within 4 GiB
     if ((uint64_t)poolSize * 64u > (1ull << 32)) {
         SetLastError("path pool too large: at most 2^26 slots (32-bit pool offsets)");
         return DCRT_E_LIMIT;
@@ -710,7 +723,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false, false, false>, (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, extension_kernel<false, false>, (int)castBlock, castLds));
         const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
-        const size_t budget = castLds < perBlock ? perBlock - castLds : 0;
+        size_t budget = castLds < perBlock ? perBlock - castLds : 0;
         uint32_t nodeCount = s.bvh_node_count;
         d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
         d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
@@ -730,6 +743,11 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         // other non-counting cast kernels assume PackBVH's)
         std::vector<dcrt_bvh_node> pairNodes;
         if (castPair) {
+            // (the budget from the occupancy of the pair kernel, the one that launches)
+            int pairPerCU = 0;
+            HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pairPerCU, CastKernel(false, false, false, true), (int)castBlock, castLds));
+            const size_t pairBlock = ((size_t)163840 / (size_t)std::max(1, pairPerCU)) & ~(size_t)15;
+            budget = castLds < pairBlock ? pairBlock - castLds : 0;
             uint32_t topNodes = 4096;
             if (const char* e = std::getenv("DCRT_TOP_NODES")) topNodes = (uint32_t)std::atoi(e);   // A/B experiments
             if (!PairLayout(s, topNodes, &pairNodes)) { SetLastError("malformed BVH: a node with two parents"); return DCRT_E_INVALID_ARG; }
@@ -767,6 +785,10 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         int megaPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel<false>, (int)castBlock, castLds));
         megaResident = (uint32_t)std::max(1, megaPerCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        int drainPerCU = 0;
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&drainPerCU, materialCaps == kCapOpaqueDelta ? drain_kernel<kCapOpaqueDelta> : drain_kernel<kCapAll>,
+                                                              (int)castBlock, castLds));
+        drainResident = (uint32_t)std::max(1, drainPerCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
     }
     HIPCHECK(hipStreamSynchronize(stream));
     hasScene = true;
@@ -943,6 +965,12 @@ int dcrt_tracer::BeginImage()
 #endif
     fc.refillLanes = tuneOverride || castAllCached ? refillLanes : DCRT_REFILL_GLOBAL;
     fc.parkLanes = parkLanes;
+    // virtual batch starts (control_kernel): the merged cast kernels of scenes outside the LDS
+    // cache carry the camera-ray fetch; not with ALLOW_ANYHIT_SHADER (NEW_PATH's opacity draw)
+    fc.virtualStart = virtualStart && mergedCasts && !castAllCached && !(frame.features & DCRT_FEATURE_ALLOW_ANYHIT) ? 1u : 0u;
+    // drain completion (drain_kernel): not with ALLOW_ANYHIT_SHADER, and not while the cast
+    // kernels are instrumented (the roofline leg's counts and launch times are the wavefront's)
+    fc.drainPaths = !(frame.features & DCRT_FEATURE_ALLOW_ANYHIT) && !instrCounters && !extTiming ? drainPaths : 0u;
     hipLaunchKernelGGL(set_frame_kernel, dim3(1), dim3(1), 0, stream, dFrame, fc);
     const uint32_t total = fc.blocksPerImage;
     const uint32_t idleThreads = std::max<uint32_t>(poolSize, 2u * (uint32_t)(sizeof(Counters) / 4));
@@ -1003,6 +1031,12 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
                               (const FrameConstants*)dFrame, (const Counters*)cnt, dGlobals, dInstr);
         hipLaunchKernelGGL(shadow, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
                            next, dGlobals, dInstr);
+    }
+    if (drainPaths) {
+        // (returns at once unless the batch's last paths are few enough: fc.drainPaths)
+        auto drain = materialCaps == kCapOpaqueDelta ? drain_kernel<kCapOpaqueDelta> : drain_kernel<kCapAll>;
+        hipLaunchKernelGGL(drain, dim3(drainResident), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
+                           dGlobals, (const SampleOut*)dSampleOut);
     }
     if (sequenced) {
         hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,

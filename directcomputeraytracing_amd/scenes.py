@@ -298,18 +298,32 @@ def hull_mesh(nu: int, nv: int, seed: int = 1234):
 
 
 def write_spaceship(directory: Path | str, width: int = 3840, height: int = 2160, nu: int = 512, nv: int = 256,
-                    ships: int = 8, seed: int = 1234) -> Path:
+                    ships: int = 8, seed: int = 1234, framing: str = "wide") -> Path:
     """Config 4: one procedural hull mesh (2*nu*(nv-1) triangles) instanced `ships` times
-    through repeated <shape type="obj"> with the same filename; engine glows are area lights."""
+    through repeated <shape type="obj"> with the same filename; engine glows are area lights.
+
+    framing "wide" (the configs[3] scene since round 1): ships scattered over a deep field,
+    about 10 % of the camera rays hit a hull. "close": a fleet in formation filling the frame
+    (broadside hulls in rows, staggered in depth) -- most camera rays hit a hull and most paths
+    bounce between hulls, a two-level-BVH traversal workload rather than a sky one."""
     d = Path(directory)
     d.mkdir(parents=True, exist_ok=True)
     write_obj(d / f"hull_{nu}x{nv}.obj", *hull_mesh(nu, nv, seed))
     rng = np.random.default_rng(seed)
     shapes = []
+    if framing not in ("wide", "close"):
+        raise ValueError(f"unknown spaceship framing {framing!r}")
     for k in range(ships):
-        pos = (float(rng.uniform(-4, 4)), float(rng.uniform(-1.5, 1.5)), float(rng.uniform(2, 14)))
-        yaw = float(rng.uniform(-60, 60))
-        pitch = float(rng.uniform(-15, 15))
+        if framing == "close":
+            col, row = k % 2, k // 2
+            pos = (float(-1.45 + 2.9 * col + rng.uniform(-0.2, 0.2)), float(-1.05 + 0.7 * row + rng.uniform(-0.05, 0.05)),
+                   float(3.2 + 0.9 * ((row + col) % 3) + rng.uniform(0.0, 0.3)))
+            yaw = float(90.0 + rng.uniform(-12, 12))
+            pitch = float(rng.uniform(-6, 6))
+        else:
+            pos = (float(rng.uniform(-4, 4)), float(rng.uniform(-1.5, 1.5)), float(rng.uniform(2, 14)))
+            yaw = float(rng.uniform(-60, 60))
+            pitch = float(rng.uniform(-15, 15))
         shapes.append(f'  <shape type="obj" id="shape_ship{k}"><string name="filename" value="hull_{nu}x{nv}.obj"/><ref id="hullmetal"/>'
                       f'<transform name="to_world"><matrix value="{mitsuba_matrix(pos, yaw=yaw, pitch=pitch)}"/></transform></shape>\n')
         # engine glow at the stern (local z = -2.02), facing backwards
@@ -317,9 +331,10 @@ def write_spaceship(directory: Path | str, width: int = 3840, height: int = 2160
         back = (pos[0] - 2.02 * math.sin(yr), pos[1], pos[2] - 2.02 * math.cos(yr))
         shapes.append(f'  <shape type="rectangle" id="shape_engine{k}"><emitter type="area"><rgb name="radiance" value="4, 6, 12"/></emitter>'
                       f'<transform name="to_world"><matrix value="{mitsuba_matrix(back, yaw=yaw + 180, scale=(0.15, 0.1, 1))}"/></transform></shape>\n')
+    camera = mitsuba_matrix((0, 0.5, -6), pitch=3) if framing == "wide" else mitsuba_matrix((0, 0.0, -1.2), pitch=0)
     body = (
         '  <integrator type="path"><integer name="max_depth" value="8"/></integrator>\n'
-        + _sensor("perspective", width, height, mitsuba_matrix((0, 0.5, -6), pitch=3), '    <float name="fov" value="55"/>\n',
+        + _sensor("perspective", width, height, camera, '    <float name="fov" value="55"/>\n',
                   '<rfilter type="box"><float name="radius" value="1"/></rfilter>')
         + '  <bsdf type="roughconductor" id="hullmetal"><rgb name="eta" value="1.657, 0.880, 0.521"/>'
           '<rgb name="k" value="9.224, 6.270, 4.837"/><float name="alpha" value="0.09"/></bsdf>\n'
@@ -327,7 +342,7 @@ def write_spaceship(directory: Path | str, width: int = 3840, height: int = 2160
         + '  <emitter type="constant"><rgb name="radiance" value="0.02, 0.03, 0.06"/></emitter>\n'
           '  <emitter type="directional"><vector name="direction" value="-0.4, -0.5, 0.75"/><rgb name="irradiance" value="3, 2.9, 2.7"/></emitter>\n'
     )
-    p = d / f"spaceship_{nu}x{nv}.xml"
+    p = d / (f"spaceship_{nu}x{nv}.xml" if framing == "wide" else f"spaceship_close_{nu}x{nv}.xml")
     p.write_text(_xml(body))
     return p
 
@@ -416,7 +431,7 @@ def write_anyhit(directory: Path | str, width: int = 64, height: int = 48) -> Pa
     return p
 
 
-CONFIGS = ("cornell", "coffee", "spaceship", "lamp")
+CONFIGS = ("cornell", "coffee", "spaceship", "lamp", "spaceship_close")
 
 
 def setup_config(scene, name: str, scene_dir: Path | str, small: bool = False, multiscattering: bool = True) -> str:
@@ -438,10 +453,12 @@ def setup_config(scene, name: str, scene_dir: Path | str, small: bool = False, m
         ms = scene.enable_multiscattering() if multiscattering else []
         return ("coffee-like Mitsuba XML 1920x1080, env cube + constant, max_depth 8, Kulla-Conty multiscattering "
                 + (f"on ({len(ms)} materials)" if ms else "off") + " (configs[2])")
-    if name == "spaceship":
+    if name in ("spaceship", "spaceship_close"):
         nu, nv = (64, 32) if small else (512, 256)
-        scene.load_from_file(write_spaceship(d, 3840, 2160, nu=nu, nv=nv, ships=8))
-        return f"spaceship-like Mitsuba XML 3840x2160, {2 * nu * (nv - 1)} tris x 8 instances (configs[3])"
+        framing = "close" if name == "spaceship_close" else "wide"
+        scene.load_from_file(write_spaceship(d, 3840, 2160, nu=nu, nv=nv, ships=8, framing=framing))
+        return (f"spaceship-like Mitsuba XML 3840x2160, {2 * nu * (nv - 1)} tris x 8 instances, {framing} framing"
+                + (" (fleet filling the frame: a traversal workload)" if framing == "close" else "") + " (configs[3])")
     if name == "lamp":
         scene.load_from_file(write_lamp(d, 3840, 2160, segments=48 if small else 96))
         return "lamp-like Mitsuba XML 3840x2160, thin lens, triangle emitters (configs[4])"

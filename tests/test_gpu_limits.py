@@ -93,3 +93,40 @@ def test_upload_refuses_short_traversal_stack(native_lib, golden_luts):
         assert lib.dcrt_tracer_upload_scene(t._h, C.byref(f)) == 0     # the exact requirement is accepted
     finally:
         t.destroy()
+
+
+def test_upload_refuses_shared_child_dag(native_lib, golden_luts):
+    """A node array in which interior nodes share their children (a DAG with 2^40 root-to-leaf
+    paths) is refused at once as malformed (RequiredTraversalStack keeps a visited set: without
+    it the walk was exponential)."""
+    import ctypes as C
+    import time
+    from directcomputeraytracing_amd import WavefrontPathTracer, _abi
+    s = cornell(16, 16, 2)
+    f = s.flat()
+    n = 41
+    nodes = np.zeros((n, 8), np.uint32)
+    box = np.array([-10, -10, -10, 10, 10, 10], np.float32).view(np.uint32)
+    for i in range(n):
+        nodes[i, :6] = box
+        if i + 1 < n:
+            nodes[i, 6] = i + 1            # right child = left child = node + 1
+            nodes[i, 7] = 0                # interior, split axis 0
+        else:
+            nodes[i, 6] = 0                # a BLAS leaf: triangle 0, one primitive
+            nodes[i, 7] = 1 << 3
+    g = _abi.FlatScene()
+    C.pointer(g)[0] = f
+    g.bvh_nodes = nodes.ctypes.data_as(C.POINTER(_abi.BVHNode))
+    g.bvh_node_count = n
+    g.tlas_node_count = 0
+    g.bvh_traversal_stack_size = 64
+    lib = _abi.load_library()
+    t = WavefrontPathTracer(path_pool_size=1 << 12)
+    try:
+        t0 = time.perf_counter()
+        rc = lib.dcrt_tracer_upload_scene(t._h, C.byref(g))
+        assert rc == -1 and b"malformed" in lib.dcrt_last_error()
+        assert time.perf_counter() - t0 < 5.0
+    finally:
+        t.destroy()

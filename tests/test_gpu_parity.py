@@ -321,6 +321,57 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
         assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
 
+@pytest.mark.parametrize("cache,scene_name,pool", [("global", "cornell", 1 << 15), ("pair", "cornell", 1 << 12),
+                                                   ("global", "xml_mix", 1 << 14), ("pair", "xml_mix", 3000)])
+def test_virtual_batch_start_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, cache, scene_name, pool):
+    """Virtual batch starts (control_kernel: the cast generates the camera rays of a batch's
+    statically claimed slots, the first MATERIAL pass recomputes NEW_PATH's rng) on the
+    global-memory and pair cast kernels, with drain completion (drain_kernel): a ragged film
+    (holes in the virtual queue), several batches, pools smaller than a batch (the rest of the
+    blocks claimed later), against the oracle (samples, RNG state, film, ray counts) and
+    against DCRT_VIRTUAL_START=0 DCRT_DRAIN_PATHS=0."""
+    from conftest import GOLDEN
+    from directcomputeraytracing_amd import FILTER_BOX, FilterParams, Scene, WavefrontPathTracer
+    monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+    monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1" if cache == "pair" else "0")
+    if scene_name == "cornell":
+        s = cornell(133, 77, 6)
+    else:
+        s = Scene((45, 29))
+        s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
+    W, H = s.resolution
+    filt = FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3)
+    runs = {}
+    # virtual start + drain completion (every path of a batch completed in drain_kernel once at
+    # most 400 remain) against neither
+    for virtual, drain in (("1", "400"), ("0", "0")):
+        monkeypatch.setenv("DCRT_VIRTUAL_START", virtual)
+        monkeypatch.setenv("DCRT_DRAIN_PATHS", drain)
+        t = WavefrontPathTracer(path_pool_size=pool, debug_rng=True)
+        try:
+            t.set_luts(golden_luts)
+            t.on_scene_loaded(s)
+            t.set_image_batch(2)
+            t.clear_film()
+            t.render_images(3, 5, filt)
+            runs[virtual] = (t.read_film(), t.read_samples(), t.read_rng(), t.counters())
+        finally:
+            t.destroy()
+    film, (pos, val), rng, c = runs["1"]
+    flat = oracle_mod.flat_with_own_bvh(s)
+    ref = np.zeros_like(film)
+    ext = shadow = 0
+    for seed in range(3, 8):
+        p, v, r, cr = oracle_mod.render(flat, golden_luts, oracle_mod.frame_params(s, seed), oracle_mod.WAVEFRONT, rng=True)
+        oracle_mod.sample_convolution(filt, p, v, ref)
+        ext += cr["extension_rays"]
+        shadow += cr["shadow_rays"]
+    assert np.array_equal(rng, r) and same_bits(pos, p).all() and same_bits(val, v).all()   # the last image
+    assert same_bits(film, ref).all()
+    assert c["extension_rays"] == ext and c["shadow_rays"] == shadow and c["new_paths"] == 5 * W * H
+    assert same_bits(runs["0"][0], film).all() and runs["0"][3]["extension_rays"] == ext
+
+
 def test_concurrent_stream_partitions_sum_to_single_film(native_lib, golden_luts):
     """bench --streams 2: two tracers on one GPU render their bands concurrently (two host
     threads, two streams); add_film_device of one film into the other == 1-tracer film."""
@@ -508,12 +559,14 @@ def test_config_scenes_bit_exact(gpu_tracer, golden_luts, oracle_mod, name, cube
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 1]))
 
 
-def test_full_size_spaceship_mesh_bit_exact(gpu_tracer, golden_luts, oracle_mod, tmp_path):
+@pytest.mark.parametrize("framing", ["wide", "close"])
+def test_full_size_spaceship_mesh_bit_exact(gpu_tracer, golden_luts, oracle_mod, tmp_path, framing):
     """configs[3] at its full mesh size (261 120 triangles x 8 instances, 522 k BVH nodes,
-    stack depth 30: most nodes outside the LDS scene cache), 320x180, 8 bounces, 1 spp."""
+    stack depth 30: most nodes outside the LDS scene cache), 320x180, 8 bounces, 1 spp; both
+    framings (the close one: hulls fill the frame, paths bounce between them)."""
     from directcomputeraytracing_amd import Scene, scenes
     s = Scene((320, 180))
-    s.load_from_file(scenes.write_spaceship(tmp_path, 320, 180, nu=512, nv=256, ships=8))
+    s.load_from_file(scenes.write_spaceship(tmp_path, 320, 180, nu=512, nv=256, ships=8, framing=framing))
     assert s.bvh_info()["total_nodes"] > 500_000
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [3]))
     assert gpu_tracer.info()["pair_traversal"] == 1   # (beyond an XCD's L2: trav_visit_pair)

@@ -4,7 +4,7 @@ BASELINE.json config that fits one GPU (configs[1..4]; the multi-GPU film split 
 configs 4/5 is exercised by bench.py --gpus N). Scenes are generated procedurally
 (deterministic) into --scene-dir. Prints one JSON line per config.
 
-  python tools/bench_configs.py [--spp K] [--configs cornell,coffee,spaceship,lamp]
+  python tools/bench_configs.py [--spp K] [--configs cornell,coffee,spaceship,spaceship_close,lamp]
 """
 from __future__ import annotations
 
@@ -105,7 +105,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spp", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--configs", default="cornell,coffee,spaceship,lamp")
+    ap.add_argument("--configs", default="cornell,coffee,spaceship,spaceship_close,lamp")
     ap.add_argument("--scene-dir", default="/tmp/dcrt_scenes")
     ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines (bench.py --streams)")
     ap.add_argument("--pool", type=int, default=0, help="path pool slots (0: 2^24 at 1080p, 2^26 at 4K)")
