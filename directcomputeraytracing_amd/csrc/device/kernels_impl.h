@@ -927,9 +927,10 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     TraversalStats st = {};
     TraversalStats stExt = {}, stShadow = {};
     constexpr int kLayout = PAIR ? kLayoutPairs : (!INSTR || ALL_CACHED ? kLayoutFlat : kLayoutScene);
-    const uint32_t virt = !ALL_CACHED && !OPACITY ? virtual_items(cnt) : 0u;
-    if (!ALL_CACHED && !OPACITY && virt) {
+    const uint32_t virt = !OPACITY ? virtual_items(cnt) : 0u;
+    if (!OPACITY && virt) {
         // A virtual batch start (control_kernel): item i is path slot i; its camera ray is
+        // (the branch costs no registers: 74 / 72 / 77 VGPRs as without it, tools/vgprs.sh)
         // NEW_PATH's (new_path<true>) from the slot's pixel, its hit goes to item i. (The
         // shadow queue is empty: the previous batch drained.) The rays traced are counted
         // here -- the queue's holes are not rays.

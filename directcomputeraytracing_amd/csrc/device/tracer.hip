@@ -387,7 +387,7 @@ struct dcrt_tracer {
     uint32_t castResidentOpacity = 0;  // the same for the ALLOW_ANYHIT_SHADER variant
     uint32_t megaResident = 0;         // persistent megakernel grid
     uint32_t drainResident = 0;        // drain_kernel grid (resident workgroups)
-    uint32_t drainPaths = 32768;       // drain_kernel threshold (DCRT_DRAIN_PATHS; 0: no drain launches)
+    uint32_t drainPaths = 0;           // drain_kernel threshold (DCRT_DRAIN_PATHS; 0: no drain launches -- the default: profiles/r04_ab_virtual_drain.txt)
     int mode = 0;                      // 0 wavefront (WavefrontPathTracer), 1 megakernel (MegakernelPathTracer)
     uint32_t CastGrid(uint32_t block, bool opacity) const
     {
@@ -965,9 +965,9 @@ int dcrt_tracer::BeginImage()
 #endif
     fc.refillLanes = tuneOverride || castAllCached ? refillLanes : DCRT_REFILL_GLOBAL;
     fc.parkLanes = parkLanes;
-    // virtual batch starts (control_kernel): the merged cast kernels of scenes outside the LDS
-    // cache carry the camera-ray fetch; not with ALLOW_ANYHIT_SHADER (NEW_PATH's opacity draw)
-    fc.virtualStart = virtualStart && mergedCasts && !castAllCached && !(frame.features & DCRT_FEATURE_ALLOW_ANYHIT) ? 1u : 0u;
+    // virtual batch starts (control_kernel): the merged cast kernels carry the camera-ray fetch;
+    // not with ALLOW_ANYHIT_SHADER (NEW_PATH's opacity draw)
+    fc.virtualStart = virtualStart && mergedCasts && !(frame.features & DCRT_FEATURE_ALLOW_ANYHIT) ? 1u : 0u;
     // drain completion (drain_kernel): not with ALLOW_ANYHIT_SHADER, and not while the cast
     // kernels are instrumented (the roofline leg's counts and launch times are the wavefront's)
     fc.drainPaths = !(frame.features & DCRT_FEATURE_ALLOW_ANYHIT) && !instrCounters && !extTiming ? drainPaths : 0u;

@@ -321,8 +321,9 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
         assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
 
-@pytest.mark.parametrize("cache,scene_name,pool", [("global", "cornell", 1 << 15), ("pair", "cornell", 1 << 12),
-                                                   ("global", "xml_mix", 1 << 14), ("pair", "xml_mix", 3000)])
+@pytest.mark.parametrize("cache,scene_name,pool", [("lds", "cornell", 1 << 15), ("global", "cornell", 1 << 15),
+                                                   ("pair", "cornell", 1 << 12), ("global", "xml_mix", 1 << 14),
+                                                   ("pair", "xml_mix", 3000)])
 def test_virtual_batch_start_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, cache, scene_name, pool):
     """Virtual batch starts (control_kernel: the cast generates the camera rays of a batch's
     statically claimed slots, the first MATERIAL pass recomputes NEW_PATH's rng) on the
@@ -332,7 +333,7 @@ def test_virtual_batch_start_bit_exact(native_lib, golden_luts, oracle_mod, monk
     against DCRT_VIRTUAL_START=0 DCRT_DRAIN_PATHS=0."""
     from conftest import GOLDEN
     from directcomputeraytracing_amd import FILTER_BOX, FilterParams, Scene, WavefrontPathTracer
-    monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+    monkeypatch.setenv("DCRT_NO_LDS_CACHE", "0" if cache == "lds" else "1")
     monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1" if cache == "pair" else "0")
     if scene_name == "cornell":
         s = cornell(133, 77, 6)
