@@ -1039,9 +1039,9 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
                            dGlobals, (const SampleOut*)dSampleOut);
     }
     if (sequenced) {
-        hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
-                           (const Globals*)dGlobals);
-        hipLaunchKernelGGL(advance_image_kernel, dim3(1), dim3(64), 0, stream, dFrame, dGlobals);
+        // (the film pass of a completed batch; its last workgroup advances to the next batch)
+        hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u, dGlobals,
+                           dFrame);
     }
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
@@ -1152,7 +1152,7 @@ int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
     if (!film.accum) { SetLastError("no film"); return DCRT_E_INVALID_ARG; }
     CHECKED(UploadFilter(f));
     hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
-                       (const Globals*)nullptr);
+                       (Globals*)nullptr, (FrameConstants*)nullptr);
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
 }
@@ -1185,7 +1185,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
             hipExtLaunchKernelGGL(mk, dim3(megaResident), dim3(castBlock), castLds, stream, e0, e1, 0, scene,
                                   (const FrameConstants*)dFrame, film, dGlobals, (uint32_t)(film.debugRng != nullptr));
             hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
-                               (const Globals*)nullptr);
+                               (Globals*)nullptr, (FrameConstants*)nullptr);
             HIPCHECK(hipGetLastError());
         }
         HIPCHECK(hipStreamSynchronize(stream));
