@@ -218,6 +218,7 @@ SIGNATURES = [
     ("dcrt_obj_material_count", _I, [_P, C.POINTER(C.c_uint32)]),
     ("dcrt_obj_get_material", _I, [_P, _U, C.POINTER(ObjMaterial)]),
     ("dcrt_obj_free", None, [_P]),
+    ("dcrt_xml_dump_tree", _I, [C.c_char_p, C.c_char_p, _U, C.POINTER(C.c_uint32)]),
     ("dcrt_tracer_create", _I, [C.POINTER(TracerConfig), C.POINTER(_P)]),
     ("dcrt_tracer_destroy", None, [_P]),
     ("dcrt_tracer_upload_scene", _I, [_P, C.POINTER(FlatScene)]),

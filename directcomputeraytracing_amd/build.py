@@ -150,6 +150,10 @@ def build_reference_checkers() -> Path | None:
         return None
     subprocess.run(["make", "-s", "-C", str(ORACLE_DIR / "ref_obj"), f"REF={REFERENCE}"], check=True,
                    stdout=subprocess.DEVNULL)
+    # ... and its vendored RapidXml for tests/test_xml_pin.py (oracle/ref_xml/Makefile)
+    if (REFERENCE / "RapidXml" / "rapidxml.hpp").exists():
+        subprocess.run(["make", "-s", "-C", str(ORACLE_DIR / "ref_xml"), f"REF={REFERENCE}"], check=True,
+                       stdout=subprocess.DEVNULL)
     return ORACLE_DIR / "_ref" / "librefobj.so"
 
 

@@ -1,4 +1,5 @@
 // capi_scene.cpp -- extern "C" surface of the host scene (include/dcrt.h).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -504,6 +505,21 @@ DCRT_API int dcrt_obj_get_material(const dcrt_obj_meshes* m, uint32_t index, dcr
 }
 
 DCRT_API void dcrt_obj_free(dcrt_obj_meshes* m) { delete m; }
+
+DCRT_API int dcrt_xml_dump_tree(const char* path, char* out, uint32_t capacity, uint32_t* out_length)
+{
+    if (!path || !out_length) return DCRT_E_INVALID_ARG;
+    DCRT_GUARD_BEGIN
+    std::string dump;
+    if (!dcrt::DumpXmlTree(path, &dump)) return DCRT_E_IO;
+    *out_length = (uint32_t)dump.size();
+    if (out && capacity) {
+        const size_t n = std::min<size_t>(dump.size(), capacity);
+        std::memcpy(out, dump.data(), n);
+    }
+    return dump.size() <= capacity ? DCRT_OK : DCRT_E_LIMIT;
+    DCRT_GUARD_END
+}
 
 }  // extern "C"
 

@@ -154,6 +154,8 @@ private:
     std::vector<dcrt_texture> flatTextures_;
     uint32_t tlasNodeCount_ = 0;
     friend bool LoadMitsubaXML(CScene* scene, const std::string& path);
+// The element / attribute tree the XML loader parsed (tests: compared with rapidxml's)
+bool DumpXmlTree(const std::string& path, std::string* out);
 };
 
 // OBJ parsing (the tinyobjloader subset WavefrontOBJLoading.cpp relies on).
@@ -176,6 +178,8 @@ bool CreateMeshFromObjData(const ObjData& data, const ObjShape* shapes, uint32_t
 void TranslateObjMaterials(const ObjData& data, int32_t textureIndexBase, std::vector<SMaterial>* out,
                            std::vector<std::string>* textureNames);
 bool LoadMitsubaXML(CScene* scene, const std::string& path);
+// The element / attribute tree the XML loader parsed (tests: compared with rapidxml's)
+bool DumpXmlTree(const std::string& path, std::string* out);
 bool LoadTextureFile(const std::string& path, CTexture* out);
 // MikkTSpace genTangSpaceDefault over a triangle list given per corner (3 per triangle;
 // texcoords carry z = 1); false for an empty list (tangent_space.cpp).

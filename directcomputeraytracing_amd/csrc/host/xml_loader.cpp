@@ -99,22 +99,6 @@ private:
         while (p_ < s_.size() && NameChar(s_[p_])) ++p_;
         return s_.substr(b, p_ - b);
     }
-    static std::string Unescape(const std::string& v)
-    {
-        std::string o;
-        for (size_t i = 0; i < v.size(); ++i) {
-            if (v[i] == '&') {
-                const size_t e = v.find(';', i);
-                if (e != std::string::npos) {
-                    const std::string ent = v.substr(i + 1, e - i - 1);
-                    const char* rep = ent == "amp" ? "&" : ent == "lt" ? "<" : ent == "gt" ? ">" : ent == "quot" ? "\"" : ent == "apos" ? "'" : nullptr;
-                    if (rep) { o += rep; i = e; continue; }
-                }
-            }
-            o += v[i];
-        }
-        return o;
-    }
     bool Element(XNode* n)
     {
         ++p_;   // '<'
@@ -135,7 +119,9 @@ private:
             const char q = s_[p_++];
             const size_t e = s_.find(q, p_);
             if (e == std::string::npos) return Fail("unterminated attribute value");
-            n->attrs.emplace_back(an, Unescape(s_.substr(p_, e - p_)));
+            // (quirk) the reference parses with rapidxml::parse_non_destructive
+            // (SceneXMLLoading.cpp:1056): no entity translation, "&amp;" stays as written
+            n->attrs.emplace_back(an, s_.substr(p_, e - p_));
             p_ = e + 1;
         }
         while (true) {
@@ -157,6 +143,19 @@ private:
     const std::string& s_;
     size_t p_ = 0;
 };
+
+// The element / attribute tree as the reference's walk sees it (rapidxml element nodes in
+// document order, attributes in order): "E<name>\n", "A<name>=<value>\n" per attribute,
+// the children, "/\n". tests/test_xml_pin.py compares it with the reference's rapidxml.
+void DumpTree(const XNode& n, std::string* out)
+{
+    for (const auto& c : n.children) {
+        *out += "E" + c->name + "\n";
+        for (const auto& a : c->attrs) *out += "A" + a.first + "=" + a.second + "\n";
+        DumpTree(*c, out);
+        *out += "/\n";
+    }
+}
 
 // ------------------------------------------------------------------ value graph (:13-581)
 enum class VT { Float, Integer, Boolean, String, Vector /* = RGB */, Matrix, Object };
@@ -556,6 +555,21 @@ bool MaterialContext::Translate(const Value& bsdf, SMaterial* m, bool twoSided, 
 }
 
 }  // namespace
+
+bool DumpXmlTree(const std::string& path, std::string* out)
+{
+    std::ifstream in(path, std::ios::binary);
+    if (!in) { SetLastError("cannot open " + path); return false; }
+    std::stringstream ss;
+    ss << in.rdbuf();
+    const std::string text = ss.str();
+    XNode doc;
+    XmlParser parser(text);
+    if (!parser.Parse(&doc)) { SetLastError("XML parse error in " + path + ": " + parser.error); return false; }
+    out->clear();
+    DumpTree(doc, out);
+    return true;
+}
 
 // CScene::LoadFromXMLFile (SceneXMLLoading.cpp:960-1512)
 bool LoadMitsubaXML(CScene* scene, const std::string& path)

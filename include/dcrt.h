@@ -438,6 +438,11 @@ DCRT_API int dcrt_obj_get_mesh(const dcrt_obj_meshes* meshes, uint32_t index, dc
 DCRT_API int dcrt_obj_material_count(const dcrt_obj_meshes* meshes, uint32_t* out_count);
 DCRT_API int dcrt_obj_get_material(const dcrt_obj_meshes* meshes, uint32_t index, dcrt_obj_material* out_material);
 DCRT_API void dcrt_obj_free(dcrt_obj_meshes* meshes);
+/* The element / attribute tree the Mitsuba XML loader parses from `path` (what
+ * SceneXMLLoading.cpp's walk over rapidxml's DOM reads, :247-581): per element in document
+ * order "E<name>\n", "A<name>=<value>\n" per attribute, its children, "/\n". Writes at most
+ * `capacity` bytes; *out_length = the full length (DCRT_E_LIMIT if it did not fit). */
+DCRT_API int dcrt_xml_dump_tree(const char* path, char* out, uint32_t capacity, uint32_t* out_length);
 
 /* ===== tracer: CWavefrontPathTracer on MI355X ============================== */
 DCRT_API int dcrt_tracer_create(const dcrt_tracer_config* config, dcrt_tracer** out_tracer);  /* Create()  */
