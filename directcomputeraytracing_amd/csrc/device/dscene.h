@@ -151,22 +151,10 @@ DEV void scene_cache_load(const DeviceScene& sc, uint32_t* stackMem, uint32_t sh
 }
 
 // ---- ray / primitive tests ----------------------------------------------------
-DEV bool ray_aabb(V3 o, V3 inv, float tMin, float tMax, float4 a, float4 b)
-{
-    const float tx0 = (a.x - o.x) * inv.x;
-    const float tx1 = (a.w - o.x) * inv.x;
-    float t0 = fminf(tx0, tx1);
-    float t1 = fmaxf(tx0, tx1);
-    const float ty0 = (a.y - o.y) * inv.y;
-    const float ty1 = (b.x - o.y) * inv.y;
-    t0 = fmaxf(t0, fminf(ty0, ty1));
-    t1 = fminf(t1, fmaxf(ty0, ty1));
-    const float tz0 = (a.z - o.z) * inv.z;
-    const float tz1 = (b.y - o.z) * inv.z;
-    t0 = fmaxf(t0, fminf(tz0, tz1));
-    t1 = fminf(t1, fmaxf(tz0, tz1));
-    return (t1 >= t0) & (t0 < tMax) & (t1 >= tMin);   // (bitwise: no exec-mask branch per node)
-}
+#ifndef DCRT_AXIS_PAIRS
+#define DCRT_AXIS_PAIRS 0
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct Shear {
     int kx, ky, kz;
@@ -309,7 +297,27 @@ struct TraversalStats {
 
 struct TravState {
     V3 o, d, invW;        // world ray and 1/d (restored on BLAS -> TLAS without dividing again)
-    V3 lo, ld, inv;       // ray in the current space (world or instance)
+    // ray in the current space (world or instance): direction ld, origin and 1/d kept as the
+    // three register pairs the packed slab test reads, (lo.x, lo.y), (inv.x, inv.y), (lo.z, inv.z)
+    // (without DCRT_AXIS_PAIRS: plain vectors -- the pairs' alignment costs the global-memory
+    // cast kernels 3 VGPRs)
+    V3 ld;
+#if DCRT_AXIS_PAIRS
+    f32x2 loXY, invXY, loZinvZ;
+    DEV V3 lo() const { return mk(loXY.x, loXY.y, loZinvZ.x); }
+    DEV V3 inv() const { return mk(invXY.x, invXY.y, loZinvZ.y); }
+    DEV void set_space(V3 o, V3 i)
+    {
+        loXY = (f32x2){o.x, o.y};
+        invXY = (f32x2){i.x, i.y};
+        loZinvZ = (f32x2){o.z, i.z};
+    }
+#else
+    V3 lo_, inv_;
+    DEV V3 lo() const { return lo_; }
+    DEV V3 inv() const { return inv_; }
+    DEV void set_space(V3 o, V3 i) { lo_ = o; inv_ = i; }
+#endif
     float tMin, tMax;
     uint32_t node;        // node index | 0x80000000 in a BLAS (the stack entries' packing)
     uint32_t sp;          // stack entries x stride (bytes): see stack_at
@@ -332,6 +340,46 @@ struct TravState {
     bool opaque;              // the current instance's INSTANCE_FLAG_OPAQUE
 };
 
+// Device node record (tracer.hip UploadScene): with DCRT_AXIS_PAIRS the box is stored per axis,
+// (min.x, max.x, min.y, max.y) (min.z, max.z, right, misc), so each slab's two planes sit in
+// one aligned register pair and the slab test runs as three packed-f32 subtractions and three
+// packed multiplies (v_pk_add_f32 / v_pk_mul_f32, the origin and 1/d component broadcast by
+// op_sel: no extra registers) -- the same IEEE operations per plane as below, so the same
+// bits. Without it, PackBVH's (min.xyz, max.x) (max.yz, right, misc).
+DEV bool ray_aabb(const TravState& s, float4 a, float4 b)
+{
+    const float tMin = s.tMin, tMax = s.tMax;
+#if DCRT_AXIS_PAIRS
+    const f32x2 px = (f32x2){a.x, a.y}, py = (f32x2){a.z, a.w}, pz = (f32x2){b.x, b.y};
+    // (each of the ray's six values broadcast from its register pair by op_sel)
+    const f32x2 tx = (px - s.loXY.xx) * s.invXY.xx;
+    const f32x2 ty = (py - s.loXY.yy) * s.invXY.yy;
+    const f32x2 tz = (pz - s.loZinvZ.xx) * s.loZinvZ.yy;
+    float t0 = fminf(tx.x, tx.y);
+    float t1 = fmaxf(tx.x, tx.y);
+    t0 = fmaxf(t0, fminf(ty.x, ty.y));
+    t1 = fminf(t1, fmaxf(ty.x, ty.y));
+    t0 = fmaxf(t0, fminf(tz.x, tz.y));
+    t1 = fminf(t1, fmaxf(tz.x, tz.y));
+    return (t1 >= t0) & (t0 < tMax) & (t1 >= tMin);
+#else
+    const V3 o = s.lo(), inv = s.inv();
+    const float tx0 = (a.x - o.x) * inv.x;
+    const float tx1 = (a.w - o.x) * inv.x;
+    float t0 = fminf(tx0, tx1);
+    float t1 = fmaxf(tx0, tx1);
+    const float ty0 = (a.y - o.y) * inv.y;
+    const float ty1 = (b.x - o.y) * inv.y;
+    t0 = fmaxf(t0, fminf(ty0, ty1));
+    t1 = fminf(t1, fmaxf(ty0, ty1));
+    const float tz0 = (a.z - o.z) * inv.z;
+    const float tz1 = (b.y - o.z) * inv.z;
+    t0 = fmaxf(t0, fminf(tz0, tz1));
+    t1 = fminf(t1, fmaxf(tz0, tz1));
+    return (t1 >= t0) & (t0 < tMax) & (t1 >= tMin);   // (bitwise: no exec-mask branch per node)
+#endif
+}
+
 // BVHAccel.inc.hlsl's near/far test `dir[axis] < 0` for all three axes at once, kept per
 // space (world, instance) so a node visit selects one bit instead of comparing three signs
 DEV uint32_t neg_mask(V3 d, uint32_t current)
@@ -344,7 +392,7 @@ DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax, bool f2b = 
 {
     s.negMask = neg_mask(d, f2b ? 8u : 0u);
     s.o = o; s.d = d; s.invW = inv_dir(d);
-    s.lo = o; s.ld = d; s.inv = inv_dir(d);
+    s.ld = d; s.set_space(o, inv_dir(d));
     s.tMin = tMin; s.tMax = tMax;
     s.node = 0; s.sp = 0; s.inst = 0;
     s.leafRef = 0; s.leafMisc = 0;
@@ -405,9 +453,8 @@ DEV bool trav_pop(TravState& s, uint32_t* lds, uint32_t stride)
     if (restore) {
         // component-wise: a struct copy inside the state becomes an alloca-local
         // memcpy that keeps SROA from promoting the state to registers
-        s.lo = mk(s.o.x, s.o.y, s.o.z);
         s.ld = mk(s.d.x, s.d.y, s.d.z);
-        s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+        s.set_space(s.o, s.invW);
         s.negMask = neg_mask(s.d, s.negMask);
     }
     return false;
@@ -448,7 +495,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         a = sc.nodes[idx * 2];
         b = sc.nodes[idx * 2 + 1];
     }
-    const bool hit = ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a, b);
+    const bool hit = ray_aabb(s, a, b);
     const uint32_t misc = asu(b.w);
     const uint32_t right = asu(b.z);
     // leaf: TLAS-leaf bit (4) or a primitive count (bits 3 and up); parked = hit && leaf
@@ -480,9 +527,8 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     // rare (about once per ray): a branch the wave skips when no lane restores; as
     // selects it cost nine v_cndmask per visit (measured 2.5 % of the cast kernel)
     if (__builtin_expect(restore, 0)) {
-        s.lo = mk(s.o.x, s.o.y, s.o.z);
         s.ld = mk(s.d.x, s.d.y, s.d.z);
-        s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+        s.set_space(s.o, s.invW);
         s.negMask = neg_mask(s.d, s.negMask);
     }
     s.parked = hit ^ descend;
@@ -537,8 +583,8 @@ DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uin
     float4 a0, b0, a1, b1;
     fetch(aRef, a0, b0);
     fetch(s.expand ? bRef : aRef, a1, b1);
-    const bool hitA = ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a0, b0);
-    const bool hitB = s.expand && ray_aabb(s.lo, s.inv, s.tMin, s.tMax, a1, b1);
+    const bool hitA = ray_aabb(s, a0, b0);
+    const bool hitB = s.expand && ray_aabb(s, a1, b1);
     // the node taken next: A if it hits, else B if it hits (push B when both hit)
     const bool take = hitA | hitB;
     const uint32_t takeRef = hitA ? aRef : bRef;
@@ -557,9 +603,8 @@ DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uin
     s.expNeg = __builtin_amdgcn_ubfe(s.negMask, misc, 1u) != 0u;
     s.expRight = right | blasBit;
     if (__builtin_expect(restore, 0)) {
-        s.lo = mk(s.o.x, s.o.y, s.o.z);
         s.ld = mk(s.d.x, s.d.y, s.d.z);
-        s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+        s.set_space(s.o, s.invW);
         s.negMask = neg_mask(s.d, s.negMask);
     }
     s.parked = take & leaf;
@@ -594,13 +639,11 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         }
         if (s.noZero && identity) {
             // x*1 + y*0 + z*0 + w*0 == x exactly for finite nonzero components
-            s.lo = mk(s.o.x, s.o.y, s.o.z);
             s.ld = mk(s.d.x, s.d.y, s.d.z);
-            s.inv = mk(s.invW.x, s.invW.y, s.invW.z);
+            s.set_space(s.o, s.invW);
         } else {
-            s.lo = mul43(s.o, 1.0f, M);
             s.ld = mul43(s.d, 0.0f, M);
-            s.inv = inv_dir(s.ld);
+            s.set_space(mul43(s.o, 1.0f, M), inv_dir(s.ld));
         }
         s.negMask = neg_mask(s.ld, s.negMask);
         s.inst = primOrInst;
@@ -615,7 +658,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
     // the shear of the current space, recomputed at every leaf instead of kept across
     // visits: fewer live registers (the cache-only kernel fits 7 waves/SIMD in 72 VGPRs:
     // 3.03 -> 2.96 ms/spp; coffee / lamp configs -1 to -2 %)
-    if (watertight) s.sh = ALL_CACHED ? make_shear_rot(s.ld, s.lo, s.inv) : make_shear(s.ld, s.inv);
+    if (watertight) s.sh = ALL_CACHED ? make_shear_rot(s.ld, s.lo(), s.inv()) : make_shear(s.ld, s.inv());
     // one triangle test: false = go on, true = the ray is finished (any-hit)
     auto test = [&](uint32_t p) __attribute__((always_inline)) {
         if (INSTR) ++st.tris;
@@ -643,8 +686,8 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
                 q2 = sc.triVerts[(size_t)p * 3 + 2];
             }
             const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
-            h = watertight ? tri_watertight(s.lo, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
-                           : tri_moller(s.lo, s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
+            h = watertight ? tri_watertight(s.lo(), s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
+                           : tri_moller(s.lo(), s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
         }
         if (OPACITY && h && !s.opaque) h = any_hit_shader(sc, p, s.matOverride, u, v, s.opacitySample);
         if (h) {

@@ -418,6 +418,9 @@ template <uint32_t CAPS>
 __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
                                                                              const Counters* prev, const SampleOut* sampleOut)
 {
+#if defined(DCRT_MATERIAL_PRIO) && DCRT_MATERIAL_PRIO > 0
+    __builtin_amdgcn_s_setprio(DCRT_MATERIAL_PRIO);   // (A/B: issue priority over a co-resident cast)
+#endif
     __shared__ uint32_t sm[96];
     // the work list: the previous iteration's extension queue (its rays have been cast) -- or
     // a batch start's virtual queue (item i = path slot i, kVirtualWord)
@@ -1212,8 +1215,14 @@ __global__ __launch_bounds__(256) void drain_kernel(PathPool pool, DeviceScene s
     const uint32_t shift = block_shift();
     const SampleOut so = *sampleOut;
     uint32_t extRays = 0, shadowRays = 0;
-    const uint32_t lanes = gridDim.x * blockDim.x;
-    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nExt + nFin; w += lanes) {
+    // paths dealt to the waves first, lanes second (path w -> wave w mod waves, lane w / waves):
+    // a wave runs a lane's path until that path ends, and its traversal and shading loops
+    // last as long as their slowest lane, so few paths per wave let each path run at its own
+    // chain's latency (the paths dealt to consecutive lanes had made every wave wait, bounce
+    // by bounce, for its slowest path -- the wavefront's drain iterations again)
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    for (uint32_t w = (threadIdx.x & 63u) * waves + wave; w < nExt + nFin; w += 64u * waves) {
         if (w >= nExt) {
             // a path MATERIAL ended with its shadow ray pending (cast this iteration): CONTROL's
             // completion, as control_kernel does it

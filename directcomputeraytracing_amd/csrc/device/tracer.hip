@@ -758,7 +758,16 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
                 if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
             }
         }
-        CHECKED(upload(&nodes, castPair ? pairNodes.data() : s.bvh_nodes, nodeCount));
+        // the device node record (dscene.h ray_aabb): DCRT_AXIS_PAIRS stores the box per axis
+        std::vector<dcrt_bvh_node> devNodes = castPair ? std::move(pairNodes) : std::vector<dcrt_bvh_node>(s.bvh_nodes, s.bvh_nodes + nodeCount);
+#if DCRT_AXIS_PAIRS
+        for (dcrt_bvh_node& n : devNodes) {
+            const float lo[3] = {n.bbox_min[0], n.bbox_min[1], n.bbox_min[2]}, hi[3] = {n.bbox_max[0], n.bbox_max[1], n.bbox_max[2]};
+            n.bbox_min[0] = lo[0]; n.bbox_min[1] = hi[0]; n.bbox_min[2] = lo[1];
+            n.bbox_max[0] = hi[1]; n.bbox_max[1] = lo[2]; n.bbox_max[2] = hi[2];
+        }
+#endif
+        CHECKED(upload(&nodes, devNodes.data(), nodeCount));
         HIPCHECK(hipStreamSynchronize(stream));   // (pairNodes ends with this block)
         d.nodes = (const float4*)nodes;
         d.nodeCount = nodeCount;
