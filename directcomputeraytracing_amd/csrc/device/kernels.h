@@ -77,7 +77,6 @@ struct Globals {
     // block outright and the shard cursors are preset past those blocks (staticGrid =
     // CONTROL workgroups, 0 = off); cleared after that iteration.
     uint32_t staticFill, staticGrid;
-    uint32_t filmBlocksDone;  // film_kernel's finished workgroups (the last one advances the batch)
     unsigned long long extRays, shadowRays, iterations;
 };
 

@@ -138,7 +138,6 @@ __global__ void set_idle_kernel(PathPool pool, Counters* counters, Globals* g, u
         g->imageTarget = 1u;
         g->staticFill = 0u;
         g->staticGrid = 0u;
-        g->filmBlocksDone = 0u;
     }
 }
 
@@ -1410,14 +1409,7 @@ __device__ __forceinline__ void film_pixel_window(const FilterConsts& c, uint32_
     *ye = (int)floorf(cy + r); *ye = *ye > (int)H - 1 ? (int)H - 1 : *ye;
 }
 
-__device__ __forceinline__ void advance_image(FrameConstants* fc, Globals* g);
-
-// With `guard` (RenderImages' sequenced iterations) the pass runs only in the iteration that
-// completed a batch, and the last workgroup to finish then advances to the next batch
-// (advance_image: the frame seed, the batch's image count and pixel blocks) -- one launch
-// instead of a film pass and an advance kernel per iteration.
-__global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t images, Globals* guard,
-                                                   FrameConstants* advanceFc)
+__global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t images, const Globals* guard)
 {
     if (guard && !guard->imageComplete) return;
     // the images of a completed batch, in order: per pixel the same additions as one
@@ -1503,19 +1495,6 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
         if (mine) film.accum[(size_t)py * W + px] = v;
         __syncthreads();   // the tile buffers are reused by the next tile
     }
-    if (guard && advanceFc) {
-        __shared__ uint32_t lastBlock;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();   // (this workgroup's reads of guard->batchImages are done)
-            lastBlock = atomicAdd(&guard->filmBlocksDone, 1u) == gridDim.x - 1u ? 1u : 0u;
-        }
-        __syncthreads();
-        if (lastBlock && threadIdx.x == 0) {
-            guard->filmBlocksDone = 0u;
-            advance_image(advanceFc, guard);
-        }
-    }
 }
 
 // film += src (dcrt_tracer_add_film_device): the films of disjoint film partitions
@@ -1529,9 +1508,9 @@ __global__ void add_film_kernel(float4* film, const float4* src, uint32_t n)
 
 // After the film pass of a completed batch: the next batch's first frame seed and
 // size, rewind the block cursors.
-__device__ __forceinline__ void advance_image(FrameConstants* fc, Globals* g)
+__global__ void advance_image_kernel(FrameConstants* fc, Globals* g)
 {
-    if (!g->imageComplete) return;
+    if (threadIdx.x != 0 || !g->imageComplete) return;
     g->imageComplete = 0u;
     g->imagesDone += g->batchImages;
     if (g->imagesDone < g->imageTarget) {

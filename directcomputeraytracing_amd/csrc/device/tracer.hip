@@ -1048,9 +1048,9 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
                            dGlobals, (const SampleOut*)dSampleOut);
     }
     if (sequenced) {
-        // (the film pass of a completed batch; its last workgroup advances to the next batch)
-        hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u, dGlobals,
-                           dFrame);
+        hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
+                           (const Globals*)dGlobals);
+        hipLaunchKernelGGL(advance_image_kernel, dim3(1), dim3(64), 0, stream, dFrame, dGlobals);
     }
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
@@ -1161,7 +1161,7 @@ int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
     if (!film.accum) { SetLastError("no film"); return DCRT_E_INVALID_ARG; }
     CHECKED(UploadFilter(f));
     hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
-                       (Globals*)nullptr, (FrameConstants*)nullptr);
+                       (const Globals*)nullptr);
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
 }
@@ -1194,7 +1194,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
             hipExtLaunchKernelGGL(mk, dim3(megaResident), dim3(castBlock), castLds, stream, e0, e1, 0, scene,
                                   (const FrameConstants*)dFrame, film, dGlobals, (uint32_t)(film.debugRng != nullptr));
             hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
-                               (Globals*)nullptr, (FrameConstants*)nullptr);
+                               (const Globals*)nullptr);
             HIPCHECK(hipGetLastError());
         }
         HIPCHECK(hipStreamSynchronize(stream));
