@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             const uint32_t vb = base / kControlBlock;
             const uint32_t claimed = (vb / kShards) * (kControlBlock >> 6) + (threadIdx.x >> 6);
             uint32_t pixel = kNoPixel, px = 0, py = 0, image = 0;
-            if (claimed < shardBlocks && block_pixel(*fc, film, shard + claimed * kShards, lane, &px, &py, &image)) {
+            if (claimed < shardBlocks && block_pixel(*fc, film, shard + claimed * kShards, lane, &px, &py, &image, kBlockInterleave ? g->batchImages : 0u)) {
                 pixel = image * (film.width * film.height) + py * film.width + px;
                 pool.flags[tid] = 0u;   // busy
             }
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     rng.s0 = rng.s1 = rng.s2 = rng.s3 = 0u;
     if (got) {
         uint32_t px = 0, py = 0, image = 0;
-        if (block_pixel(*fc, film, block, lane, &px, &py, &image)) {
+        if (block_pixel(*fc, film, block, lane, &px, &py, &image, kBlockInterleave ? g->batchImages : 0u)) {
             // NEW_PATH :211-237 (image `image` of the batch has frame seed frameSeed + image)
             rng = rng_init(px, py, fc->frameSeed + image);
             const float psx = next1(rng), psy = next1(rng);
@@ -665,9 +665,30 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
     const bool watertight = (features & DCRT_FEATURE_WATERTIGHT) != 0;
     const bool f2b = (features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
     const uint32_t wavesPerBlock = blockDim.x >> 6;
-    const uint32_t waves = gridDim.x * wavesPerBlock;
-    const uint32_t waveId = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
+    // XCD-aware split (DCRT_XCD_DEAL): the queue is cut into chunks of C items dealt
+    // round-robin to the 8 groups of workgroups that share an XCD (blockIdx mod 8 labels them),
+    // each group dealing its chunks among its own waves as below. With the batch's images
+    // interleaved block by block (kBlockInterleave) a chunk is one screen region of every image,
+    // so a group's node and triangle fetches stay within fewer regions' working sets in its L2;
+    // 8 chunks per group spread over the queue keep the groups' costs even.
+    uint32_t waves = gridDim.x * wavesPerBlock;
+    uint32_t waveId = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
+    uint32_t xcdGroup = 0, lgChunk = 0;
+    const bool xcdDeal = DCRT_XCD_DEAL && (gridDim.x & 7u) == 0u && n >= 64u * 64u;
+    if (xcdDeal) {
+        xcdGroup = blockIdx.x & 7u;
+        lgChunk = 31u - (uint32_t)__clz((int)(n >> 6));   // C = 2^lgChunk <= n / 64
+        const uint32_t C = 1u << lgChunk, full = n >> (lgChunk + 3u), rem = n - (full << (lgChunk + 3u));
+        const uint32_t before = xcdGroup << lgChunk;
+        n = (full << lgChunk) + (rem > before ? min(rem - before, C) : 0u);
+        waves = (gridDim.x >> 3) * wavesPerBlock;
+        waveId = (blockIdx.x >> 3) * wavesPerBlock + (threadIdx.x >> 6);
+    }
+    // the queue item of the group's j-th item
+    auto groupItem = [&](uint32_t j) {
+        return xcdDeal ? ((((j >> lgChunk) << 3) + xcdGroup) << lgChunk) + (j & ((1u << lgChunk) - 1u)) : j;
+    };
     // Work split: the queue is cut into groups of kInterleave consecutive items (one
     // region of the image / one producer workgroup each) dealt round-robin to the
     // waves, so every wave samples the whole queue and per-wave costs even out
@@ -726,7 +747,8 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         if (refill) {
             const uint32_t idx = itemIndex(k);
             if (free && k < end && idx < n) {
-                item = fetch(idx, lookup(idx), s);
+                const uint32_t qi = groupItem(idx);
+                item = fetch(qi, lookup(qi), s);
                 if (!f2b) s.negMask = 0u;
                 // (kNoItem: the queue item has no ray -- a hole of a virtual batch start)
                 ls = item != kNoItem ? kRun : kIdle;

@@ -2,10 +2,6 @@ set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-AB_CONFIGS="spaceship cornell" PASSES=2 bash tools/ab_configs2.sh || exit $?
-for cfg in spaceship; do
-  OUT=gpurun_out/seq_$cfg; mkdir -p $OUT
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$GRAFT_REPO_ROOT/$OUT" -o trace -- python3 "$GRAFT_REPO_ROOT/bench.py" --config $cfg --steps 8 --warmup 0 --no-cpu-baseline --streams 1 --repeats 1 --roofline-images 1 --spaceship-spp 0 > "$GRAFT_REPO_ROOT/$OUT/bench.log" 2>&1) || exit $?
-  f=$(ls $OUT/*kernel_trace.csv | head -1)
-  python tools/kseq.py $f 0 48 > $OUT/seq.txt; cat $OUT/seq.txt
-done
+DCRT_LIB=gpu_ab/b_xcd.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "virtual or config or spaceship or render" > gpurun_out/pytest_xcd.log 2>&1; rc=$?; echo "pytest(xcd) rc=$rc"; tail -3 gpurun_out/pytest_xcd.log
+[ $rc -eq 0 ] || exit $rc
+AB_CONFIGS="spaceship_close spaceship cornell" PASSES=2 bash tools/ab_configs2.sh
