@@ -83,7 +83,18 @@ struct DeviceScene {
     uint32_t cachedInstances;     // 0, or instanceCount: every inverse transform + identity flag, after the triangles
     uint32_t singlePrimLeaves;    // 1: every BLAS leaf holds exactly one triangle (BVHAccel.cpp's builder always does)
     uint32_t pairLayout;          // node order: 0 PackBVH's (flat scene), 1 child pairs (kLayoutPairs)
+    // MATERIAL's LDS scene copy (material_kernel<CAPS, true>, small scenes): the material and
+    // light counts it copies (0 when the variant is not used)
+    uint32_t ldsMaterials, ldsLights;
 };
+
+// MATERIAL's LDS scene copy, in 16-B units: triVerts (3 T), triShade (6 T), the forward
+// instance transforms (3 I), then 4-B words: instance light indices (I), overrides (I),
+// materials (13 M), lights (7 L). Bytes for T triangles, I instances, M materials, L lights.
+__host__ __device__ inline uint32_t material_lds_bytes(uint32_t T, uint32_t I, uint32_t M, uint32_t L)
+{
+    return 16u * (9u * T + 3u * I) + 4u * (2u * I + 13u * M + 7u * L);
+}
 
 // Node orders on the device. kLayoutFlat is PackBVH's depth-first order, as in the flat
 // scene: an interior node's left child is node + 1 and its `right` field the right child.

@@ -413,7 +413,11 @@ static_assert(DCRT_MATERIAL_BLOCK % 64 == 0 && DCRT_MATERIAL_BLOCK <= 960, "MATE
 #define DCRT_MATERIAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(CAPS == kCapAll ? DCRT_MATERIAL_WAVES_PER_EU : 1, 8)))
 // CAPS: the scene capabilities this variant is compiled for (kCapAll = any scene; see
 // kCapOpaqueDelta in dscene.h and dcrt_tracer::UploadScene).
-template <uint32_t CAPS>
+// SCENE_LDS: the scene arrays MATERIAL's shading reads per item (pre-gathered triangles, the
+// forward instance transforms and instance words, materials, lights) are copied into LDS by
+// each workgroup first (small scenes: material_lds_bytes within the host's budget), so
+// HitInfoToIntersection's dependent fetches (hit -> triangle -> material) are LDS reads.
+template <uint32_t CAPS, bool SCENE_LDS>
 __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
                                                                              const Counters* prev, const SampleOut* sampleOut)
 {
@@ -430,6 +434,33 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     const uint32_t count = drained(prev) ? 0u : (virt ? virt : qm.prefix[kShards]);
     const uint32_t shard = blockIdx.x % kShards;
     const uint32_t fshard = blockIdx.x % kFinShards;
+    if constexpr (SCENE_LDS) {
+        extern __shared__ float4 sceneLds[];
+        if (blockIdx.x * blockDim.x >= count) return;   // (no item: no copy)
+        const uint32_t T = sc.triangleCount, I = sc.instanceCount;
+        float4* tv = sceneLds;
+        float4* ts = tv + 3u * T;
+        float4* tf = ts + 6u * T;
+        uint32_t* w = (uint32_t*)(tf + 3u * I);
+        uint32_t* li = w;
+        uint32_t* ov = li + I;
+        uint32_t* mt = ov + I;
+        uint32_t* lt = mt + 13u * sc.ldsMaterials;
+        for (uint32_t i = threadIdx.x; i < 3u * T; i += blockDim.x) tv[i] = sc.triVerts[i];
+        for (uint32_t i = threadIdx.x; i < 6u * T; i += blockDim.x) ts[i] = sc.triShade[i];
+        for (uint32_t i = threadIdx.x; i < 3u * I; i += blockDim.x) tf[i] = sc.transforms[i];
+        for (uint32_t i = threadIdx.x; i < I; i += blockDim.x) { li[i] = sc.instanceLightIndices[i]; ov[i] = sc.overrides[i]; }
+        for (uint32_t i = threadIdx.x; i < 13u * sc.ldsMaterials; i += blockDim.x) mt[i] = ((const uint32_t*)sc.materials)[i];
+        for (uint32_t i = threadIdx.x; i < 7u * sc.ldsLights; i += blockDim.x) lt[i] = ((const uint32_t*)sc.lights)[i];
+        __syncthreads();
+        sc.triVerts = tv;
+        sc.triShade = ts;
+        sc.transforms = tf;
+        sc.instanceLightIndices = li;
+        sc.overrides = ov;
+        sc.materials = (const dcrt_material*)mt;
+        sc.lights = (const dcrt_light*)lt;
+    }
     DCRT_MCLK_INIT;
     uint32_t itemsDone = 0;
     uint32_t round = 0;   // grid-stride round: alternates block_append2's sm halves
