@@ -410,7 +410,10 @@ static_assert(DCRT_MATERIAL_BLOCK % 64 == 0 && DCRT_MATERIAL_BLOCK <= 960, "MATE
 #ifndef DCRT_MATERIAL_WAVES_PER_EU
 #define DCRT_MATERIAL_WAVES_PER_EU 5
 #endif
-#define DCRT_MATERIAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(CAPS == kCapAll ? DCRT_MATERIAL_WAVES_PER_EU : 1, 8)))
+#ifndef DCRT_MATERIAL_OD_WAVES_PER_EU
+#define DCRT_MATERIAL_OD_WAVES_PER_EU 1   // (the opaque / delta-light variants: the compiler's choice)
+#endif
+#define DCRT_MATERIAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(CAPS == kCapAll ? DCRT_MATERIAL_WAVES_PER_EU : DCRT_MATERIAL_OD_WAVES_PER_EU, 8)))
 // CAPS: the scene capabilities this variant is compiled for (kCapAll = any scene; see
 // kCapOpaqueDelta in dscene.h and dcrt_tracer::UploadScene).
 // SCENE_LDS: the scene arrays MATERIAL's shading reads per item (pre-gathered triangles, the
