@@ -786,7 +786,29 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         d.nodes = (const float4*)nodes;
         d.nodeCount = nodeCount;
         d.pairLayout = castPair ? 1u : 0u;
+        const size_t stackLds = castLds;
         castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * (castAllCached ? 144 : 48) + (size_t)d.cachedInstances * 64;
+        // The budget above divides 160 KiB evenly among the workgroups the registers allow; the
+        // LDS is allocated in granules (and the kernel's static LDS comes on top), so the cache
+        // could cost a workgroup per CU (the spaceship pair kernel ran 5 of its 6). Trim the
+        // cache -- triangles first, then nodes, a granule at a time -- until the launched kernel
+        // keeps the occupancy the stack alone allows.
+        bool trim = true;
+        if (const char* e = std::getenv("DCRT_LDS_TRIM")) trim = std::atoi(e) != 0;   // (A/B)
+        if (!castAllCached && trim) {
+            auto occupancy = [&](size_t lds) {
+                int n = 0;
+                if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, CastKernel(false, false, false, castPair), (int)castBlock, lds));
+                else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extension_kernel<false, false>, (int)castBlock, lds));
+                return n;
+            };
+            const int target = occupancy(stackLds);
+            while (occupancy(castLds) < target && (d.cachedTris > 0 || d.cachedNodes > 0)) {
+                if (d.cachedTris > 0) d.cachedTris -= std::min<uint32_t>(d.cachedTris, 11);   // 528 B
+                else d.cachedNodes -= std::min<uint32_t>(d.cachedNodes, 16);                  // 512 B
+                castLds = stackLds + (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * 48;
+            }
+        }
         scene = d;
     }
     {
@@ -1490,6 +1512,8 @@ DCRT_API int dcrt_tracer_get_info(dcrt_tracer* t, dcrt_tracer_info* out)
     out->pair_traversal = t->hasScene && t->castPair ? 1u : 0u;
     out->control_grid = t->controlGrid;
     out->material_grid = t->materialGrid;
+    out->cast_grid = t->castResident;
+    out->material_lds = t->materialLds;
     return DCRT_OK;
 }
 

@@ -284,6 +284,8 @@ typedef struct dcrt_tracer_info {
     uint32_t pair_traversal;      /* 1: the cast kernel expands node pairs (scene beyond L2), over the device
                                      child-pair node order */
     uint32_t control_grid, material_grid;   /* CONTROL / MATERIAL workgroups per launch  */
+    uint32_t cast_grid;           /* persistent cast-kernel workgroups (resident on the chip) */
+    uint32_t material_lds;        /* bytes of MATERIAL's LDS scene copy (0: not used)      */
 } dcrt_tracer_info;
 
 typedef struct dcrt_tracer dcrt_tracer;
