@@ -321,6 +321,39 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
         assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
 
+@pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
+def test_material_lds_scene_copy_bit_exact(native_lib, golden_luts, monkeypatch, scene_name):
+    """MATERIAL's LDS scene copy (material_kernel<CAPS, true>: triangles, forward transforms,
+    instance words, materials and lights read from LDS) against the global-memory variant
+    (DCRT_MATERIAL_LDS=0): the same samples, RNG state and film bit for bit; the copy is what
+    the default picks for these small scenes (the other parity tests compare it with the
+    oracle)."""
+    from conftest import GOLDEN
+    from directcomputeraytracing_amd import FILTER_BOX, FilterParams, Scene, WavefrontPathTracer
+    if scene_name == "cornell":
+        s = cornell(96, 64, 6)
+    else:
+        s = Scene((45, 29))
+        s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
+    filt = FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3)
+    runs = {}
+    for budget in ("16384", "0"):
+        monkeypatch.setenv("DCRT_MATERIAL_LDS", budget)
+        t = WavefrontPathTracer(path_pool_size=1 << 14, debug_rng=True)
+        try:
+            t.set_luts(golden_luts)
+            t.on_scene_loaded(s)
+            lds = t.info()["material_lds"]
+            assert (lds > 0) == (budget != "0")
+            t.clear_film()
+            t.render_images(0, 3, filt)
+            runs[budget] = (t.read_film(), t.read_samples(), t.read_rng())
+        finally:
+            t.destroy()
+    (fa, (pa, va), ra), (fb, (pb, vb), rb) = runs["16384"], runs["0"]
+    assert np.array_equal(ra, rb) and same_bits(pa, pb).all() and same_bits(va, vb).all() and same_bits(fa, fb).all()
+
+
 @pytest.mark.parametrize("cache,scene_name,pool", [("lds", "cornell", 1 << 15), ("global", "cornell", 1 << 15),
                                                    ("pair", "cornell", 1 << 12), ("global", "xml_mix", 1 << 14),
                                                    ("pair", "xml_mix", 3000)])
