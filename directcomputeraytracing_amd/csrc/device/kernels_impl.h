@@ -186,7 +186,7 @@ __global__ void build_tri_verts_kernel(const dcrt_vertex* vertices, const uint32
 // scans the slots for fully idle waves, which claim the next 8x8 block and start its
 // paths (NEW_PATH). With every block claimed (the batch's first pass claims all of
 // them) a pass is the finish list only, not a read of every slot's flags.
-__global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, Film film, const FrameConstants* fc, Counters* cnt,
+__global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, Film film, const FrameConstants* __restrict__ fc, Counters* cnt,
                                                        const Counters* prev, Globals* g, uint32_t debugRng)
 {
     __shared__ uint32_t sm[64];
@@ -421,8 +421,8 @@ static_assert(DCRT_MATERIAL_BLOCK % 64 == 0 && DCRT_MATERIAL_BLOCK <= 960, "MATE
 // each workgroup first (small scenes: material_lds_bytes within the host's budget), so
 // HitInfoToIntersection's dependent fetches (hit -> triangle -> material) are LDS reads.
 template <uint32_t CAPS, bool SCENE_LDS>
-__global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
-                                                                             const Counters* prev, const SampleOut* sampleOut)
+__global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fcr, Counters* cnt,
+                                                                             const Counters* prev, const SampleOut* __restrict__ sampleOut)
 {
 #if defined(DCRT_MATERIAL_PRIO) && DCRT_MATERIAL_PRIO > 0
     __builtin_amdgcn_s_setprio(DCRT_MATERIAL_PRIO);   // (A/B: issue priority over a co-resident cast)
@@ -437,6 +437,11 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     const uint32_t count = drained(prev) ? 0u : (virt ? virt : qm.prefix[kShards]);
     const uint32_t shard = blockIdx.x % kShards;
     const uint32_t fshard = blockIdx.x % kFinShards;
+    // The frame constants through a restrict-qualified pointer: nothing this kernel stores
+    // aliases them, so their reads in the item loop are scalar loads (scalar cache) -- through
+    // the plain pointer they were vector loads, each waited on at once, several dependent round
+    // trips per round.
+    const FrameConstants& fcv = *fcr;
     if constexpr (SCENE_LDS) {
         extern __shared__ float4 sceneLds[];
         if (blockIdx.x * blockDim.x >= count) return;   // (no item: no copy)
@@ -507,7 +512,7 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
             // its pixel -- the rng after the five camera draws, isDelta, bounce 0, T = 1,
             // bsdfPdf = 0, Li = 0, no light sampling result
             V3 unusedO, unusedD;
-            rng = new_path<false>(*fc, newPixel, &unusedO, &unusedD);
+            rng = new_path<false>(fcv, newPixel, &unusedO, &unusedD);
             path = i;
             flags = kFlagDelta;
             thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
@@ -548,10 +553,10 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         float extOpacity = 0.0f, shadowOpacity = 0.0f;
         V3 T, L, lsr;
         DCRT_MCLK(0);
-        shade_path<CAPS>(sc, *fc, hit, dir, rng, flags, thr, li, T, L, lsr, terminate, hasShadow, nO, nD, sO, sD,
+        shade_path<CAPS>(sc, fcv, hit, dir, rng, flags, thr, li, T, L, lsr, terminate, hasShadow, nO, nD, sO, sD,
                          extOpacity, shadowOpacity);
         DCRT_MCLK(4);
-        if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430
+        if (fcv.features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430
             if (!terminate) slot(pool.extOpacity, out) = extOpacity;
             if (hasShadow) slot(pool.shadowOpacity, out) = shadowOpacity;
         }
@@ -618,10 +623,10 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         r[1] = make_float4(sD.x, sD.y, sD.z, asf(terminate ? (fPos | kDestFinish) : qNext));
         // the path slot beside it: only ALLOW_ANYHIT_SHADER's cast reads it (the shadow ray's
         // opacity sample is per slot)
-        if (fc->features & DCRT_FEATURE_ALLOW_ANYHIT) slot(pool.shadowQueue, sq) = path;
+        if (fcv.features & DCRT_FEATURE_ALLOW_ANYHIT) slot(pool.shadowQueue, sq) = path;
     }
     if (ends) {
-        sample_at(outPos, pix) = pixel_sample(*fc, pix);
+        sample_at(outPos, pix) = pixel_sample(fcv, pix);
         sample_at(outVal, pix) = sample;
     }
     DCRT_MCLK(6);
@@ -887,7 +892,7 @@ __device__ __forceinline__ void emit_occlusion(const PathPool& pool, uint32_t de
 // OPACITY: the ALLOW_ANYHIT_SHADER variant (a separate instantiation, so the default
 // kernels carry none of its state).
 template <bool INSTR, bool OPACITY>
-__global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, const Counters* cnt,
+__global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void extension_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fc, const Counters* cnt,
                                                          Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
@@ -938,7 +943,7 @@ __device__ __forceinline__ void end_iteration(const Counters* cnt, Counters* nex
 }
 
 template <bool INSTR, bool OPACITY>
-__global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
+__global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fc, Counters* cnt,
                                                       Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
@@ -971,7 +976,7 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
 // results are those of the two separate kernels.
 template <bool INSTR, bool OPACITY, bool ALL_CACHED, bool PAIR>
 __global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHED_CAST_WAVES_PER_EU : DCRT_CAST_WAVES_PER_EU, 8))) void cast_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fc, Counters* cnt,
+__attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHED_CAST_WAVES_PER_EU : DCRT_CAST_WAVES_PER_EU, 8))) void cast_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fc, Counters* cnt,
                                                                      Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];

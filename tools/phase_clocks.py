@@ -62,9 +62,10 @@ def main():
     m = out[8:15].astype(np.float64)
     mt = m.sum()
     print(f"MATERIAL: {int(out[15])} lane-items (waves x items), wave-cycles per wave-item {mt / max(1, out[15]):.0f}")
-    for i, name in enumerate(("loads + Li update", "HitInfoToIntersection", "emission (EvaluateLight)", "NEE: light sample, BSDF eval/pdf, shadow ray",
-                              "BSDF sample + new ray", "stores", "queue appends")):
-        print(f"  {name:46s} {m[i] / 1e9:8.3f} Gcycles  {100 * m[i] / mt:5.1f} %")
+    # (material_kernel's DCRT_MCLK sections: 0 loads, 4 shade_path, 5 end-of-path loads, 6 appends + stores)
+    for i, name in ((0, "loads (hit, state halves) + Li update"), (4, "shade_path (HitInfo, emission, NEE, BSDF sample)"),
+                    (5, "end-of-path (pixel, debug RNG)"), (6, "queue appends + record / sample stores")):
+        print(f"  {name:50s} {m[i] / 1e9:8.3f} Gcycles  {100 * m[i] / mt:5.1f} %")
     tr.destroy()
 
 
