@@ -1105,7 +1105,7 @@ __device__ __forceinline__ bool trace_full(const DeviceScene& sc, V3 o, V3 d, fl
 }
 
 template <bool OPACITY>
-__global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameConstants* fcp, Film film, Globals* g, uint32_t debugRng)
+__global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameConstants* __restrict__ fcp, Film film, Globals* g, uint32_t debugRng)
 {
     extern __shared__ uint32_t stackMem[];
     scene_cache_load(sc, stackMem, block_shift());
@@ -1248,8 +1248,8 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
 // other in its lane and different paths overlap. The next iteration then finds the queues
 // empty (kDrainedWord) and the batch complete.
 template <uint32_t CAPS>
-__global__ __launch_bounds__(256) void drain_kernel(PathPool pool, DeviceScene sc, const FrameConstants* fcp, Counters* cnt,
-                                                    Globals* g, const SampleOut* sampleOut)
+__global__ __launch_bounds__(256) void drain_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fcp, Counters* cnt,
+                                                    Globals* g, const SampleOut* __restrict__ sampleOut)
 {
     const FrameConstants& fc = *fcp;
     if (!fc.drainPaths || g->stopped || virtual_items(cnt)) return;
