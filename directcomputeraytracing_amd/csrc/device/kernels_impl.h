@@ -522,18 +522,24 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
             const uint32_t q = qpos(pool.recCap, qm, i);
             const PathStateA& ps = state_at(pool.stateAPrev, q);
             const PathStateB& psB = state_at(pool.stateBPrev, q);
+            // All of the item's loads in one round trip: both state halves and the shadow result
+            // are read unconditionally (position q is always allocated; what the flags say is not
+            // there is stale and not used) -- conditioned on the flags, the compiler issued them
+            // only after the first half arrived, a second and third dependent round trip.
             const uint4 r4 = ps.rng;
-            rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
             l2 = ps.lsrMisc;
+            const float4 bThr = psB.thr, bLi = psB.liLsr;
+            const uint32_t shRaw = pool.shadowHitPrev[q];
+            rng.s0 = r4.x; rng.s1 = r4.y; rng.s2 = r4.z; rng.s3 = r4.w;
             path = asu(l2.w);
             flags = asu(l2.z);
             // a new path's first pass: NEW_PATH's constants, not the record's unwritten half
             const bool first = (flags & kFlagFirst) != 0u;
-            thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : psB.thr;
-            l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : psB.liLsr;
+            thr = first ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : bThr;
+            l4 = first ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : bLi;
             // the last shadow ray's result exists only if the path cast one (a position nothing
             // wrote this batch holds a stale value; its lsr is 0 then, but it is not read)
-            if (flags & kFlagShadowPending) shadowHit = pool.shadowHitPrev[q] != 0u;
+            shadowHit = (flags & kFlagShadowPending) != 0u && shRaw != 0u;
             flags &= ~(kFlagFirst | kFlagShadowPending);
         }
         F3 li{l4.x, l4.y, l4.z};
