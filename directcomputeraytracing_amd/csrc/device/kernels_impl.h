@@ -416,11 +416,13 @@ static_assert(DCRT_MATERIAL_BLOCK % 64 == 0 && DCRT_MATERIAL_BLOCK <= 960, "MATE
 #define DCRT_MATERIAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(CAPS == kCapAll ? DCRT_MATERIAL_WAVES_PER_EU : DCRT_MATERIAL_OD_WAVES_PER_EU, 8)))
 // CAPS: the scene capabilities this variant is compiled for (kCapAll = any scene; see
 // kCapOpaqueDelta in dscene.h and dcrt_tracer::UploadScene).
-// SCENE_LDS: the scene arrays MATERIAL's shading reads per item (pre-gathered triangles, the
-// forward instance transforms and instance words, materials, lights) are copied into LDS by
-// each workgroup first (small scenes: material_lds_bytes within the host's budget), so
-// HitInfoToIntersection's dependent fetches (hit -> triangle -> material) are LDS reads.
-template <uint32_t CAPS, bool SCENE_LDS>
+// SCENE_LDS: the scene arrays MATERIAL's shading reads per item are copied into LDS by each
+// workgroup first, so HitInfoToIntersection's dependent fetches are LDS reads -- 1: all of them
+// (pre-gathered triangles, the forward instance transforms and instance words, materials,
+// lights: small scenes, material_lds_bytes within the host's budget); 2: all but the triangles
+// (larger scenes: the hit -> triangle fetch stays global, the triangle -> material one and the
+// light sample's reads become LDS reads); 0: none.
+template <uint32_t CAPS, int SCENE_LDS>
 __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fcr, Counters* cnt,
                                                                              const Counters* prev, const SampleOut* __restrict__ sampleOut)
 {
@@ -442,10 +444,10 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     // the plain pointer they were vector loads, each waited on at once, several dependent round
     // trips per round.
     const FrameConstants& fcv = *fcr;
-    if constexpr (SCENE_LDS) {
+    if constexpr (SCENE_LDS != 0) {
         extern __shared__ float4 sceneLds[];
         if (blockIdx.x * blockDim.x >= count) return;   // (no item: no copy)
-        const uint32_t T = sc.triangleCount, I = sc.instanceCount;
+        const uint32_t T = SCENE_LDS == 1 ? sc.triangleCount : 0u, I = sc.instanceCount;
         float4* tv = sceneLds;
         float4* ts = tv + 3u * T;
         float4* tf = ts + 6u * T;
@@ -461,8 +463,10 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         for (uint32_t i = threadIdx.x; i < 13u * sc.ldsMaterials; i += blockDim.x) mt[i] = ((const uint32_t*)sc.materials)[i];
         for (uint32_t i = threadIdx.x; i < 7u * sc.ldsLights; i += blockDim.x) lt[i] = ((const uint32_t*)sc.lights)[i];
         __syncthreads();
-        sc.triVerts = tv;
-        sc.triShade = ts;
+        if constexpr (SCENE_LDS == 1) {
+            sc.triVerts = tv;
+            sc.triShade = ts;
+        }
         sc.transforms = tf;
         sc.instanceLightIndices = li;
         sc.overrides = ov;

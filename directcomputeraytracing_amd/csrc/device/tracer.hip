@@ -254,6 +254,7 @@ struct dcrt_tracer {
     // "virtual workgroups" vb = blockIdx.x + round * gridDim.x
     uint32_t controlGrid = 0, materialGrid = 0;
     uint32_t materialLds = 0;          // MATERIAL's dynamic LDS: the scene copy's bytes (0: the global-memory variant)
+    uint32_t materialLdsMode = 0;      // material_kernel<CAPS, mode>: 0 no copy, 1 whole shading data, 2 all but the triangles
     uint32_t iterationsPerRender = kDefaultIterations;
     bool debugRng = false;
     // cast-kernel refill / park thresholds (persistent_trace): refill when 36 lanes are idle
@@ -478,7 +479,7 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
         HIPCHECK(hipGetDeviceProperties(&prop, device));
         int cPerCU = 0, mPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&cPerCU, control_kernel, (int)kControlBlock, 0));
-        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&mPerCU, material_kernel<kCapAll, false>, (int)kMaterialBlock, 0));
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&mPerCU, material_kernel<kCapAll, 0>, (int)kMaterialBlock, 0));
         auto resident = [&](int perCU, const char* knob, uint32_t mul) {
             if (const char* g = std::getenv(knob)) mul = (uint32_t)std::max(0, std::atoi(g));
             if (mul == 0) return V;
@@ -708,17 +709,22 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     }
     for (uint32_t i = 0; i < s.light_count; ++i) sceneCaps |= (s.lights[i].flags & 0xFu) << kCapLightShift;
     materialCaps = (sceneCaps & ~kCapOpaqueDelta) == 0u ? kCapOpaqueDelta : kCapAll;
-    // MATERIAL's LDS scene copy for small scenes (material_kernel<CAPS, true>; DCRT_MATERIAL_LDS
-    // = bytes budget, 0: off)
+    // MATERIAL's LDS scene copy (material_kernel<CAPS, mode>): the whole shading data of a small
+    // scene (mode 1), else everything but the triangles (mode 2) -- DCRT_MATERIAL_LDS = bytes
+    // budget, 0: off; DCRT_MATERIAL_LDS_PARTIAL=0: no mode 2
     {
         uint32_t budget = 16384;
         if (const char* e = std::getenv("DCRT_MATERIAL_LDS")) budget = (uint32_t)std::max(0, std::atoi(e));
-        const uint64_t bytes = material_lds_bytes(s.triangle_count, s.instance_count, s.material_count, s.light_count);
-        const bool fits = s.triangle_count > 0 && bytes <= budget && s.triangle_count < (1u << 20) && s.instance_count < (1u << 20) &&
-                          s.material_count < (1u << 20) && s.light_count < (1u << 20);
-        materialLds = fits ? (uint32_t)bytes : 0u;
-        d.ldsMaterials = fits ? s.material_count : 0u;
-        d.ldsLights = fits ? s.light_count : 0u;
+        bool partial = true;
+        if (const char* e = std::getenv("DCRT_MATERIAL_LDS_PARTIAL")) partial = std::atoi(e) != 0;
+        const bool counts = s.triangle_count > 0 && s.triangle_count < (1u << 20) && s.instance_count < (1u << 20) &&
+                            s.material_count < (1u << 20) && s.light_count < (1u << 20);
+        const uint64_t whole = material_lds_bytes(s.triangle_count, s.instance_count, s.material_count, s.light_count);
+        const uint64_t rest = material_lds_bytes(0u, s.instance_count, s.material_count, s.light_count);
+        materialLdsMode = !counts ? 0u : whole <= budget ? 1u : (partial && rest <= budget ? 2u : 0u);
+        materialLds = materialLdsMode == 1 ? (uint32_t)whole : materialLdsMode == 2 ? (uint32_t)rest : 0u;
+        d.ldsMaterials = materialLdsMode ? s.material_count : 0u;
+        d.ldsLights = materialLdsMode ? s.light_count : 0u;
         scene = d;
     }
     if (const char* g = std::getenv("DCRT_MATERIAL_GENERIC")) {   // A/B: always the generic variant
@@ -1057,8 +1063,11 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     if (timed) CHECKED(TimedPair(kTimedControl, &c0, &c1));
     hipExtLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, c0, c1, 0, pool, film,
                           (const FrameConstants*)dFrame, cnt, (const Counters*)next, dGlobals, (uint32_t)(film.debugRng != nullptr));
-    auto material = materialCaps == kCapOpaqueDelta ? (materialLds ? material_kernel<kCapOpaqueDelta, true> : material_kernel<kCapOpaqueDelta, false>)
-                                                    : (materialLds ? material_kernel<kCapAll, true> : material_kernel<kCapAll, false>);
+    auto material = materialCaps == kCapOpaqueDelta
+                        ? (materialLdsMode == 1 ? material_kernel<kCapOpaqueDelta, 1>
+                                                : materialLdsMode == 2 ? material_kernel<kCapOpaqueDelta, 2> : material_kernel<kCapOpaqueDelta, 0>)
+                        : (materialLdsMode == 1 ? material_kernel<kCapAll, 1>
+                                                : materialLdsMode == 2 ? material_kernel<kCapAll, 2> : material_kernel<kCapAll, 0>);
     if (timed) CHECKED(TimedPair(kTimedMaterial, &m0, &m1));
     hipExtLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), materialLds, stream, m0, m1, 0, pool, scene,
                           (const FrameConstants*)dFrame, cnt, (const Counters*)next, (const SampleOut*)dSampleOut);

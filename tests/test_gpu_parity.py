@@ -323,11 +323,12 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
 
 @pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
 def test_material_lds_scene_copy_bit_exact(native_lib, golden_luts, monkeypatch, scene_name):
-    """MATERIAL's LDS scene copy (material_kernel<CAPS, true>: triangles, forward transforms,
-    instance words, materials and lights read from LDS) against the global-memory variant
-    (DCRT_MATERIAL_LDS=0): the same samples, RNG state and film bit for bit; the copy is what
-    the default picks for these small scenes (the other parity tests compare it with the
-    oracle)."""
+    """MATERIAL's LDS scene copy (material_kernel<CAPS, 1>: triangles, forward transforms,
+    instance words, materials and lights read from LDS; <CAPS, 2>: all but the triangles)
+    against the global-memory variant (DCRT_MATERIAL_LDS=0): the same samples, RNG state and
+    film bit for bit; the whole copy is what the default picks for these small scenes, the
+    partial one what it picks for the larger config scenes (the other parity tests compare
+    both with the oracle)."""
     from conftest import GOLDEN
     from directcomputeraytracing_amd import FILTER_BOX, FilterParams, Scene, WavefrontPathTracer
     if scene_name == "cornell":
@@ -336,22 +337,26 @@ def test_material_lds_scene_copy_bit_exact(native_lib, golden_luts, monkeypatch,
         s = Scene((45, 29))
         s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
     filt = FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3)
-    runs = {}
-    for budget in ("16384", "0"):
+    runs, sizes = {}, {}
+    # 16 KiB: the whole copy; 1 KiB: all but the triangles (the partial copy larger scenes get);
+    # 0: none
+    for budget in ("16384", "1024", "0"):
         monkeypatch.setenv("DCRT_MATERIAL_LDS", budget)
         t = WavefrontPathTracer(path_pool_size=1 << 14, debug_rng=True)
         try:
             t.set_luts(golden_luts)
             t.on_scene_loaded(s)
-            lds = t.info()["material_lds"]
-            assert (lds > 0) == (budget != "0")
+            sizes[budget] = t.info()["material_lds"]
             t.clear_film()
             t.render_images(0, 3, filt)
             runs[budget] = (t.read_film(), t.read_samples(), t.read_rng())
         finally:
             t.destroy()
-    (fa, (pa, va), ra), (fb, (pb, vb), rb) = runs["16384"], runs["0"]
-    assert np.array_equal(ra, rb) and same_bits(pa, pb).all() and same_bits(va, vb).all() and same_bits(fa, fb).all()
+    assert sizes["16384"] > sizes["1024"] > 0 and sizes["0"] == 0
+    fb, (pb, vb), rb = runs["0"]
+    for budget in ("16384", "1024"):
+        fa, (pa, va), ra = runs[budget]
+        assert np.array_equal(ra, rb) and same_bits(pa, pb).all() and same_bits(va, vb).all() and same_bits(fa, fb).all(), budget
 
 
 @pytest.mark.parametrize("cache,scene_name,pool", [("lds", "cornell", 1 << 15), ("global", "cornell", 1 << 15),
