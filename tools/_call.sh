@@ -2,4 +2,6 @@ set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 8 --warmup 1 --dist-backend gloo --no-cpu-baseline --spaceship-spp 0 > gpurun_out/two_rank.json 2>gpurun_out/two_rank.err; rc=$?; echo "rc=$rc"; tail -c 1500 gpurun_out/two_rank.json; tail -5 gpurun_out/two_rank.err
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+AB_CONFIGS="cornell coffee lamp" PASSES=2 BENCH_ARGS="--repeats 3" bash tools/ab_configs2.sh
