@@ -829,6 +829,10 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
             if (v >= 1 && v < perCU) perCU = v;
         }
         castResident = (uint32_t)std::max(1, perCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        if (const char* m = std::getenv("DCRT_CAST_GRID_MUL")) {   // (A/B: k x resident, workgroups retire in k rounds)
+            const int k = std::atoi(m);
+            if (k >= 2 && k <= 16) castResident *= (uint32_t)k;
+        }
         int opacityPerCU = 0;
         if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, CastKernel(false, true, castAllCached, castPair), (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLds));
