@@ -1514,7 +1514,10 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
         film_pixel_window(c, min((uint32_t)x0 + kFilmTile - 1u, W - 1u), min((uint32_t)y0 + kFilmTile - 1u, H - 1u), W, H,
                           &unused0, &txe, &unused1, &tye);
         const int spanX = txe - txs + 1, spanY = tye - tys + 1;
-        if (spanX > kFilmSpan || spanY > kFilmSpan) {
+#ifndef DCRT_FILM_DIRECT
+#define DCRT_FILM_DIRECT 0
+#endif
+        if (DCRT_FILM_DIRECT || spanX > kFilmSpan || spanY > kFilmSpan) {
             // wide filters: the direct gather from memory
             for (uint32_t b = 0; b < count && mine; ++b) {
                 const float2* sPos = film.samplePosition + (size_t)b * total;
