@@ -479,7 +479,14 @@ DEV bool trav_pop(TravState& s, uint32_t* lds, uint32_t stride)
 // the top, and selects pick the outcome; the lanes of a wave stay convergent.
 // ALL_CACHED: the whole BVH and every triangle sit in the LDS scene cache (small scenes),
 // so node and triangle fetches are plain ds_read_b128 (no FLAT select, no global path).
-template <bool INSTR, bool ALL_CACHED = false, int LAYOUT = kLayoutScene>
+// ENTER (the cache-only, non-opacity kernels): a hit TLAS leaf of an instance whose inverse is
+// exactly the identity (misc bit 0, set at upload in the device node copy: a leaf's split-axis
+// bits are otherwise unused) enters its BLAS here instead of parking for phase B -- for a ray
+// with no zero component that entry changes nothing but the node and the instance (trav_leaf's
+// identity branch), and the BLAS root is the next node visited either way, so the visits, the
+// BLAS-entry count and the hits are the same.
+constexpr uint32_t kMiscIdentityLeaf = 1u;
+template <bool INSTR, bool ALL_CACHED = false, int LAYOUT = kLayoutScene, bool ENTER = false>
 DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
@@ -512,6 +519,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     // leaf: TLAS-leaf bit (4) or a primitive count (bits 3 and up); parked = hit && leaf
     // is formed as hit ^ descend below (a mask operation, not a second compare of misc)
     const bool descend = hit & (misc < 4u);
+    const bool enter = ENTER && (hit & ((misc & (4u | kMiscIdentityLeaf)) == (4u | kMiscIdentityLeaf)) & s.noZero);
     // near/far by the split axis' direction sign (one bit of the space's sign mask);
     // children keep the BLAS bit of the packed node reference
     // (v_bfe takes its offset from the low 5 bits of misc: the split axis for an interior
@@ -533,8 +541,12 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         st.deep12 += s.sp >= 12u * stride ? 1u : 0u;
     }
 #endif
-    s.node = descend ? nearChild : (pop ? top : s.node);
+    s.node = descend ? nearChild : (enter ? (right | 0x80000000u) : (pop ? top : s.node));
     s.sp = descend ? s.sp + stride : (pop ? s.sp - stride : s.sp);
+    if (ENTER) {
+        s.inst = enter ? (misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT : s.inst;
+        if (INSTR && enter) ++st.blas;
+    }
     // rare (about once per ray): a branch the wave skips when no lane restores; as
     // selects it cost nine v_cndmask per visit (measured 2.5 % of the cast kernel)
     if (__builtin_expect(restore, 0)) {
@@ -542,7 +554,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         s.set_space(s.o, s.invW);
         s.negMask = neg_mask(s.d, s.negMask);
     }
-    s.parked = hit ^ descend;
+    s.parked = hit ^ (descend | enter);
     if (!ALL_CACHED) {   // (ALL_CACHED: phase B reads them from the LDS copy of the node)
         s.leafRef = right;
         s.leafMisc = misc;

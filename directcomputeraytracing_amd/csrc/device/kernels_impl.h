@@ -704,6 +704,9 @@ __device__ uint32_t g_waveItems[2][16][8192];
 
 
 constexpr uint32_t kNoItem = 0xFFFFFFFFu;   // a fetch's "no ray for this item"
+#ifndef DCRT_INLINE_ENTRY
+#define DCRT_INLINE_ENTRY 0   // identity-instance BLAS entries in phase A (trav_visit ENTER; A/B)
+#endif
 
 template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, bool PAIR = false,
           int LAYOUT = kLayoutScene, typename Lookup, typename Fetch, typename Emit>
@@ -815,7 +818,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             for (int k = 0; k < kVisitsPerCheck; ++k) {
                 if (ls == kRun) {
                     const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair<false, LAYOUT>(sc, s, lds, shift)
-                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT>(sc, s, lds, shift, st);
+                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, ALL_CACHED && !OPACITY && DCRT_INLINE_ENTRY>(sc, s, lds, shift, st);
                     if (fin) ls = kFin;
                     else if (s.parked) ls = kPark;
                 }

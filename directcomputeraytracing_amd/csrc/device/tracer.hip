@@ -780,6 +780,15 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         }
         // the device node record (dscene.h ray_aabb): DCRT_AXIS_PAIRS stores the box per axis
         std::vector<dcrt_bvh_node> devNodes = castPair ? std::move(pairNodes) : std::vector<dcrt_bvh_node>(s.bvh_nodes, s.bvh_nodes + nodeCount);
+        // the cache-only kernels enter identity instances' BLASes in phase A (dscene.h
+        // kMiscIdentityLeaf): TLAS leaves carry the flag in their otherwise unused axis bits
+        if (castAllCached) {
+            for (dcrt_bvh_node& n : devNodes) {
+                if (!(n.misc & 0x4u)) continue;
+                const uint32_t inst = (n.misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
+                n.misc = (n.misc & ~0x3u) | (inst < s.instance_count && identity[inst] ? kMiscIdentityLeaf : 0u);
+            }
+        }
 #if DCRT_AXIS_PAIRS
         for (dcrt_bvh_node& n : devNodes) {
             const float lo[3] = {n.bbox_min[0], n.bbox_min[1], n.bbox_min[2]}, hi[3] = {n.bbox_max[0], n.bbox_max[1], n.bbox_max[2]};
