@@ -705,7 +705,7 @@ __device__ uint32_t g_waveItems[2][16][8192];
 
 constexpr uint32_t kNoItem = 0xFFFFFFFFu;   // a fetch's "no ray for this item"
 #ifndef DCRT_INLINE_ENTRY
-#define DCRT_INLINE_ENTRY 0   // identity-instance BLAS entries in phase A (trav_visit ENTER; A/B)
+#define DCRT_INLINE_ENTRY 1   // identity-instance BLAS entries in phase A (trav_visit ENTER)
 #endif
 
 template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, bool PAIR = false,
