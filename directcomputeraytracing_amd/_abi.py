@@ -137,7 +137,8 @@ class TracerInfo(C.Structure):
     _fields_ = [("path_pool_size", C.c_uint32), ("scene_in_lds", C.c_uint32), ("cached_nodes", C.c_uint32),
                 ("cached_triangles", C.c_uint32), ("cast_block", C.c_uint32), ("traversal_stack", C.c_uint32),
                 ("material_generic", C.c_uint32), ("pair_traversal", C.c_uint32), ("control_grid", C.c_uint32),
-                ("material_grid", C.c_uint32), ("cast_grid", C.c_uint32), ("material_lds", C.c_uint32)]
+                ("material_grid", C.c_uint32), ("cast_grid", C.c_uint32), ("material_lds", C.c_uint32),
+                ("cast_identity", C.c_uint32)]
 
 
 class MaterialSetting(C.Structure):

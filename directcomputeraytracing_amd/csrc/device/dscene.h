@@ -357,6 +357,23 @@ struct TravState {
 // packed multiplies (v_pk_add_f32 / v_pk_mul_f32, the origin and 1/d component broadcast by
 // op_sel: no extra registers) -- the same IEEE operations per plane as below, so the same
 // bits. Without it, PackBVH's (min.xyz, max.x) (max.yz, right, misc).
+// (IDENT: the world ray's o / 1/d in every space -- see trav_visit)
+DEV bool ray_aabb_raw(V3 o, V3 inv, float tMin, float tMax, float4 a, float4 b)
+{
+    const float tx0 = (a.x - o.x) * inv.x;
+    const float tx1 = (a.w - o.x) * inv.x;
+    float t0 = fminf(tx0, tx1);
+    float t1 = fmaxf(tx0, tx1);
+    const float ty0 = (a.y - o.y) * inv.y;
+    const float ty1 = (b.x - o.y) * inv.y;
+    t0 = fmaxf(t0, fminf(ty0, ty1));
+    t1 = fminf(t1, fmaxf(ty0, ty1));
+    const float tz0 = (a.z - o.z) * inv.z;
+    const float tz1 = (b.y - o.z) * inv.z;
+    t0 = fmaxf(t0, fminf(tz0, tz1));
+    t1 = fminf(t1, fmaxf(tz0, tz1));
+    return (t1 >= t0) & (t0 < tMax) & (t1 >= tMin);
+}
 DEV bool ray_aabb(const TravState& s, float4 a, float4 b)
 {
     const float tMin = s.tMin, tMax = s.tMax;
@@ -453,13 +470,14 @@ template <bool ALL_CACHED>
 DEV uint32_t stack_stride(uint32_t shift) { return ALL_CACHED ? 1024u : 4u << shift; }
 
 // Pop the next node (BVHAccel.inc.hlsl stack pop); true when the stack is empty.
+template <bool IDENT = false>
 DEV bool trav_pop(TravState& s, uint32_t* lds, uint32_t stride)
 {
     if (s.sp == 0u) return true;
     const uint32_t packed = stack_at(lds, s.sp);
     s.sp -= stride;
     s.expand = false;
-    const bool restore = (int)s.node < 0 && (int)packed >= 0;   // BLAS -> TLAS
+    const bool restore = !IDENT && (int)s.node < 0 && (int)packed >= 0;   // BLAS -> TLAS
     s.node = packed;
     if (restore) {
         // component-wise: a struct copy inside the state becomes an alloca-local
@@ -486,7 +504,17 @@ DEV bool trav_pop(TravState& s, uint32_t* lds, uint32_t stride)
 // identity branch), and the BLAS root is the next node visited either way, so the visits, the
 // BLAS-entry count and the hits are the same.
 constexpr uint32_t kMiscIdentityLeaf = 1u;
-template <bool INSTR, bool ALL_CACHED = false, int LAYOUT = kLayoutScene, bool ENTER = false>
+// IDENT (cache-only kernels of scenes whose instances all have exactly the identity inverse, every
+// OBJ scene): no instance space is kept. The instance-space ray of such an instance is the world
+// ray with -0 components turned into +0 (x*1 + y*0 + z*0 + w*0), and that changes no box test's
+// outcome -- a zero direction component gives 1/d = +-inf, and with either sign the slab is
+// (-inf, +inf) when the origin lies strictly inside it and empty otherwise; a -0 origin or
+// plane coordinate changes only the sign of a zero t, which no comparison sees -- nor the
+// near/far order (d < 0 is false for both zeros). So box tests use the world ray in every space,
+// BLAS entries and exits change nothing but the node and instance, and only the triangle tests
+// take the instance-space ray, formed where they need it (o + 0, d + 0: the same bits as the
+// identity transform). The nine registers of the instance-space ray are then free.
+template <bool INSTR, bool ALL_CACHED = false, int LAYOUT = kLayoutScene, bool ENTER = false, bool IDENT = false>
 DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
@@ -513,13 +541,13 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         a = sc.nodes[idx * 2];
         b = sc.nodes[idx * 2 + 1];
     }
-    const bool hit = ray_aabb(s, a, b);
+    const bool hit = IDENT ? ray_aabb_raw(s.o, s.invW, s.tMin, s.tMax, a, b) : ray_aabb(s, a, b);
     const uint32_t misc = asu(b.w);
     const uint32_t right = asu(b.z);
     // leaf: TLAS-leaf bit (4) or a primitive count (bits 3 and up); parked = hit && leaf
     // is formed as hit ^ descend below (a mask operation, not a second compare of misc)
     const bool descend = hit & (misc < 4u);
-    const bool enter = ENTER && (hit & ((misc & (4u | kMiscIdentityLeaf)) == (4u | kMiscIdentityLeaf)) & s.noZero);
+    const bool enter = ENTER && (hit & ((misc & (4u | kMiscIdentityLeaf)) == (4u | kMiscIdentityLeaf)) & (IDENT || s.noZero));
     // near/far by the split axis' direction sign (one bit of the space's sign mask);
     // children keep the BLAS bit of the packed node reference
     // (v_bfe takes its offset from the low 5 bits of misc: the split axis for an interior
@@ -533,7 +561,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     const bool empty = s.sp == 0u;
     const bool pop = !hit && !empty;
     const bool done = !hit && empty;
-    const bool restore = pop && (int)s.node < 0 && (int)top >= 0;    // BLAS -> TLAS: back to the world ray
+    const bool restore = !IDENT && pop && (int)s.node < 0 && (int)top >= 0;    // BLAS -> TLAS: back to the world ray
 #ifdef DCRT_PHASE_CLOCKS
     if (INSTR && descend) {
         st.deep4 += s.sp >= 4u * stride ? 1u : 0u;
@@ -639,7 +667,7 @@ DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uin
 // Phase B: the parked leaf's work. TLAS leaf: move the ray into the instance and
 // continue at its BLAS root. BLAS leaf: test triangles [ref, ref + count), then pop.
 // LANE_ANY: any-hit is a per-lane choice (s.anyHit), for the merged ray-cast kernel
-template <bool ANY_HIT, bool INSTR, bool OPACITY = false, bool LANE_ANY = false, bool ALL_CACHED = false>
+template <bool ANY_HIT, bool INSTR, bool OPACITY = false, bool LANE_ANY = false, bool ALL_CACHED = false, bool IDENT = false>
 DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     s.parked = false;
@@ -650,6 +678,12 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         leafMisc = asu(b.w);
     }
     const uint32_t primOrInst = (leafMisc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
+    if (IDENT && (leafMisc & 0x4u)) {   // (every instance the identity: see trav_visit)
+        s.inst = primOrInst;
+        s.node = leafRef | 0x80000000u;
+        if (INSTR) ++st.blas;
+        return false;
+    }
     if (leafMisc & 0x4u) {
         const float4* M;
         uint32_t identity;
@@ -681,7 +715,11 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
     // the shear of the current space, recomputed at every leaf instead of kept across
     // visits: fewer live registers (the cache-only kernel fits 7 waves/SIMD in 72 VGPRs:
     // 3.03 -> 2.96 ms/spp; coffee / lamp configs -1 to -2 %)
-    if (watertight) s.sh = ALL_CACHED ? make_shear_rot(s.ld, s.lo(), s.inv()) : make_shear(s.ld, s.inv());
+    // (IDENT: the instance-space ray formed here, o + 0 and d + 0; 1/d of its dominant axis --
+    // the only one the shear reads -- is nonzero, so the world ray's)
+    const V3 spO = IDENT ? mk(s.o.x + 0.0f, s.o.y + 0.0f, s.o.z + 0.0f) : s.lo();
+    const V3 spD = IDENT ? mk(s.d.x + 0.0f, s.d.y + 0.0f, s.d.z + 0.0f) : s.ld;
+    if (watertight) s.sh = ALL_CACHED ? make_shear_rot(spD, spO, IDENT ? s.invW : s.inv()) : make_shear(spD, IDENT ? s.invW : s.inv());
     // one triangle test: false = go on, true = the ray is finished (any-hit)
     auto test = [&](uint32_t p) __attribute__((always_inline)) {
         if (INSTR) ++st.tris;
@@ -709,8 +747,8 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
                 q2 = sc.triVerts[(size_t)p * 3 + 2];
             }
             const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
-            h = watertight ? tri_watertight(s.lo(), s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
-                           : tri_moller(s.lo(), s.ld, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
+            h = watertight ? tri_watertight(spO, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
+                           : tri_moller(spO, spD, s.tMin, s.tMax, v0, v1, v2, &t, &u, &v, &bf);
         }
         if (OPACITY && h && !s.opaque) h = any_hit_shader(sc, p, s.matOverride, u, v, s.opacitySample);
         if (h) {
@@ -730,7 +768,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         for (uint32_t p = leafRef; p < end; ++p)
             if (test(p)) return true;
     }
-    return trav_pop(s, lds, stack_stride<ALL_CACHED>(shift));
+    return trav_pop<IDENT>(s, lds, stack_stride<ALL_CACHED>(shift));
 }
 
 // ---- texture emulation ----------------------------------------------------------

@@ -709,7 +709,7 @@ constexpr uint32_t kNoItem = 0xFFFFFFFFu;   // a fetch's "no ray for this item"
 #endif
 
 template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, bool PAIR = false,
-          int LAYOUT = kLayoutScene, typename Lookup, typename Fetch, typename Emit>
+          int LAYOUT = kLayoutScene, bool IDENT = false, typename Lookup, typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
                                                  uint32_t kParkLanes, uint32_t* lds, uint32_t shift, Lookup lookup, Fetch fetch,
                                                  Emit emit, TraversalStats& st, int waveTag = -1)
@@ -818,7 +818,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             for (int k = 0; k < kVisitsPerCheck; ++k) {
                 if (ls == kRun) {
                     const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair<false, LAYOUT>(sc, s, lds, shift)
-                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, ALL_CACHED && !OPACITY && DCRT_INLINE_ENTRY>(sc, s, lds, shift, st);
+                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, ALL_CACHED && !OPACITY && DCRT_INLINE_ENTRY, IDENT>(sc, s, lds, shift, st);
                     if (fin) ls = kFin;
                     else if (s.parked) ls = kPark;
                 }
@@ -843,7 +843,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         // phase B: the parked lanes' leaf work, shared by many lanes at once
         if (__ballot(ls == kPark) != 0ull) DCRT_PHASE_COUNT(5);
         if (ls == kPark)
-            ls = trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED>(sc, s, watertight, lds, shift, st) ? kFin : kRun;
+            ls = trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED, IDENT>(sc, s, watertight, lds, shift, st) ? kFin : kRun;
         DCRT_PHASE(2);
     }
     DCRT_PHASE_FLUSH();
@@ -987,9 +987,15 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
 // iteration instead of two, and a shadow ray can fill a lane an extension ray left
 // idle. Per lane the ray keeps its own semantics (closest hit vs first hit), so the
 // results are those of the two separate kernels.
-template <bool INSTR, bool OPACITY, bool ALL_CACHED, bool PAIR>
+// IDENT: the cache-only kernel of a scene whose instances all have the identity inverse
+// (trav_visit): no instance-space ray, 8 waves/SIMD.
+#ifndef DCRT_IDENT_CAST_WAVES_PER_EU
+#define DCRT_IDENT_CAST_WAVES_PER_EU 8
+#endif
+template <bool INSTR, bool OPACITY, bool ALL_CACHED, bool PAIR, bool IDENT = false>
 __global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHED_CAST_WAVES_PER_EU : DCRT_CAST_WAVES_PER_EU, 8))) void cast_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fc, Counters* cnt,
+__attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? (IDENT ? DCRT_IDENT_CAST_WAVES_PER_EU : DCRT_CACHED_CAST_WAVES_PER_EU)
+                                                                    : DCRT_CAST_WAVES_PER_EU, 8))) void cast_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fc, Counters* cnt,
                                                                      Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];
@@ -1014,7 +1020,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
         const FrameConstants& f = *fc;
         const uint32_t* pixels = sgpr_ptr((const uint32_t*)pool.pixel);
         uint32_t rays = 0;
-        persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout>(
+        persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT>(
             sc, virt, f.features, f.refillLanes, f.parkLanes, stackMem + threadIdx.x, block_shift(),
             [&](uint32_t i) __attribute__((always_inline)) { return i; },
             [&](uint32_t i, uint32_t v, TravState& s) __attribute__((always_inline)) {
@@ -1041,7 +1047,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? DCRT_CACHE
     } else {
     // (node order: the pair kernels run on pair-ordered scenes, the other non-counting ones on
     // PackBVH-ordered ones -- tracer.hip takes both from castPair -- the counting ones on either)
-    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout>(
+    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
             // either kind: its record's position in its queue (no load)
@@ -1811,6 +1817,8 @@ template __global__ void cast_kernel<true, true, false, false>(PathPool, DeviceS
 template __global__ void cast_kernel<true, true, true, false>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void cast_kernel<false, false, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void cast_kernel<false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void megakernel<false>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void megakernel<true>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void batch_trace_kernel<false, false>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);

@@ -111,8 +111,9 @@ uint32_t FilterSupportRows(float r, uint32_t H)
 using CastFn = void (*)(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 // cast_kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER x whole scene in the LDS cache
 // x pair-expanding traversal (the non-counting kernels of scenes not in the LDS cache)
-CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair)
+CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair, bool ident = false)
 {
+    if (ident && allCached && !opacity) return instr ? cast_kernel<true, false, true, false, true> : cast_kernel<false, false, true, false, true>;
     static const CastFn table[8] = {
         cast_kernel<false, false, false, false>, cast_kernel<false, false, true, false>, cast_kernel<false, true, false, false>,
         cast_kernel<false, true, true, false>, cast_kernel<true, false, false, false>, cast_kernel<true, false, true, false>,
@@ -255,6 +256,7 @@ struct dcrt_tracer {
     uint32_t controlGrid = 0, materialGrid = 0;
     uint32_t materialLds = 0;          // MATERIAL's dynamic LDS: the scene copy's bytes (0: the global-memory variant)
     uint32_t materialLdsMode = 0;      // material_kernel<CAPS, mode>: 0 no copy, 1 whole shading data, 2 all but the triangles
+    bool castIdent = false;            // cache-only cast kernel without instance space (every instance the identity: dscene.h IDENT)
     uint32_t iterationsPerRender = kDefaultIterations;
     bool debugRng = false;
     // cast-kernel refill / park thresholds (persistent_trace): refill when 36 lanes are idle
@@ -780,6 +782,21 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         }
         // the device node record (dscene.h ray_aabb): DCRT_AXIS_PAIRS stores the box per axis
         std::vector<dcrt_bvh_node> devNodes = castPair ? std::move(pairNodes) : std::vector<dcrt_bvh_node>(s.bvh_nodes, s.bvh_nodes + nodeCount);
+        // every instance the identity: the cache-only kernel keeps no instance space (IDENT;
+        // DCRT_IDENT_CAST=0: off, A/B)
+        // (bitwise: +1 and +0 entries only -- with a -0 entry the transform of a -0 component could
+        // stay -0, where IDENT's o + 0 gives +0)
+        castIdent = castAllCached && s.instance_count > 0;
+        for (uint32_t i = 0; castIdent && i < s.instance_count; ++i) {
+            const float* m = s.instance_transforms[s.instance_count + i].m;
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 4; ++c) {
+                    uint32_t bits;
+                    std::memcpy(&bits, &m[r * 4 + c], 4);
+                    castIdent = castIdent && bits == (r == c ? 0x3F800000u : 0u);
+                }
+        }
+        if (const char* e = std::getenv("DCRT_IDENT_CAST")) castIdent = castIdent && std::atoi(e) != 0;
         // the cache-only kernels enter identity instances' BLASes in phase A (dscene.h
         // kMiscIdentityLeaf): TLAS leaves carry the flag in their otherwise unused axis bits
         if (castAllCached) {
@@ -831,7 +848,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         hipDeviceProp_t prop;
         HIPCHECK(hipGetDeviceProperties(&prop, device));
         int perCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, CastKernel(false, false, castAllCached, castPair), (int)castBlock, castLds));
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, CastKernel(false, false, castAllCached, castPair, castIdent), (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false, false>, (int)castBlock, castLds));
         if (const char* b = std::getenv("DCRT_CAST_BLOCKS_PER_CU")) {   // tuning experiments
             const int v = std::atoi(b);
@@ -1087,7 +1104,7 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     if (timed) CHECKED(TimedPair(kTimedCast, &e0, &e1));
     // kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER
     if (mergedCasts) {
-        auto cast = CastKernel(instrCounters, opacity, castAllCached, castPair);
+        auto cast = CastKernel(instrCounters, opacity, castAllCached, castPair, castIdent);
         hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), castLds, stream, e0, e1, 0, pool, scene,
                               (const FrameConstants*)dFrame, cnt, next, dGlobals, dInstr);
     } else {
@@ -1536,6 +1553,7 @@ DCRT_API int dcrt_tracer_get_info(dcrt_tracer* t, dcrt_tracer_info* out)
     out->material_grid = t->materialGrid;
     out->cast_grid = t->castResident;
     out->material_lds = t->materialLds;
+    out->cast_identity = t->castIdent ? 1u : 0u;
     return DCRT_OK;
 }
 

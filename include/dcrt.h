@@ -286,6 +286,8 @@ typedef struct dcrt_tracer_info {
     uint32_t control_grid, material_grid;   /* CONTROL / MATERIAL workgroups per launch  */
     uint32_t cast_grid;           /* persistent cast-kernel workgroups (resident on the chip) */
     uint32_t material_lds;        /* bytes of MATERIAL's LDS scene copy (0: not used)      */
+    uint32_t cast_identity;       /* 1: the cache-only cast kernel without instance space
+                                     (every instance's inverse exactly the identity)       */
 } dcrt_tracer_info;
 
 typedef struct dcrt_tracer dcrt_tracer;

@@ -321,6 +321,39 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
         assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
 
+def test_identity_cast_kernel_bit_exact(native_lib, golden_luts, monkeypatch):
+    """The cache-only cast kernel without instance space (every instance's inverse exactly the
+    identity, as for every OBJ shape: IDENT in dscene.h) against the kernel that keeps it
+    (DCRT_IDENT_CAST=0): the same samples, RNG state, film and ray counts bit for bit, and the
+    instrumented traversal counts (node visits, triangle tests, BLAS entries) equal."""
+    from directcomputeraytracing_amd import FILTER_BOX, FilterParams, WavefrontPathTracer
+    s = cornell(96, 64, 6)
+    filt = FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3)
+    runs = {}
+    for ident in ("1", "0"):
+        monkeypatch.setenv("DCRT_IDENT_CAST", ident)
+        t = WavefrontPathTracer(path_pool_size=1 << 14, debug_rng=True)
+        try:
+            t.set_luts(golden_luts)
+            t.on_scene_loaded(s)
+            info = t.info()
+            assert info["scene_in_lds"] == 1 and info["cast_identity"] == (1 if ident == "1" else 0)
+            t.clear_film()
+            t.render_images(0, 3, filt)
+            film, samples, rng, c = t.read_film(), t.read_samples(), t.read_rng(), t.counters()
+            t.set_instrumentation(True, False)
+            t.reset_stats()
+            t.render_images(0, 2, filt)
+            st = t.traversal_stats()
+            runs[ident] = (film, samples, rng, c, {k: st[k] for k in st if k.endswith(("visits", "tests", "entries"))})
+        finally:
+            t.destroy()
+    (fa, (pa, va), ra, ca, sa), (fb, (pb, vb), rb, cb, sb) = runs["1"], runs["0"]
+    assert np.array_equal(ra, rb) and same_bits(pa, pb).all() and same_bits(va, vb).all() and same_bits(fa, fb).all()
+    assert ca["extension_rays"] == cb["extension_rays"] and ca["shadow_rays"] == cb["shadow_rays"]
+    assert sa == sb and sa["ext_node_visits"] > 0
+
+
 @pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
 def test_material_lds_scene_copy_bit_exact(native_lib, golden_luts, monkeypatch, scene_name):
     """MATERIAL's LDS scene copy (material_kernel<CAPS, 1>: triangles, forward transforms,
