@@ -569,7 +569,14 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         st.deep12 += s.sp >= 12u * stride ? 1u : 0u;
     }
 #endif
-    s.node = descend ? nearChild : (enter ? (right | 0x80000000u) : (pop ? top : s.node));
+    // (three exclusive cases as a select chain on the stack top read at the step's start: as a
+    // nested conditional the compiler branched and sank that read into the pop case -- a second
+    // LDS round trip per popping step)
+    uint32_t nextNode = pop ? top : s.node;
+    nextNode = enter ? (right | 0x80000000u) : nextNode;
+    nextNode = descend ? nearChild : nextNode;
+    asm volatile("" : "+v"(nextNode));
+    s.node = nextNode;
     s.sp = descend ? s.sp + stride : (pop ? s.sp - stride : s.sp);
     if (ENTER) {
         s.inst = enter ? (misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT : s.inst;
