@@ -4,4 +4,4 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
-AB_CONFIGS="cornell coffee" PASSES=3 BENCH_ARGS="--repeats 3" bash tools/ab_configs2.sh
+AB_CONFIGS="cornell coffee spaceship" PASSES=2 BENCH_ARGS="--repeats 3" bash tools/ab_configs2.sh
