@@ -994,8 +994,11 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
 #endif
 template <bool INSTR, bool OPACITY, bool ALL_CACHED, bool PAIR, bool IDENT = false>
 __global__ __launch_bounds__(256)
+#ifndef DCRT_GLOBAL_CAST_WAVES_PER_EU
+#define DCRT_GLOBAL_CAST_WAVES_PER_EU DCRT_CAST_WAVES_PER_EU   // (the global-memory, non-pair kernel; A/B)
+#endif
 __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? (IDENT ? DCRT_IDENT_CAST_WAVES_PER_EU : DCRT_CACHED_CAST_WAVES_PER_EU)
-                                                                    : DCRT_CAST_WAVES_PER_EU, 8))) void cast_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fc, Counters* cnt,
+                                   : (!ALL_CACHED && !PAIR && !OPACITY && !INSTR ? DCRT_GLOBAL_CAST_WAVES_PER_EU : DCRT_CAST_WAVES_PER_EU), 8))) void cast_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fc, Counters* cnt,
                                                                      Counters* nextCnt, Globals* g, unsigned long long* instr)
 {
     extern __shared__ uint32_t stackMem[];

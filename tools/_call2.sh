@@ -2,6 +2,5 @@ set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu.log
-[ $rc -eq 0 ] || exit $rc
-AB_CONFIGS="cornell coffee spaceship" PASSES=2 BENCH_ARGS="--repeats 3" bash tools/ab_configs2.sh
+AB_CONFIGS="coffee lamp" PASSES=2 BENCH_ARGS="--repeats 3" bash tools/ab_configs2.sh
+for lib in a_base b_glob7; do DCRT_LIB=gpu_ab/$lib.so timeout -k 10 300 python bench.py --config coffee --steps 2 --warmup 0 --no-cpu-baseline --repeats 1 --roofline-images 1 --spaceship-spp 0 2>/dev/null | tail -1 | python -c "import sys,json; d=json.loads(sys.stdin.read()); print('$lib', d['roofline']['launch'])"; done
