@@ -744,6 +744,12 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         int regPerCU = 0;
         if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false, false, false>, (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, extension_kernel<false, false>, (int)castBlock, castLds));
+#ifndef DCRT_CAST_LDS_BLOCKS
+#define DCRT_CAST_LDS_BLOCKS 0   // A/B: size the cache for this many workgroups per CU (0: as registers allow)
+#endif
+        int ldsBlocks = DCRT_CAST_LDS_BLOCKS;
+        if (const char* e = std::getenv("DCRT_CAST_LDS_BLOCKS")) ldsBlocks = std::atoi(e);
+        if (ldsBlocks >= 1 && ldsBlocks < regPerCU) regPerCU = ldsBlocks;
         const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
         size_t budget = castLds < perBlock ? perBlock - castLds : 0;
         uint32_t nodeCount = s.bvh_node_count;
@@ -834,7 +840,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
                 else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extension_kernel<false, false>, (int)castBlock, lds));
                 return n;
             };
-            const int target = occupancy(stackLds);
+            const int target = ldsBlocks >= 1 ? std::min(occupancy(stackLds), ldsBlocks) : occupancy(stackLds);
             while (occupancy(castLds) < target && (d.cachedTris > 0 || d.cachedNodes > 0)) {
                 if (d.cachedTris > 0) d.cachedTris -= std::min<uint32_t>(d.cachedTris, 11);   // 528 B
                 else d.cachedNodes -= std::min<uint32_t>(d.cachedNodes, 16);                  // 512 B
