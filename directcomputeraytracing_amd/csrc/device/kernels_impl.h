@@ -818,7 +818,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             for (int k = 0; k < kVisitsPerCheck; ++k) {
                 if (ls == kRun) {
                     const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair<false, LAYOUT>(sc, s, lds, shift)
-                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, ALL_CACHED && !OPACITY && DCRT_INLINE_ENTRY, IDENT>(sc, s, lds, shift, st);
+                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, (ALL_CACHED || IDENT) && !OPACITY && DCRT_INLINE_ENTRY, IDENT>(sc, s, lds, shift, st);
                     if (fin) ls = kFin;
                     else if (s.parked) ls = kPark;
                 }
@@ -1822,6 +1822,8 @@ template __global__ void cast_kernel<false, false, false, true>(PathPool, Device
 template __global__ void cast_kernel<false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void cast_kernel<false, false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void cast_kernel<true, false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, false, false, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<true, false, false, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void megakernel<false>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void megakernel<true>(DeviceScene, const FrameConstants*, Film, Globals*, uint32_t);
 template __global__ void batch_trace_kernel<false, false>(DeviceScene, const dcrt_ray*, uint32_t, uint32_t, dcrt_ray_hit*, uint32_t*, unsigned long long*);

@@ -114,6 +114,7 @@ using CastFn = void (*)(PathPool, DeviceScene, const FrameConstants*, Counters*,
 CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair, bool ident = false)
 {
     if (ident && allCached && !opacity) return instr ? cast_kernel<true, false, true, false, true> : cast_kernel<false, false, true, false, true>;
+    if (ident && !opacity && (instr || !pair)) return instr ? cast_kernel<true, false, false, false, true> : cast_kernel<false, false, false, false, true>;
     static const CastFn table[8] = {
         cast_kernel<false, false, false, false>, cast_kernel<false, false, true, false>, cast_kernel<false, true, false, false>,
         cast_kernel<false, true, true, false>, cast_kernel<true, false, false, false>, cast_kernel<true, false, true, false>,
@@ -744,12 +745,6 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         int regPerCU = 0;
         if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false, false, false>, (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, extension_kernel<false, false>, (int)castBlock, castLds));
-#ifndef DCRT_CAST_LDS_BLOCKS
-#define DCRT_CAST_LDS_BLOCKS 0   // A/B: size the cache for this many workgroups per CU (0: as registers allow)
-#endif
-        int ldsBlocks = DCRT_CAST_LDS_BLOCKS;
-        if (const char* e = std::getenv("DCRT_CAST_LDS_BLOCKS")) ldsBlocks = std::atoi(e);
-        if (ldsBlocks >= 1 && ldsBlocks < regPerCU) regPerCU = ldsBlocks;
         const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
         size_t budget = castLds < perBlock ? perBlock - castLds : 0;
         uint32_t nodeCount = s.bvh_node_count;
@@ -763,6 +758,25 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         castAllCached = castBlock == 256 && d.cachedNodes == nodeCount && d.cachedTris == s.triangle_count &&
                         (size_t)d.cachedNodes * 32 + (size_t)s.triangle_count * 144 + (size_t)s.instance_count * 64 <= budget;
         d.cachedInstances = castAllCached ? s.instance_count : 0u;
+        // A scene the cache does not hold whole: the cache leaves `reserve` bytes of each CU's LDS
+        // free, so workgroups of the other pipeline's kernels (MATERIAL, CONTROL) can be resident
+        // beside the cast's -- with the cache sized to the last byte they could not
+        // (DCRT_CAST_LDS_RESERVE, bytes per CU)
+#ifndef DCRT_CAST_LDS_RESERVE
+#define DCRT_CAST_LDS_RESERVE 12288   // (A/B: coffee -2 to -3 %, lamp -1 %; profiles/r04_ab_round4.txt)
+#endif
+        size_t reserve = DCRT_CAST_LDS_RESERVE;
+        if (const char* e = std::getenv("DCRT_CAST_LDS_RESERVE")) reserve = (size_t)std::max(0, std::atoi(e));
+        reserve = std::min<size_t>(reserve, 163840);
+        if (!castAllCached) {
+            const size_t perBlockR = ((163840 - reserve) / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
+            budget = castLds < perBlockR ? perBlockR - castLds : 0;
+            d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
+            d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
+            if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {
+                if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
+            }
+        }
         // trav_visit_pair where the traversal's fetches miss L2: nodes + triangles beyond an
         // XCD's 4 MiB L2 (DCRT_PAIR_TRAVERSAL=0/1 forces it off / on, A/B and tests)
         castPair = !castAllCached && (size_t)nodeCount * 32 + (size_t)s.triangle_count * 48 > ((size_t)4 << 20);
@@ -774,7 +788,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
             // (the budget from the occupancy of the pair kernel, the one that launches)
             int pairPerCU = 0;
             HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pairPerCU, CastKernel(false, false, false, true), (int)castBlock, castLds));
-            const size_t pairBlock = ((size_t)163840 / (size_t)std::max(1, pairPerCU)) & ~(size_t)15;
+            const size_t pairBlock = ((163840 - reserve) / (size_t)std::max(1, pairPerCU)) & ~(size_t)15;
             budget = castLds < pairBlock ? pairBlock - castLds : 0;
             uint32_t topNodes = 4096;
             if (const char* e = std::getenv("DCRT_TOP_NODES")) topNodes = (uint32_t)std::atoi(e);   // A/B experiments
@@ -792,7 +806,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         // DCRT_IDENT_CAST=0: off, A/B)
         // (bitwise: +1 and +0 entries only -- with a -0 entry the transform of a -0 component could
         // stay -0, where IDENT's o + 0 gives +0)
-        castIdent = castAllCached && s.instance_count > 0;
+        castIdent = (castAllCached || !castPair) && mergedCasts && s.instance_count > 0;
         for (uint32_t i = 0; castIdent && i < s.instance_count; ++i) {
             const float* m = s.instance_transforms[s.instance_count + i].m;
             for (int r = 0; r < 3; ++r)
@@ -805,7 +819,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         if (const char* e = std::getenv("DCRT_IDENT_CAST")) castIdent = castIdent && std::atoi(e) != 0;
         // the cache-only kernels enter identity instances' BLASes in phase A (dscene.h
         // kMiscIdentityLeaf): TLAS leaves carry the flag in their otherwise unused axis bits
-        if (castAllCached) {
+        if (castAllCached || castIdent) {
             for (dcrt_bvh_node& n : devNodes) {
                 if (!(n.misc & 0x4u)) continue;
                 const uint32_t inst = (n.misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
@@ -840,7 +854,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
                 else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extension_kernel<false, false>, (int)castBlock, lds));
                 return n;
             };
-            const int target = ldsBlocks >= 1 ? std::min(occupancy(stackLds), ldsBlocks) : occupancy(stackLds);
+            const int target = occupancy(stackLds);
             while (occupancy(castLds) < target && (d.cachedTris > 0 || d.cachedNodes > 0)) {
                 if (d.cachedTris > 0) d.cachedTris -= std::min<uint32_t>(d.cachedTris, 11);   // 528 B
                 else d.cachedNodes -= std::min<uint32_t>(d.cachedNodes, 16);                  // 512 B

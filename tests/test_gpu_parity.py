@@ -321,12 +321,15 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
         assert same_bits(pos, p_ref).all() and same_bits(val, v_ref).all()
 
 
-def test_identity_cast_kernel_bit_exact(native_lib, golden_luts, monkeypatch):
-    """The cache-only cast kernel without instance space (every instance's inverse exactly the
-    identity, as for every OBJ shape: IDENT in dscene.h) against the kernel that keeps it
-    (DCRT_IDENT_CAST=0): the same samples, RNG state, film and ray counts bit for bit, and the
-    instrumented traversal counts (node visits, triangle tests, BLAS entries) equal."""
+@pytest.mark.parametrize("cached", [True, False])
+def test_identity_cast_kernel_bit_exact(native_lib, golden_luts, monkeypatch, cached):
+    """The cast kernel without instance space (every instance's inverse exactly the identity, as
+    for every OBJ shape: IDENT in dscene.h) against the kernel that keeps it (DCRT_IDENT_CAST=0),
+    as the cache-only kernel and (DCRT_NO_LDS_CACHE=1) as the global-memory one: the same samples,
+    RNG state, film and ray counts bit for bit, and the instrumented traversal counts (node
+    visits, triangle tests, BLAS entries) equal."""
     from directcomputeraytracing_amd import FILTER_BOX, FilterParams, WavefrontPathTracer
+    monkeypatch.setenv("DCRT_NO_LDS_CACHE", "0" if cached else "1")
     s = cornell(96, 64, 6)
     filt = FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3)
     runs = {}
@@ -337,7 +340,7 @@ def test_identity_cast_kernel_bit_exact(native_lib, golden_luts, monkeypatch):
             t.set_luts(golden_luts)
             t.on_scene_loaded(s)
             info = t.info()
-            assert info["scene_in_lds"] == 1 and info["cast_identity"] == (1 if ident == "1" else 0)
+            assert info["scene_in_lds"] == (1 if cached else 0) and info["cast_identity"] == (1 if ident == "1" else 0)
             t.clear_film()
             t.render_images(0, 3, filt)
             film, samples, rng, c = t.read_film(), t.read_samples(), t.read_rng(), t.counters()
