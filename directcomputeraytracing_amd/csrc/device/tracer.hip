@@ -123,6 +123,17 @@ CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair, bool iden
     return table[(instr ? 4 : 0) + (opacity ? 2 : 0) + (allCached ? 1 : 0)];
 }
 
+// Workgroups per CU that a workgroup's LDS allocation allows. hipOccupancyMaxActiveBlocksPerMultiprocessor
+// rounds the allocation to 512 B, but gfx950 allocates LDS in 1280-B granules (160 KiB / 128). Measured
+// on the persistent cast grid (one workgroup per resident slot): 6 x 26944 B and 5 x 32768 B per CU
+// ran with 5 and 4 workgroups resident (the last one as a tail: cast launches +26 % / +29 %), while
+// 6 x 26608 B ran with 6 -- the 1280-B rounding predicts all three (profiles/r04_ab_round4.txt).
+constexpr size_t kLdsPerCU = 163840, kLdsGranule = 1280;
+int LdsResident(size_t lds)
+{
+    return lds ? (int)(kLdsPerCU / ((lds + kLdsGranule - 1) / kLdsGranule * kLdsGranule)) : 1 << 20;
+}
+
 // The LDS stack depth traversal of the uploaded tree needs: the most interior nodes on
 // any root-to-leaf path through a TLAS leaf into its BLAS (each descent pushes the far
 // child; BVHAccel.inc.hlsl:143-154). Children lie after their parent (depth-first
@@ -745,6 +756,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         int regPerCU = 0;
         if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false, false, false>, (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, extension_kernel<false, false>, (int)castBlock, castLds));
+        regPerCU = std::min(regPerCU, LdsResident(castLds));
         const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
         size_t budget = castLds < perBlock ? perBlock - castLds : 0;
         uint32_t nodeCount = s.bvh_node_count;
@@ -788,6 +800,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
             // (the budget from the occupancy of the pair kernel, the one that launches)
             int pairPerCU = 0;
             HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pairPerCU, CastKernel(false, false, false, true), (int)castBlock, castLds));
+            pairPerCU = std::min(pairPerCU, LdsResident(castLds));
             const size_t pairBlock = ((163840 - reserve) / (size_t)std::max(1, pairPerCU)) & ~(size_t)15;
             budget = castLds < pairBlock ? pairBlock - castLds : 0;
             uint32_t topNodes = 4096;
@@ -852,7 +865,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
                 int n = 0;
                 if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, CastKernel(false, false, false, castPair), (int)castBlock, lds));
                 else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extension_kernel<false, false>, (int)castBlock, lds));
-                return n;
+                return std::min(n, LdsResident(lds));
             };
             const int target = occupancy(stackLds);
             while (occupancy(castLds) < target && (d.cachedTris > 0 || d.cachedNodes > 0)) {
@@ -870,6 +883,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         int perCU = 0;
         if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, CastKernel(false, false, castAllCached, castPair, castIdent), (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false, false>, (int)castBlock, castLds));
+        perCU = std::min(perCU, LdsResident(castLds));
         if (const char* b = std::getenv("DCRT_CAST_BLOCKS_PER_CU")) {   // tuning experiments
             const int v = std::atoi(b);
             if (v >= 1 && v < perCU) perCU = v;
@@ -882,14 +896,14 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         int opacityPerCU = 0;
         if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, CastKernel(false, true, castAllCached, castPair), (int)castBlock, castLds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLds));
-        castResidentOpacity = (uint32_t)std::max(1, std::min(opacityPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        castResidentOpacity = (uint32_t)std::max(1, std::min(std::min(opacityPerCU, LdsResident(castLds)), perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int megaPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel<false>, (int)castBlock, castLds));
-        megaResident = (uint32_t)std::max(1, megaPerCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        megaResident = (uint32_t)std::max(1, std::min(megaPerCU, LdsResident(castLds))) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int drainPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&drainPerCU, materialCaps == kCapOpaqueDelta ? drain_kernel<kCapOpaqueDelta> : drain_kernel<kCapAll>,
                                                               (int)castBlock, castLds));
-        drainResident = (uint32_t)std::max(1, drainPerCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        drainResident = (uint32_t)std::max(1, std::min(drainPerCU, LdsResident(castLds))) * (uint32_t)std::max(1, prop.multiProcessorCount);
     }
     HIPCHECK(hipStreamSynchronize(stream));
     hasScene = true;

@@ -1,12 +1,10 @@
 set -u
 cd "${GRAFT_REPO_ROOT}"
-mkdir -p gpurun_out/profiles
+mkdir -p gpurun_out
 export TMPDIR=/tmp
-WORKLOADS="coffee 16 coffee;coffee 16 coffee_noms --no-multiscattering;lamp 16 lamp" bash tools/refresh_profiles.sh || exit $?
-cp gpurun_out/profiles/r04_*_pmc_traffic.json profiles/
-: > gpurun_out/profiles/r04_configs.jsonl
-for item in "cornell" "coffee" "coffee --no-multiscattering" "spaceship" "spaceship_close" "lamp"; do
-  timeout -k 10 400 python bench.py --config $item --steps 16 --warmup 2 --no-cpu-baseline --repeats 3 --roofline-images 16 --spaceship-spp 0 > gpurun_out/cfg.json 2>gpurun_out/cfg.err || exit $?
-  tail -1 gpurun_out/cfg.json >> gpurun_out/profiles/r04_configs.jsonl
-  python -c "import json;d=json.load(open('gpurun_out/cfg.json'));print('$item', d['ms_per_spp'], d['repeat_ms_per_spp'], d['value'], d['roofline'].get('frac'), d.get('pipeline_roofline',{}).get('frac'), d['roofline'].get('frac_algorithmic'), d['material']['avg_launch_us'])"
-done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+AB_CONFIGS="spaceship spaceship_close" AB_STEPS=8 PASSES=2 BENCH_ARGS="--repeats 3" AB_VARIANTS="guard
+guard_nocache DCRT_NO_LDS_CACHE=1
+guard_blk5 DCRT_CAST_BLOCKS_PER_CU=5" bash tools/ab_env2.sh
+for cfg in spaceship coffee lamp cornell; do timeout -k 10 300 python bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline --repeats 1 --roofline-images 1 --spaceship-spp 0 2>/dev/null | tail -1 | python -c "import sys,json; d=json.loads(sys.stdin.read()); print('$cfg', d['roofline']['launch'])" || exit 1; done
