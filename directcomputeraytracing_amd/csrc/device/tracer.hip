@@ -748,6 +748,10 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
     // dscene.h); keep a workgroup's stack <= 32 KiB
     castBlock = 256;
     while (castBlock > 64 && (size_t)(d.stackSize + 2) * castBlock * 4 > 32768) castBlock >>= 1;
+    if (const char* e = std::getenv("DCRT_CAST_BLOCK")) {   // (A/B: 64 / 128 / 256, at most the default)
+        const uint32_t v = (uint32_t)std::atoi(e);
+        if ((v == 64 || v == 128 || v == 256) && v <= castBlock) castBlock = v;
+    }
     castLds = (size_t)(d.stackSize + 2) * castBlock * 4;
     if (castLds > 65536) { SetLastError("BVH traversal stack too deep for LDS"); return DCRT_E_LIMIT; }
     {
