@@ -78,6 +78,8 @@ struct DeviceScene {
     uint32_t triangleCount;
     uint32_t envCubeSize;
     uint32_t stackSize;           // per-lane traversal stack entries
+    uint32_t stackRows;           // LDS stack rows per lane: stackSize + 2, or + 1 for the compact pair layout
+    uint32_t pushCapRows;         // the highest row a push writes: stackSize + 1, or stackSize (compact)
     uint32_t cachedNodes;         // nodes [0, cachedNodes) are mirrored in LDS (scene_cache_load)
     uint32_t cachedTris;          // triVerts of triangles [0, cachedTris) likewise, after the nodes
     uint32_t cachedInstances;     // 0, or instanceCount: every inverse transform + identity flag, after the triangles
@@ -124,7 +126,7 @@ DEV void node_children(const DeviceScene& sc, uint32_t node, uint32_t right, uin
 
 DEV float4* scene_cache(const DeviceScene& sc, uint32_t* stackMem, uint32_t shift)
 {
-    return (float4*)(stackMem + ((sc.stackSize + 2u) << shift));
+    return (float4*)(stackMem + (sc.stackRows << shift));
 }
 // Triangles of the cache-only variant (ALL_CACHED kernels) are stored three times, once
 // per watertight-test axis permutation: copy z holds every vertex as (v[z+1], v[z+2], v[z])
@@ -648,8 +650,11 @@ DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uin
     const uint32_t takeRef = hitA ? aRef : bRef;
     const uint32_t right = asu(hitA ? b0.z : b1.z);
     const uint32_t misc = asu(hitA ? b0.w : b1.w);
-    stack_at(lds, s.sp + stride) = bRef;
     const bool push = hitA & hitB;
+    // (the branch-free push: at row count + 1, at most pushCapRows. In the compact layout
+    // (stackSize + 1 rows) a full stack, which never pushes, writes its own top back to the top
+    // row instead of a spare row above it; otherwise the written row is unused)
+    stack_at(lds, min(s.sp + stride, sc.pushCapRows * stride)) = push ? bRef : top;
     const bool empty = s.sp == 0u;
     const bool pop = !take && !empty;
     const bool done = !take && empty;

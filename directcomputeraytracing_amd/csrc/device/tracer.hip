@@ -291,6 +291,9 @@ struct dcrt_tracer {
     bool hasScene = false;
     uint32_t castBlock = 256;
     size_t castLds = 0;
+    size_t castLdsFull = 0;            // the layout of every kernel but the compact pair cast: stackSize + 2 rows
+    bool compactStack = false;         // DCRT_COMPACT_STACK: the pair cast kernel on stackSize + 1 rows
+    DeviceScene sceneCompact{};
     bool castAllCached = false;        // the scene fits the LDS cache: cast_kernel<., ., true, .>
     bool castPair = false;             // trav_visit_pair: the scene outgrows an XCD's L2 (UploadScene)
     bool mergedCasts = true;           // one cast_kernel per iteration (DCRT_SPLIT_CASTS=1: EXT then SHADOW)
@@ -752,6 +755,12 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         const uint32_t v = (uint32_t)std::atoi(e);
         if ((v == 64 || v == 128 || v == 256) && v <= castBlock) castBlock = v;
     }
+    d.stackRows = d.stackSize + 2u;
+    d.pushCapRows = d.stackSize + 1u;
+    // (DCRT_COMPACT_STACK, A/B: the pair cast kernel drops the top spare row -- decided below,
+    // once castPair is known; castLds then counts its rows, castLdsFull the other kernels')
+    bool compactWanted = false;
+    if (const char* e = std::getenv("DCRT_COMPACT_STACK")) compactWanted = std::atoi(e) != 0;
     castLds = (size_t)(d.stackSize + 2) * castBlock * 4;
     if (castLds > 65536) { SetLastError("BVH traversal stack too deep for LDS"); return DCRT_E_LIMIT; }
     {
@@ -797,6 +806,8 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         // XCD's 4 MiB L2 (DCRT_PAIR_TRAVERSAL=0/1 forces it off / on, A/B and tests)
         castPair = !castAllCached && (size_t)nodeCount * 32 + (size_t)s.triangle_count * 48 > ((size_t)4 << 20);
         if (const char* pv = std::getenv("DCRT_PAIR_TRAVERSAL")) castPair = !castAllCached && std::atoi(pv) != 0;
+        compactStack = compactWanted && castPair && mergedCasts;
+        if (compactStack) castLds -= (size_t)castBlock * 4;   // (the stack rows only, so far)
         // the node order goes with it (dscene.h kLayoutPairs: the pair kernels assume it, the
         // other non-counting cast kernels assume PackBVH's)
         std::vector<dcrt_bvh_node> pairNodes;
@@ -879,6 +890,10 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
             }
         }
         scene = d;
+        sceneCompact = d;
+        sceneCompact.stackRows = d.stackSize + 1u;
+        sceneCompact.pushCapRows = d.stackSize;
+        castLdsFull = castLds + (compactStack ? (size_t)castBlock * 4 : 0);
     }
     {
         // The persistent traversal kernels run exactly one resident wave of workgroups.
@@ -898,16 +913,16 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
             if (k >= 2 && k <= 16) castResident *= (uint32_t)k;
         }
         int opacityPerCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, CastKernel(false, true, castAllCached, castPair), (int)castBlock, castLds));
-        else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLds));
-        castResidentOpacity = (uint32_t)std::max(1, std::min(std::min(opacityPerCU, LdsResident(castLds)), perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, CastKernel(false, true, castAllCached, castPair), (int)castBlock, castLdsFull));
+        else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLdsFull));
+        castResidentOpacity = (uint32_t)std::max(1, std::min(std::min(opacityPerCU, LdsResident(castLdsFull)), perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int megaPerCU = 0;
-        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel<false>, (int)castBlock, castLds));
-        megaResident = (uint32_t)std::max(1, std::min(megaPerCU, LdsResident(castLds))) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel<false>, (int)castBlock, castLdsFull));
+        megaResident = (uint32_t)std::max(1, std::min(megaPerCU, LdsResident(castLdsFull))) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int drainPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&drainPerCU, materialCaps == kCapOpaqueDelta ? drain_kernel<kCapOpaqueDelta> : drain_kernel<kCapAll>,
-                                                              (int)castBlock, castLds));
-        drainResident = (uint32_t)std::max(1, std::min(drainPerCU, LdsResident(castLds))) * (uint32_t)std::max(1, prop.multiProcessorCount);
+                                                              (int)castBlock, castLdsFull));
+        drainResident = (uint32_t)std::max(1, std::min(drainPerCU, LdsResident(castLdsFull))) * (uint32_t)std::max(1, prop.multiProcessorCount);
     }
     HIPCHECK(hipStreamSynchronize(stream));
     hasScene = true;
@@ -1143,22 +1158,24 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     // kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER
     if (mergedCasts) {
         auto cast = CastKernel(instrCounters, opacity, castAllCached, castPair, castIdent);
-        hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), castLds, stream, e0, e1, 0, pool, scene,
+        const bool compact = compactStack && !instrCounters && !opacity;   // (the compact pair kernel)
+        hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), compact ? castLds : castLdsFull, stream, e0, e1, 0, pool,
+                              compact ? sceneCompact : scene,
                               (const FrameConstants*)dFrame, cnt, next, dGlobals, dInstr);
     } else {
         auto ext = instrCounters ? (opacity ? extension_kernel<true, true> : extension_kernel<true, false>)
                                  : (opacity ? extension_kernel<false, true> : extension_kernel<false, false>);
         auto shadow = instrCounters ? (opacity ? shadow_kernel<true, true> : shadow_kernel<true, false>)
                                     : (opacity ? shadow_kernel<false, true> : shadow_kernel<false, false>);
-        hipExtLaunchKernelGGL(ext, dim3(castGrid), dim3(castBlock), castLds, stream, e0, e1, 0, pool, scene,
+        hipExtLaunchKernelGGL(ext, dim3(castGrid), dim3(castBlock), castLdsFull, stream, e0, e1, 0, pool, scene,
                               (const FrameConstants*)dFrame, (const Counters*)cnt, dGlobals, dInstr);
-        hipLaunchKernelGGL(shadow, dim3(castGrid), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
+        hipLaunchKernelGGL(shadow, dim3(castGrid), dim3(castBlock), castLdsFull, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
                            next, dGlobals, dInstr);
     }
     if (drainPaths) {
         // (returns at once unless the batch's last paths are few enough: fc.drainPaths)
         auto drain = materialCaps == kCapOpaqueDelta ? drain_kernel<kCapOpaqueDelta> : drain_kernel<kCapAll>;
-        hipLaunchKernelGGL(drain, dim3(drainResident), dim3(castBlock), castLds, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
+        hipLaunchKernelGGL(drain, dim3(drainResident), dim3(castBlock), castLdsFull, stream, pool, scene, (const FrameConstants*)dFrame, cnt,
                            dGlobals, (const SampleOut*)dSampleOut);
     }
     if (sequenced) {
@@ -1305,7 +1322,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (extTiming) CHECKED(TimedPair(kTimedCast, &e0, &e1));
             auto mk = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) ? megakernel<true> : megakernel<false>;
-            hipExtLaunchKernelGGL(mk, dim3(megaResident), dim3(castBlock), castLds, stream, e0, e1, 0, scene,
+            hipExtLaunchKernelGGL(mk, dim3(megaResident), dim3(castBlock), castLdsFull, stream, e0, e1, 0, scene,
                                   (const FrameConstants*)dFrame, film, dGlobals, (uint32_t)(film.debugRng != nullptr));
             hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
                                (const Globals*)nullptr);
@@ -1668,7 +1685,7 @@ static int TraceBatch(dcrt_tracer* t, const dcrt_ray* d_rays, uint32_t n, dcrt_r
     unsigned long long* instr = t->instrCounters ? t->dInstr : nullptr;
     auto kernel = any ? (instr ? batch_trace_kernel<true, true> : batch_trace_kernel<true, false>)
                       : (instr ? batch_trace_kernel<false, true> : batch_trace_kernel<false, false>);
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(t->castBlock), t->castLds, t->stream, t->scene, d_rays, n, features, d_hits, d_occ, instr);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(t->castBlock), t->castLdsFull, t->stream, t->scene, d_rays, n, features, d_hits, d_occ, instr);
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
 }
