@@ -1,12 +1,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT}"
-mkdir -p gpurun_out/profiles
+mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-timeout -k 10 600 python bench.py > gpurun_out/profiles/r04_bench_default.json 2>gpurun_out/bd.err || exit $?
-timeout -k 10 600 python bench.py --steps 20 > gpurun_out/profiles/r04_bench_s20.json 2>gpurun_out/b20.err || exit $?
-python -c "
-import json
-for f in ('r04_bench_default','r04_bench_s20'):
-    d=json.load(open('gpurun_out/profiles/'+f+'.json')); print(f, d['value'], d['ms_per_spp'], d['repeat_ms_per_spp'], 'cast', d['roofline']['avg_launch_us'], d['roofline']['frac'], 'pipe', d['pipeline_roofline']['frac'], 'spaceship', d['spaceship']['ms_per_spp'], d['spaceship']['roofline']['frac'], d['spaceship']['roofline']['avg_launch_us'])
-"
+AB_CONFIGS="coffee lamp" PASSES=2 BENCH_ARGS="--repeats 3" AB_VARIANTS="r12k
+r0 DCRT_CAST_LDS_RESERVE=0" bash tools/ab_env2.sh
+for r in 0 12288; do for cfg in coffee lamp; do DCRT_CAST_LDS_RESERVE=$r timeout -k 10 300 python bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline --repeats 1 --roofline-images 1 --spaceship-spp 0 2>/dev/null | tail -1 | python -c "import sys,json; d=json.loads(sys.stdin.read()); l=d['roofline']['launch']; print('$cfg reserve $r', l['cast_grid'], l['cached_nodes'])" || exit 1; done; done
