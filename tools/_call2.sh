@@ -2,4 +2,5 @@ set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-AB_CONFIGS="spaceship_close spaceship" AB_STEPS=8 PASSES=2 BENCH_ARGS="--repeats 3" bash tools/ab_configs2.sh
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
