@@ -5,7 +5,8 @@ A *step* is N one-sample-per-pixel images of the full film (N = number of GPUs;
 frame seed = image index), rendered by the wavefront pipeline and convolved
 into the fp32 film. Each rank renders its round-robin stripes (+halo) of every
 image, so per-GPU work per step is one full image: weak scaling. ``--gpus N``
-> 1 is launched by torch.distributed.run; one RCCL reduce of the RGBA32F film
+> 1 is launched by torch.distributed.run (started here as a child process when
+the driver did not launch the ranks itself); one RCCL reduce of the RGBA32F film
 closes the timed region.
 
 ``--config coffee|spaceship|lamp`` runs BASELINE.json's other configs (procedural
@@ -168,8 +169,45 @@ def cpu_baseline(scene, luts_arrays, seconds: float, label: str = "1920x1080 8-b
             "ms_per_spp_extrapolated": round(elapsed * 1e3 * H / done_rows, 1)}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(argv, gpus: int, port: int) -> list:
+    """`bench.py --gpus N` started without a launcher: the torch.distributed.run command that
+    starts its N ranks (one process per GPU, rendezvous on 127.0.0.1), same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *argv]
+
+
+def check_world(gpus: int, env=os.environ):
+    """None when this process is a rank of a --gpus-sized job (or a lone --gpus 1 process);
+    "launch" when --gpus N > 1 was given without a launcher (start the ranks as children);
+    otherwise the error message (the launcher's world size differs from --gpus)."""
+    world = env.get("WORLD_SIZE")
+    if world is None:
+        return "launch" if gpus > 1 else None
+    if int(world) != gpus:
+        return f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: the launcher started a different number of ranks"
+    return None
+
+
 def main():
     args = parse()
+    state = check_world(args.gpus)
+    if state == "launch":
+        # Nothing here has touched the GPU (no torch, no libdcrt yet): start the ranks as a
+        # CHILD process tree (never an exec) and relay rank 0's JSON line and the exit code.
+        import subprocess
+        cmd = launcher_command(sys.argv[1:], args.gpus, free_port())
+        print("bench.py: launching " + " ".join(cmd), file=sys.stderr, flush=True)
+        sys.exit(subprocess.run(cmd).returncode)
+    if state is not None:
+        print(state, file=sys.stderr, flush=True)
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -55,6 +55,27 @@ def test_two_rank_bench_film_equals_single_rank(tmp_path):
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def test_bench_gpus_without_launcher_starts_its_ranks(tmp_path):
+    """`python bench.py --gpus 2` with no launcher: bench.py starts torch.distributed.run as a
+    child process (before touching the GPU) and relays rank 0's line, which must say n_gpus 2
+    -- never a silent one-process n_gpus 1 line. Both ranks share the box's one GPU (gloo)."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "1",
+                        "--warmup", "0", "--width", "256", "--height", "144", "--bounces", "4", "--pool", str(1 << 16),
+                        "--no-cpu-baseline", "--roofline-images", "1", "--stripe", "16", "--spaceship-spp", "0",
+                        "--repeats", "1"], capture_output=True, text=True, timeout=900, env=env)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert all(json.loads(l)["n_gpus"] != 1 for l in lines), lines
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 2 and json.loads(lines[0])["multi_gpu"]["world_size"] == 2
+    # a launcher that started a different number of ranks than --gpus: refused before any GPU work
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1"], capture_output=True,
+                       text=True, timeout=120, env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2 and not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
 def test_bench_runs_other_baseline_configs(tmp_path):
     """bench.py --config: BASELINE configs[2] (coffee-like XML scene) through the same
     path; one JSON line with its own metric name and the ray totals."""

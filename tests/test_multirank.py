@@ -158,3 +158,23 @@ def test_gloo_two_rank_film_reduce_is_bit_exact(tmp_path, oracle_mod, golden_lut
         p, v, _, _ = oracle_mod.render(s.flat(), golden_luts, s.frame_params(seed), oracle_mod.WAVEFRONT)
         oracle_mod.sample_convolution(filt, p, v, ref)
     assert np.array_equal(reduced.view(np.uint32), ref.view(np.uint32))
+
+
+def test_bench_world_check_and_launcher_command():
+    """bench.py --gpus N: without a launcher it starts its N ranks (torch.distributed.run on
+    127.0.0.1, same arguments); under a launcher a world size other than --gpus is refused."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.check_world(1, {}) is None
+    assert bench.check_world(8, {}) == "launch"
+    assert bench.check_world(8, {"WORLD_SIZE": "8"}) is None
+    assert bench.check_world(1, {"WORLD_SIZE": "1"}) is None
+    assert "WORLD_SIZE=4" in bench.check_world(8, {"WORLD_SIZE": "4"})
+    assert "WORLD_SIZE=2" in bench.check_world(1, {"WORLD_SIZE": "2"})
+    cmd = bench.launcher_command(["--gpus", "8", "--steps", "5"], 8, 29555)
+    i = cmd.index("torch.distributed.run")
+    assert cmd[i - 1] == "-m" and cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29555"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "5"] and cmd[-5].endswith("bench.py")
