@@ -546,7 +546,8 @@ def cast_roofline(tracer, R, filt, workload_key, traffic_json=None) -> dict:
             "bytes_per_launch": int(bytes_per_launch), "avg_launch_us": round(avg_ms * 1e3, 2),
             "launches": int(launches), "images": R, "scene_in_lds": bool(info["scene_in_lds"]),
             "launch": {k: int(info[k]) for k in ("cast_grid", "cast_block", "cached_nodes", "cached_triangles", "traversal_stack",
-                                                 "pair_traversal", "material_grid", "material_lds", "cast_identity")},
+                                                 "pair_traversal", "material_grid", "material_lds", "cast_identity",
+                                                 "stack_lds_rows", "ring_rows", "cast_waves_per_cu")},
             "extension_rays": int(cr["extension_rays"]), "shadow_rays": int(cr["shadow_rays"]),
             "per_ext_ray": {"nodes": st["ext_node_visits"] / max(1, cr["extension_rays"]),
                             "tris": st["ext_triangle_tests"] / max(1, cr["extension_rays"]),

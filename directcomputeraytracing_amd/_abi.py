@@ -138,7 +138,8 @@ class TracerInfo(C.Structure):
                 ("cached_triangles", C.c_uint32), ("cast_block", C.c_uint32), ("traversal_stack", C.c_uint32),
                 ("material_generic", C.c_uint32), ("pair_traversal", C.c_uint32), ("control_grid", C.c_uint32),
                 ("material_grid", C.c_uint32), ("cast_grid", C.c_uint32), ("material_lds", C.c_uint32),
-                ("cast_identity", C.c_uint32)]
+                ("cast_identity", C.c_uint32), ("stack_lds_rows", C.c_uint32), ("ring_rows", C.c_uint32),
+                ("cast_waves_per_cu", C.c_uint32)]
 
 
 class MaterialSetting(C.Structure):
@@ -246,6 +247,7 @@ SIGNATURES = [
     ("dcrt_tracer_traversal_stats", _I, [_P, C.POINTER(TraversalStats)]),
     ("dcrt_tracer_reset_stats", _I, [_P]),
     ("dcrt_tracer_get_info", _I, [_P, C.POINTER(TracerInfo)]),
+    ("dcrt_tracer_debug_ring_spills", _I, [_P, C.POINTER(C.c_uint64)]),
     ("dcrt_tracer_synchronize", _I, [_P]),
     ("dcrt_tracer_get_luts", _I, [_P, C.POINTER(BxDFLuts)]),
     ("dcrt_tracer_set_luts", _I, [_P, C.POINTER(BxDFLuts)]),

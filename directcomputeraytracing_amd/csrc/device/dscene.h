@@ -78,8 +78,13 @@ struct DeviceScene {
     uint32_t triangleCount;
     uint32_t envCubeSize;
     uint32_t stackSize;           // per-lane traversal stack entries
-    uint32_t stackRows;           // LDS stack rows per lane: stackSize + 2, or + 1 for the compact pair layout
-    uint32_t pushCapRows;         // the highest row a push writes: stackSize + 1, or stackSize (compact)
+    uint32_t stackRows;           // LDS stack rows per lane: stackSize + 2, or ringRows (RING kernels)
+    // RING kernels (persistent_trace): the LDS holds a window of ringRows (a power of two, >= 8) of
+    // the lane's stack as a ring -- entry e at row e mod ringRows -- and the entries below the
+    // window live in `spill`, a [stackSize][lanes of the grid] column per lane (entry e of global
+    // lane gl at spill[(e - 1) * lanes + gl]). 0: the whole stack in LDS.
+    uint32_t ringRows;
+    uint32_t* spill;
     uint32_t cachedNodes;         // nodes [0, cachedNodes) are mirrored in LDS (scene_cache_load)
     uint32_t cachedTris;          // triVerts of triangles [0, cachedTris) likewise, after the nodes
     uint32_t cachedInstances;     // 0, or instanceCount: every inverse transform + identity flag, after the triangles
@@ -164,11 +169,6 @@ DEV void scene_cache_load(const DeviceScene& sc, uint32_t* stackMem, uint32_t sh
 }
 
 // ---- ray / primitive tests ----------------------------------------------------
-#ifndef DCRT_AXIS_PAIRS
-#define DCRT_AXIS_PAIRS 0
-#endif
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
 struct Shear {
     int kx, ky, kz;
     float sx, sy, sz;
@@ -310,30 +310,16 @@ struct TraversalStats {
 
 struct TravState {
     V3 o, d, invW;        // world ray and 1/d (restored on BLAS -> TLAS without dividing again)
-    // ray in the current space (world or instance): direction ld, origin and 1/d kept as the
-    // three register pairs the packed slab test reads, (lo.x, lo.y), (inv.x, inv.y), (lo.z, inv.z)
-    // (without DCRT_AXIS_PAIRS: plain vectors -- the pairs' alignment costs the global-memory
-    // cast kernels 3 VGPRs)
+    // ray in the current space (world or instance): direction ld, origin and 1/d
     V3 ld;
-#if DCRT_AXIS_PAIRS
-    f32x2 loXY, invXY, loZinvZ;
-    DEV V3 lo() const { return mk(loXY.x, loXY.y, loZinvZ.x); }
-    DEV V3 inv() const { return mk(invXY.x, invXY.y, loZinvZ.y); }
-    DEV void set_space(V3 o, V3 i)
-    {
-        loXY = (f32x2){o.x, o.y};
-        invXY = (f32x2){i.x, i.y};
-        loZinvZ = (f32x2){o.z, i.z};
-    }
-#else
     V3 lo_, inv_;
     DEV V3 lo() const { return lo_; }
     DEV V3 inv() const { return inv_; }
     DEV void set_space(V3 o, V3 i) { lo_ = o; inv_ = i; }
-#endif
     float tMin, tMax;
     uint32_t node;        // node index | 0x80000000 in a BLAS (the stack entries' packing)
     uint32_t sp;          // stack entries x stride (bytes): see stack_at
+    uint32_t base;        // RING kernels: entries spilled below the LDS window, x stride (ring_maintain)
     uint32_t inst;
     uint32_t leafRef, leafMisc;   // the visited leaf whose work is pending (parked; not kept with ALL_CACHED)
     bool found, parked, noZero;   // noZero: no component of o, d is +-0
@@ -353,12 +339,7 @@ struct TravState {
     bool opaque;              // the current instance's INSTANCE_FLAG_OPAQUE
 };
 
-// Device node record (tracer.hip UploadScene): with DCRT_AXIS_PAIRS the box is stored per axis,
-// (min.x, max.x, min.y, max.y) (min.z, max.z, right, misc), so each slab's two planes sit in
-// one aligned register pair and the slab test runs as three packed-f32 subtractions and three
-// packed multiplies (v_pk_add_f32 / v_pk_mul_f32, the origin and 1/d component broadcast by
-// op_sel: no extra registers) -- the same IEEE operations per plane as below, so the same
-// bits. Without it, PackBVH's (min.xyz, max.x) (max.yz, right, misc).
+// Slab test on PackBVH's node record (min.xyz, max.x) (max.yz, right, misc).
 // (IDENT: the world ray's o / 1/d in every space -- see trav_visit)
 DEV bool ray_aabb_raw(V3 o, V3 inv, float tMin, float tMax, float4 a, float4 b)
 {
@@ -379,20 +360,6 @@ DEV bool ray_aabb_raw(V3 o, V3 inv, float tMin, float tMax, float4 a, float4 b)
 DEV bool ray_aabb(const TravState& s, float4 a, float4 b)
 {
     const float tMin = s.tMin, tMax = s.tMax;
-#if DCRT_AXIS_PAIRS
-    const f32x2 px = (f32x2){a.x, a.y}, py = (f32x2){a.z, a.w}, pz = (f32x2){b.x, b.y};
-    // (each of the ray's six values broadcast from its register pair by op_sel)
-    const f32x2 tx = (px - s.loXY.xx) * s.invXY.xx;
-    const f32x2 ty = (py - s.loXY.yy) * s.invXY.yy;
-    const f32x2 tz = (pz - s.loZinvZ.xx) * s.loZinvZ.yy;
-    float t0 = fminf(tx.x, tx.y);
-    float t1 = fmaxf(tx.x, tx.y);
-    t0 = fmaxf(t0, fminf(ty.x, ty.y));
-    t1 = fminf(t1, fmaxf(ty.x, ty.y));
-    t0 = fmaxf(t0, fminf(tz.x, tz.y));
-    t1 = fminf(t1, fmaxf(tz.x, tz.y));
-    return (t1 >= t0) & (t0 < tMax) & (t1 >= tMin);
-#else
     const V3 o = s.lo(), inv = s.inv();
     const float tx0 = (a.x - o.x) * inv.x;
     const float tx1 = (a.w - o.x) * inv.x;
@@ -407,7 +374,6 @@ DEV bool ray_aabb(const TravState& s, float4 a, float4 b)
     t0 = fmaxf(t0, fminf(tz0, tz1));
     t1 = fminf(t1, fmaxf(tz0, tz1));
     return (t1 >= t0) & (t0 < tMax) & (t1 >= tMin);   // (bitwise: no exec-mask branch per node)
-#endif
 }
 
 // BVHAccel.inc.hlsl's near/far test `dir[axis] < 0` for all three axes at once, kept per
@@ -424,7 +390,7 @@ DEV void trav_init(TravState& s, V3 o, V3 d, float tMin, float tMax, bool f2b = 
     s.o = o; s.d = d; s.invW = inv_dir(d);
     s.ld = d; s.set_space(o, inv_dir(d));
     s.tMin = tMin; s.tMax = tMax;
-    s.node = 0; s.sp = 0; s.inst = 0;
+    s.node = 0; s.sp = 0; s.base = 0; s.inst = 0;
     s.leafRef = 0; s.leafMisc = 0;
     s.found = false; s.parked = false; s.anyHit = false;
     s.expand = false; s.expNeg = false; s.expRight = 0;
@@ -470,13 +436,20 @@ DEV uint32_t& stack_at(uint32_t* lds, uint32_t byteOffset) { return *(uint32_t*)
 // becomes the ds_write's immediate offset
 template <bool ALL_CACHED>
 DEV uint32_t stack_stride(uint32_t shift) { return ALL_CACHED ? 1024u : 4u << shift; }
+// The LDS row of stack position `byteOffset` (entries x stride): itself, or in a RING kernel the
+// position modulo the window (sc.ringRows rows; a power of two, so one AND with a uniform mask)
+template <bool RING>
+DEV uint32_t stack_row(const DeviceScene& sc, uint32_t byteOffset, uint32_t shift)
+{
+    return RING ? byteOffset & ((sc.ringRows << (shift + 2u)) - 1u) : byteOffset;
+}
 
 // Pop the next node (BVHAccel.inc.hlsl stack pop); true when the stack is empty.
-template <bool IDENT = false>
-DEV bool trav_pop(TravState& s, uint32_t* lds, uint32_t stride)
+template <bool IDENT = false, bool RING = false>
+DEV bool trav_pop(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t stride, uint32_t shift)
 {
     if (s.sp == 0u) return true;
-    const uint32_t packed = stack_at(lds, s.sp);
+    const uint32_t packed = stack_at(lds, stack_row<RING>(sc, s.sp, shift));
     s.sp -= stride;
     s.expand = false;
     const bool restore = !IDENT && (int)s.node < 0 && (int)packed >= 0;   // BLAS -> TLAS
@@ -516,7 +489,7 @@ constexpr uint32_t kMiscIdentityLeaf = 1u;
 // BLAS entries and exits change nothing but the node and instance, and only the triangle tests
 // take the instance-space ray, formed where they need it (o + 0, d + 0: the same bits as the
 // identity transform). The nine registers of the instance-space ray are then free.
-template <bool INSTR, bool ALL_CACHED = false, int LAYOUT = kLayoutScene, bool ENTER = false, bool IDENT = false>
+template <bool INSTR, bool ALL_CACHED = false, int LAYOUT = kLayoutScene, bool ENTER = false, bool IDENT = false, bool RING = false>
 DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
@@ -528,7 +501,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
 #endif
     // the stack top (read only by a pop) is issued together with the node fetch: this
     // visit's push writes the row above it, so the two LDS round trips of a visit overlap
-    const uint32_t top = stack_at(lds, s.sp);
+    const uint32_t top = stack_at(lds, stack_row<RING>(sc, s.sp, shift));
     const uint32_t idx = s.node & 0x7FFFFFFFu;
     float4 a, b;
     if (ALL_CACHED) {
@@ -559,7 +532,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     node_children<LAYOUT>(sc, s.node, right, &next, &rightRef);
     const uint32_t nearChild = neg ? rightRef : next;
     const uint32_t farChild = neg ? next : rightRef;
-    stack_at(lds, s.sp + stride) = farChild;
+    stack_at(lds, stack_row<RING>(sc, s.sp + stride, shift)) = farChild;
     const bool empty = s.sp == 0u;
     const bool pop = !hit && !empty;
     const bool done = !hit && empty;
@@ -614,11 +587,11 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
 // * a far child that hits at the parent is pushed and tested again when popped (visit).
 // The stack holds a subset of the reference's entries (a push needs both children to hit),
 // so the uploaded stack size bounds it too.
-template <bool ALL_CACHED = false, int LAYOUT = kLayoutScene>
+template <bool ALL_CACHED = false, int LAYOUT = kLayoutScene, bool RING = false>
 DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift)
 {
     const uint32_t stride = stack_stride<ALL_CACHED>(shift);
-    const uint32_t top = stack_at(lds, s.sp);
+    const uint32_t top = stack_at(lds, stack_row<RING>(sc, s.sp, shift));
     const uint32_t blasBit = s.node & 0x80000000u;
     // record A: the node itself (visit) or its near child (expand); record B: the far child
     // (expand only)
@@ -651,10 +624,8 @@ DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uin
     const uint32_t right = asu(hitA ? b0.z : b1.z);
     const uint32_t misc = asu(hitA ? b0.w : b1.w);
     const bool push = hitA & hitB;
-    // (the branch-free push: at row count + 1, at most pushCapRows. In the compact layout
-    // (stackSize + 1 rows) a full stack, which never pushes, writes its own top back to the top
-    // row instead of a spare row above it; otherwise the written row is unused)
-    stack_at(lds, min(s.sp + stride, sc.pushCapRows * stride)) = push ? bRef : top;
+    // (the branch-free push: row count + 1 is written either way, and is unused unless pushed)
+    stack_at(lds, stack_row<RING>(sc, s.sp + stride, shift)) = bRef;
     const bool empty = s.sp == 0u;
     const bool pop = !take && !empty;
     const bool done = !take && empty;
@@ -679,7 +650,8 @@ DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uin
 // Phase B: the parked leaf's work. TLAS leaf: move the ray into the instance and
 // continue at its BLAS root. BLAS leaf: test triangles [ref, ref + count), then pop.
 // LANE_ANY: any-hit is a per-lane choice (s.anyHit), for the merged ray-cast kernel
-template <bool ANY_HIT, bool INSTR, bool OPACITY = false, bool LANE_ANY = false, bool ALL_CACHED = false, bool IDENT = false>
+template <bool ANY_HIT, bool INSTR, bool OPACITY = false, bool LANE_ANY = false, bool ALL_CACHED = false, bool IDENT = false,
+          bool RING = false>
 DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     s.parked = false;
@@ -780,7 +752,7 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         for (uint32_t p = leafRef; p < end; ++p)
             if (test(p)) return true;
     }
-    return trav_pop<IDENT>(s, lds, stack_stride<ALL_CACHED>(shift));
+    return trav_pop<IDENT, RING>(sc, s, lds, stack_stride<ALL_CACHED>(shift), shift);
 }
 
 // ---- texture emulation ----------------------------------------------------------

@@ -19,12 +19,6 @@ constexpr uint32_t kFlagDelta = 0x10000000u;           // the path's last BSDF l
 constexpr uint32_t kFlagFirst = 0x08000000u;           // a new path's state record holds NEW_PATH's rng only (PathStateA)
 constexpr uint32_t kFlagShadowPending = 0x04000000u;   // the path cast a shadow ray last pass: its result is at its position
 constexpr uint32_t kBlockW = 8, kBlockH = 8;           // one wave64 = one 8x8 pixel block
-// DCRT_XCD_DEAL: the cast kernels deal queue chunks to the workgroups sharing an XCD
-// (persistent_trace), and a batch's images alternate block by block (block_pixel)
-#ifndef DCRT_XCD_DEAL
-#define DCRT_XCD_DEAL 0
-#endif
-constexpr bool kBlockInterleave = DCRT_XCD_DEAL != 0;
 #ifndef DCRT_CONTROL_BLOCK
 #define DCRT_CONTROL_BLOCK 256
 #endif
@@ -356,20 +350,11 @@ DEV Rng new_path(const FrameConstants& fc, uint32_t p, V3* o, V3* d)
 
 // Pixel of lane `lane` in claimed block `block` of the batch: image, then 8-row group,
 // then 8-column block. False for lanes outside the film or past the last rendered row.
-// (interleave != 0: the batch's `interleave` images alternate block by block -- block b is
-// block b / interleave of image b % interleave -- so a stretch of the batch's blocks, and of the
-// queues that follow their order, is one screen region of every image: DCRT_XCD_DEAL)
 DEV bool block_pixel(const FrameConstants& fc, const Film& film, uint32_t block, uint32_t lane, uint32_t* px, uint32_t* py,
-                     uint32_t* image, uint32_t interleave = 0)
+                     uint32_t* image)
 {
-    uint32_t local;
-    if (interleave) {
-        local = block / interleave;
-        *image = block - local * interleave;
-    } else {
-        *image = block / fc.blocksPerImage;
-        local = block - *image * fc.blocksPerImage;
-    }
+    *image = block / fc.blocksPerImage;
+    const uint32_t local = block - *image * fc.blocksPerImage;
     const uint32_t band = local / fc.blocksX, bx = local - band * fc.blocksX;
     const uint32_t ri = band * kBlockH + lane / kBlockW;
     *px = bx * kBlockW + (lane % kBlockW);

@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
             const uint32_t vb = base / kControlBlock;
             const uint32_t claimed = (vb / kShards) * (kControlBlock >> 6) + (threadIdx.x >> 6);
             uint32_t pixel = kNoPixel, px = 0, py = 0, image = 0;
-            if (claimed < shardBlocks && block_pixel(*fc, film, shard + claimed * kShards, lane, &px, &py, &image, kBlockInterleave ? g->batchImages : 0u)) {
+            if (claimed < shardBlocks && block_pixel(*fc, film, shard + claimed * kShards, lane, &px, &py, &image)) {
                 pixel = image * (film.width * film.height) + py * film.width + px;
                 pool.flags[tid] = 0u;   // busy
             }
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     rng.s0 = rng.s1 = rng.s2 = rng.s3 = 0u;
     if (got) {
         uint32_t px = 0, py = 0, image = 0;
-        if (block_pixel(*fc, film, block, lane, &px, &py, &image, kBlockInterleave ? g->batchImages : 0u)) {
+        if (block_pixel(*fc, film, block, lane, &px, &py, &image)) {
             // NEW_PATH :211-237 (image `image` of the batch has frame seed frameSeed + image)
             rng = rng_init(px, py, fc->frameSeed + image);
             const float psx = next1(rng), psy = next1(rng);
@@ -708,8 +708,45 @@ constexpr uint32_t kNoItem = 0xFFFFFFFFu;   // a fetch's "no ray for this item"
 #define DCRT_INLINE_ENTRY 1   // identity-instance BLAS entries in phase A (trav_visit ENTER)
 #endif
 
+// RING stacks: the lane's LDS stack is a window of sc.ringRows entries (dscene.h stack_row) over
+// a per-lane global column (sc.spill). Before every batch of kVisitsPerCheck node visits the wave
+// checks that each lane's window can take the batch: a visit writes the row above its top (push or
+// not), so the window must hold at most ringRows - 1 entries before each visit, i.e. at most
+// ringRows - 3 before the batch; and a visit (or the following leaf work) pops at most one entry,
+// so with entries spilled below the window it must hold at least kVisitsPerCheck + 1. A lane
+// outside those bounds moves entries between the window and its spill column until the window
+// holds ringRows / 2 (or every entry). The entries' values and order are untouched: traversal,
+// hits and counts are those of the whole-stack kernels bit for bit.
+template <bool RING>
+__device__ __forceinline__ void ring_maintain(const DeviceScene& sc, TravState& s, bool active, uint32_t* lds, uint32_t shift)
+{
+    if constexpr (RING) {
+        const uint32_t stride = 4u << shift;
+        const uint32_t live = s.sp - s.base;
+        const bool spill = active && live > (sc.ringRows - 3u) * stride;
+        const bool fill = active && s.base != 0u && live <= (uint32_t)kVisitsPerCheck * stride;
+        if (__builtin_expect(__ballot(spill | fill) != 0ull, 0)) {
+            const uint32_t lanes = gridDim.x * blockDim.x;
+            uint32_t* col = sc.spill + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+            const uint32_t half = (sc.ringRows >> 1) * stride;
+            const uint32_t target = s.sp > half ? s.sp - half : 0u;   // the new base
+            if (spill) {
+                // positions base + 1 .. target go to the column (entry e at col[(e - 1) * lanes])
+                for (uint32_t p = s.base + stride; p <= target; p += stride)
+                    col[(size_t)((p >> (shift + 2u)) - 1u) * lanes] = stack_at(lds, stack_row<true>(sc, p, shift));
+                s.base = target;
+            } else if (fill) {
+                // positions target + 1 .. base come back into the window
+                for (uint32_t p = target + stride; p <= s.base; p += stride)
+                    stack_at(lds, stack_row<true>(sc, p, shift)) = col[(size_t)((p >> (shift + 2u)) - 1u) * lanes];
+                s.base = target;
+            }
+        }
+    }
+}
+
 template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, bool PAIR = false,
-          int LAYOUT = kLayoutScene, bool IDENT = false, typename Lookup, typename Fetch, typename Emit>
+          int LAYOUT = kLayoutScene, bool IDENT = false, bool RING = false, typename Lookup, typename Fetch, typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
                                                  uint32_t kParkLanes, uint32_t* lds, uint32_t shift, Lookup lookup, Fetch fetch,
                                                  Emit emit, TraversalStats& st, int waveTag = -1)
@@ -718,29 +755,8 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
     const bool f2b = (features & DCRT_FEATURE_NO_FRONT_TO_BACK) == 0;
     const uint32_t wavesPerBlock = blockDim.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    // XCD-aware split (DCRT_XCD_DEAL): the queue is cut into chunks of C items dealt
-    // round-robin to the 8 groups of workgroups that share an XCD (blockIdx mod 8 labels them),
-    // each group dealing its chunks among its own waves as below. With the batch's images
-    // interleaved block by block (kBlockInterleave) a chunk is one screen region of every image,
-    // so a group's node and triangle fetches stay within fewer regions' working sets in its L2;
-    // 8 chunks per group spread over the queue keep the groups' costs even.
-    uint32_t waves = gridDim.x * wavesPerBlock;
-    uint32_t waveId = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
-    uint32_t xcdGroup = 0, lgChunk = 0;
-    const bool xcdDeal = DCRT_XCD_DEAL && (gridDim.x & 7u) == 0u && n >= 64u * 64u;
-    if (xcdDeal) {
-        xcdGroup = blockIdx.x & 7u;
-        lgChunk = 31u - (uint32_t)__clz((int)(n >> 6));   // C = 2^lgChunk <= n / 64
-        const uint32_t C = 1u << lgChunk, full = n >> (lgChunk + 3u), rem = n - (full << (lgChunk + 3u));
-        const uint32_t before = xcdGroup << lgChunk;
-        n = (full << lgChunk) + (rem > before ? min(rem - before, C) : 0u);
-        waves = (gridDim.x >> 3) * wavesPerBlock;
-        waveId = (blockIdx.x >> 3) * wavesPerBlock + (threadIdx.x >> 6);
-    }
-    // the queue item of the group's j-th item
-    auto groupItem = [&](uint32_t j) {
-        return xcdDeal ? ((((j >> lgChunk) << 3) + xcdGroup) << lgChunk) + (j & ((1u << lgChunk) - 1u)) : j;
-    };
+    const uint32_t waves = gridDim.x * wavesPerBlock;
+    const uint32_t waveId = blockIdx.x * wavesPerBlock + (threadIdx.x >> 6);
     // Work split: the queue is cut into groups of kInterleave consecutive items (one
     // region of the image / one producer workgroup each) dealt round-robin to the
     // waves, so every wave samples the whole queue and per-wave costs even out
@@ -799,8 +815,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         if (refill) {
             const uint32_t idx = itemIndex(k);
             if (free && k < end && idx < n) {
-                const uint32_t qi = groupItem(idx);
-                item = fetch(qi, lookup(qi), s);
+                item = fetch(idx, lookup(idx), s);
                 if (!f2b) s.negMask = 0u;
                 // (kNoItem: the queue item has no ray -- a hole of a virtual batch start)
                 ls = item != kNoItem ? kRun : kIdle;
@@ -814,11 +829,12 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         // (a lane whose ray ends here only flags it: the result is written at the next
         // refill point, which keeps the stores out of the unrolled visit steps)
         for (;;) {
+            ring_maintain<RING>(sc, s, ls == kRun || ls == kPark, lds, shift);
 #pragma unroll
             for (int k = 0; k < kVisitsPerCheck; ++k) {
                 if (ls == kRun) {
-                    const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair<false, LAYOUT>(sc, s, lds, shift)
-                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, (ALL_CACHED || IDENT) && !OPACITY && DCRT_INLINE_ENTRY, IDENT>(sc, s, lds, shift, st);
+                    const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair<false, LAYOUT, RING>(sc, s, lds, shift)
+                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, (ALL_CACHED || IDENT) && !OPACITY && DCRT_INLINE_ENTRY, IDENT, RING>(sc, s, lds, shift, st);
                     if (fin) ls = kFin;
                     else if (s.parked) ls = kPark;
                 }
@@ -843,7 +859,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         // phase B: the parked lanes' leaf work, shared by many lanes at once
         if (__ballot(ls == kPark) != 0ull) DCRT_PHASE_COUNT(5);
         if (ls == kPark)
-            ls = trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED, IDENT>(sc, s, watertight, lds, shift, st) ? kFin : kRun;
+            ls = trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED, IDENT, RING>(sc, s, watertight, lds, shift, st) ? kFin : kRun;
         DCRT_PHASE(2);
     }
     DCRT_PHASE_FLUSH();
@@ -992,7 +1008,9 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
 #ifndef DCRT_IDENT_CAST_WAVES_PER_EU
 #define DCRT_IDENT_CAST_WAVES_PER_EU 8
 #endif
-template <bool INSTR, bool OPACITY, bool ALL_CACHED, bool PAIR, bool IDENT = false>
+// RING: the traversal stack as an LDS window over a per-lane global column (ring_maintain), for
+// scenes whose whole stack would cost LDS occupancy (tracer.hip UploadScene).
+template <bool INSTR, bool OPACITY, bool ALL_CACHED, bool PAIR, bool IDENT = false, bool RING = false>
 __global__ __launch_bounds__(256)
 #ifndef DCRT_GLOBAL_CAST_WAVES_PER_EU
 #define DCRT_GLOBAL_CAST_WAVES_PER_EU DCRT_CAST_WAVES_PER_EU   // (the global-memory, non-pair kernel; A/B)
@@ -1023,7 +1041,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? (IDENT ? D
         const FrameConstants& f = *fc;
         const uint32_t* pixels = sgpr_ptr((const uint32_t*)pool.pixel);
         uint32_t rays = 0;
-        persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT>(
+        persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT, RING>(
             sc, virt, f.features, f.refillLanes, f.parkLanes, stackMem + threadIdx.x, block_shift(),
             [&](uint32_t i) __attribute__((always_inline)) { return i; },
             [&](uint32_t i, uint32_t v, TravState& s) __attribute__((always_inline)) {
@@ -1050,7 +1068,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? (IDENT ? D
     } else {
     // (node order: the pair kernels run on pair-ordered scenes, the other non-counting ones on
     // PackBVH-ordered ones -- tracer.hip takes both from castPair -- the counting ones on either)
-    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT>(
+    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT, RING>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
             // either kind: its record's position in its queue (no load)
@@ -1526,10 +1544,7 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
         film_pixel_window(c, min((uint32_t)x0 + kFilmTile - 1u, W - 1u), min((uint32_t)y0 + kFilmTile - 1u, H - 1u), W, H,
                           &unused0, &txe, &unused1, &tye);
         const int spanX = txe - txs + 1, spanY = tye - tys + 1;
-#ifndef DCRT_FILM_DIRECT
-#define DCRT_FILM_DIRECT 0
-#endif
-        if (DCRT_FILM_DIRECT || spanX > kFilmSpan || spanY > kFilmSpan) {
+        if (spanX > kFilmSpan || spanY > kFilmSpan) {
             // wide filters: the direct gather from memory
             for (uint32_t b = 0; b < count && mine; ++b) {
                 const float2* sPos = film.samplePosition + (size_t)b * total;

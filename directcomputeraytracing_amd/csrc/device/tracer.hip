@@ -110,9 +110,15 @@ uint32_t FilterSupportRows(float r, uint32_t H)
 
 using CastFn = void (*)(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 // cast_kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER x whole scene in the LDS cache
-// x pair-expanding traversal (the non-counting kernels of scenes not in the LDS cache)
-CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair, bool ident = false)
+// x pair-expanding traversal (the non-counting kernels of scenes not in the LDS cache) x the
+// world ray in every space (IDENT) x the spilling stack window (RING: non-counting, opaque,
+// global-memory kernels)
+CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair, bool ident = false, bool ring = false)
 {
+    if (ring && !instr && !opacity && !allCached) {
+        if (pair) return cast_kernel<false, false, false, true, false, true>;
+        return ident ? cast_kernel<false, false, false, false, true, true> : cast_kernel<false, false, false, false, false, true>;
+    }
     if (ident && allCached && !opacity) return instr ? cast_kernel<true, false, true, false, true> : cast_kernel<false, false, true, false, true>;
     if (ident && !opacity && (instr || !pair)) return instr ? cast_kernel<true, false, false, false, true> : cast_kernel<false, false, false, false, true>;
     static const CastFn table[8] = {
@@ -291,9 +297,10 @@ struct dcrt_tracer {
     bool hasScene = false;
     uint32_t castBlock = 256;
     size_t castLds = 0;
-    size_t castLdsFull = 0;            // the layout of every kernel but the compact pair cast: stackSize + 2 rows
-    bool compactStack = false;         // DCRT_COMPACT_STACK: the pair cast kernel on stackSize + 1 rows
-    DeviceScene sceneCompact{};
+    size_t castLdsFull = 0;            // the layout of every kernel but the ring cast: stackSize + 2 rows + the cache
+    uint32_t ringRows = 0;             // the ring cast kernel's LDS stack window (0: whole stack in LDS)
+    DeviceScene sceneRing{};           // the scene as the ring cast kernel sees it (stackRows = ringRows, spill column)
+    uint32_t castPerCU = 0;            // resident cast workgroups per CU
     bool castAllCached = false;        // the scene fits the LDS cache: cast_kernel<., ., true, .>
     bool castPair = false;             // trav_visit_pair: the scene outgrows an XCD's L2 (UploadScene)
     bool mergedCasts = true;           // one cast_kernel per iteration (DCRT_SPLIT_CASTS=1: EXT then SHADOW)
@@ -756,79 +763,51 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         if ((v == 64 || v == 128 || v == 256) && v <= castBlock) castBlock = v;
     }
     d.stackRows = d.stackSize + 2u;
-    d.pushCapRows = d.stackSize + 1u;
-    // (DCRT_COMPACT_STACK, A/B: the pair cast kernel drops the top spare row -- decided below,
-    // once castPair is known; castLds then counts its rows, castLdsFull the other kernels')
-    bool compactWanted = false;
-    if (const char* e = std::getenv("DCRT_COMPACT_STACK")) compactWanted = std::atoi(e) != 0;
+    d.ringRows = 0u;
+    d.spill = nullptr;
+    ringRows = 0;
     castLds = (size_t)(d.stackSize + 2) * castBlock * 4;
     if (castLds > 65536) { SetLastError("BVH traversal stack too deep for LDS"); return DCRT_E_LIMIT; }
+    // resident workgroups per CU of a cast kernel with `lds` bytes of dynamic LDS: registers and
+    // LDS (gfx950's 1280-B allocation granule, LdsResident)
+    auto castOccupancy = [&](CastFn k, size_t lds, int* out) -> int {
+        int n = 0;
+        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, (int)castBlock, lds));
+        else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extension_kernel<false, false>, (int)castBlock, lds));
+        *out = std::min(n, LdsResident(lds));
+        return DCRT_OK;
+    };
     {
         // LDS scene cache in what the cast kernel's register-limited occupancy leaves of the
         // CU's 160 KiB per workgroup: BVH nodes first, then pre-gathered triangles
         int regPerCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, cast_kernel<false, false, false, false>, (int)castBlock, castLds));
-        else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&regPerCU, extension_kernel<false, false>, (int)castBlock, castLds));
-        regPerCU = std::min(regPerCU, LdsResident(castLds));
+        CHECKED(castOccupancy(cast_kernel<false, false, false, false>, castLds, &regPerCU));
         const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
         size_t budget = castLds < perBlock ? perBlock - castLds : 0;
         uint32_t nodeCount = s.bvh_node_count;
         d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
         d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
-        if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {   // A/B experiments
-            if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
-        }
+        bool noCache = false;
+        if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) noCache = std::atoi(off) != 0;   // A/B experiments, tests
+        if (noCache) d.cachedNodes = d.cachedTris = 0;
         // (the LDS-only variant assumes 256-thread workgroups: its stack stride is a constant)
         // (the cache-only variant keeps three permuted copies of every triangle: 144 B each)
         castAllCached = castBlock == 256 && d.cachedNodes == nodeCount && d.cachedTris == s.triangle_count &&
                         (size_t)d.cachedNodes * 32 + (size_t)s.triangle_count * 144 + (size_t)s.instance_count * 64 <= budget;
         d.cachedInstances = castAllCached ? s.instance_count : 0u;
-        // A scene the cache does not hold whole: the cache leaves `reserve` bytes of each CU's LDS
-        // free, so workgroups of the other pipeline's kernels (MATERIAL, CONTROL) can be resident
-        // beside the cast's -- with the cache sized to the last byte they could not
-        // (DCRT_CAST_LDS_RESERVE, bytes per CU)
-#ifndef DCRT_CAST_LDS_RESERVE
-#define DCRT_CAST_LDS_RESERVE 12288   // (A/B: coffee -2 to -3 %, lamp -1 %; profiles/r04_ab_round4.txt)
-#endif
-        size_t reserve = DCRT_CAST_LDS_RESERVE;
-        if (const char* e = std::getenv("DCRT_CAST_LDS_RESERVE")) reserve = (size_t)std::max(0, std::atoi(e));
-        reserve = std::min<size_t>(reserve, 163840);
-        if (!castAllCached) {
-            const size_t perBlockR = ((163840 - reserve) / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
-            budget = castLds < perBlockR ? perBlockR - castLds : 0;
-            d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
-            d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
-            if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {
-                if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
-            }
-        }
         // trav_visit_pair where the traversal's fetches miss L2: nodes + triangles beyond an
         // XCD's 4 MiB L2 (DCRT_PAIR_TRAVERSAL=0/1 forces it off / on, A/B and tests)
         castPair = !castAllCached && (size_t)nodeCount * 32 + (size_t)s.triangle_count * 48 > ((size_t)4 << 20);
         if (const char* pv = std::getenv("DCRT_PAIR_TRAVERSAL")) castPair = !castAllCached && std::atoi(pv) != 0;
-        compactStack = compactWanted && castPair && mergedCasts;
-        if (compactStack) castLds -= (size_t)castBlock * 4;   // (the stack rows only, so far)
         // the node order goes with it (dscene.h kLayoutPairs: the pair kernels assume it, the
         // other non-counting cast kernels assume PackBVH's)
         std::vector<dcrt_bvh_node> pairNodes;
         if (castPair) {
-            // (the budget from the occupancy of the pair kernel, the one that launches)
-            int pairPerCU = 0;
-            HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pairPerCU, CastKernel(false, false, false, true), (int)castBlock, castLds));
-            pairPerCU = std::min(pairPerCU, LdsResident(castLds));
-            const size_t pairBlock = ((163840 - reserve) / (size_t)std::max(1, pairPerCU)) & ~(size_t)15;
-            budget = castLds < pairBlock ? pairBlock - castLds : 0;
             uint32_t topNodes = 4096;
             if (const char* e = std::getenv("DCRT_TOP_NODES")) topNodes = (uint32_t)std::atoi(e);   // A/B experiments
             if (!PairLayout(s, topNodes, &pairNodes)) { SetLastError("malformed BVH: a node with two parents"); return DCRT_E_INVALID_ARG; }
             nodeCount = (uint32_t)pairNodes.size();
-            d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
-            d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
-            if (const char* off = std::getenv("DCRT_NO_LDS_CACHE")) {
-                if (std::atoi(off)) d.cachedNodes = d.cachedTris = 0;
-            }
         }
-        // the device node record (dscene.h ray_aabb): DCRT_AXIS_PAIRS stores the box per axis
         std::vector<dcrt_bvh_node> devNodes = castPair ? std::move(pairNodes) : std::vector<dcrt_bvh_node>(s.bvh_nodes, s.bvh_nodes + nodeCount);
         // every instance the identity: the cache-only kernel keeps no instance space (IDENT;
         // DCRT_IDENT_CAST=0: off, A/B)
@@ -845,6 +824,49 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
                 }
         }
         if (const char* e = std::getenv("DCRT_IDENT_CAST")) castIdent = castIdent && std::atoi(e) != 0;
+        // The spilling stack (cast_kernel<..., RING>: an LDS window of K rows over a per-lane global
+        // column, kernels_impl.h ring_maintain) where the whole stack costs the launched kernel
+        // resident workgroups: a deep BVH (spaceship: 30 entries = 32 KiB per 256-lane workgroup,
+        // 4 workgroups per CU where its registers allow 6). DCRT_STACK_RING = K (a power of two,
+        // 8..64) forces a window of K rows (tests: K below the scene's depth spills), 0: never.
+        if (!castAllCached && mergedCasts) {
+            int forced = -1;
+            if (const char* e = std::getenv("DCRT_STACK_RING")) forced = std::atoi(e);
+            const uint32_t K = forced > 0 ? (uint32_t)forced : 16u;
+            const bool validK = K >= 8u && K <= 64u && (K & (K - 1u)) == 0u;
+            if (forced > 0 && !validK) { SetLastError("DCRT_STACK_RING: a power of two in [8, 64]"); return DCRT_E_INVALID_ARG; }
+            if (forced > 0) {
+                ringRows = K;
+            } else if (forced < 0 && K < d.stackSize + 2u) {
+                int whole = 0, ring = 0;
+                CHECKED(castOccupancy(CastKernel(false, false, false, castPair, castIdent, false), castLds, &whole));
+                CHECKED(castOccupancy(CastKernel(false, false, false, castPair, castIdent, true), (size_t)K * castBlock * 4, &ring));
+                if (ring > whole) ringRows = K;
+            }
+        }
+        // A scene the cache does not hold whole: the cache leaves `reserve` bytes of each CU's LDS
+        // free, so workgroups of the other pipeline's kernels (MATERIAL, CONTROL) can be resident
+        // beside the cast's -- with the cache sized to the last byte they could not
+        // (DCRT_CAST_LDS_RESERVE, bytes per CU)
+#ifndef DCRT_CAST_LDS_RESERVE
+#define DCRT_CAST_LDS_RESERVE 12288   // (A/B: coffee -2 to -3 %, lamp -1 %; profiles/r04_ab_round4.txt)
+#endif
+        size_t reserve = DCRT_CAST_LDS_RESERVE;
+        if (const char* e = std::getenv("DCRT_CAST_LDS_RESERVE")) reserve = (size_t)std::max(0, std::atoi(e));
+        reserve = std::min<size_t>(reserve, 163840);
+        const CastFn launched = CastKernel(false, false, castAllCached, castPair, castIdent, ringRows != 0);
+        // the launched kernel's stack bytes: the ring window, or the whole stack
+        const size_t stackLds = ringRows ? (size_t)ringRows * castBlock * 4 : castLds;
+        if (!castAllCached) {
+            // the cache budget from the occupancy of the kernel that launches
+            int perCU = 0;
+            CHECKED(castOccupancy(launched, stackLds, &perCU));
+            const size_t perBlockR = ((163840 - reserve) / (size_t)std::max(1, perCU)) & ~(size_t)15;
+            budget = stackLds < perBlockR ? perBlockR - stackLds : 0;
+            d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
+            d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
+            if (noCache) d.cachedNodes = d.cachedTris = 0;
+        }
         // the cache-only kernels enter identity instances' BLASes in phase A (dscene.h
         // kMiscIdentityLeaf): TLAS leaves carry the flag in their otherwise unused axis bits
         if (castAllCached || castIdent) {
@@ -854,20 +876,13 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
                 n.misc = (n.misc & ~0x3u) | (inst < s.instance_count && identity[inst] ? kMiscIdentityLeaf : 0u);
             }
         }
-#if DCRT_AXIS_PAIRS
-        for (dcrt_bvh_node& n : devNodes) {
-            const float lo[3] = {n.bbox_min[0], n.bbox_min[1], n.bbox_min[2]}, hi[3] = {n.bbox_max[0], n.bbox_max[1], n.bbox_max[2]};
-            n.bbox_min[0] = lo[0]; n.bbox_min[1] = hi[0]; n.bbox_min[2] = lo[1];
-            n.bbox_max[0] = hi[1]; n.bbox_max[1] = lo[2]; n.bbox_max[2] = hi[2];
-        }
-#endif
         CHECKED(upload(&nodes, devNodes.data(), nodeCount));
-        HIPCHECK(hipStreamSynchronize(stream));   // (pairNodes ends with this block)
+        HIPCHECK(hipStreamSynchronize(stream));   // (devNodes ends with this block)
         d.nodes = (const float4*)nodes;
         d.nodeCount = nodeCount;
         d.pairLayout = castPair ? 1u : 0u;
-        const size_t stackLds = castLds;
-        castLds += (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * (castAllCached ? 144 : 48) + (size_t)d.cachedInstances * 64;
+        const size_t cacheBytes = [&] { return (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * (castAllCached ? 144 : 48) + (size_t)d.cachedInstances * 64; }();
+        size_t launchLds = stackLds + cacheBytes;
         // The budget above divides 160 KiB evenly among the workgroups the registers allow; the
         // LDS is allocated in granules (and the kernel's static LDS comes on top), so the cache
         // could cost a workgroup per CU (the spaceship pair kernel ran 5 of its 6). Trim the
@@ -876,46 +891,41 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         bool trim = true;
         if (const char* e = std::getenv("DCRT_LDS_TRIM")) trim = std::atoi(e) != 0;   // (A/B)
         if (!castAllCached && trim) {
-            auto occupancy = [&](size_t lds) {
-                int n = 0;
-                if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, CastKernel(false, false, false, castPair), (int)castBlock, lds));
-                else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extension_kernel<false, false>, (int)castBlock, lds));
-                return std::min(n, LdsResident(lds));
-            };
-            const int target = occupancy(stackLds);
-            while (occupancy(castLds) < target && (d.cachedTris > 0 || d.cachedNodes > 0)) {
+            int target = 0, now = 0;
+            CHECKED(castOccupancy(launched, stackLds, &target));
+            for (;;) {
+                CHECKED(castOccupancy(launched, launchLds, &now));
+                if (now >= target || (d.cachedTris == 0 && d.cachedNodes == 0)) break;
                 if (d.cachedTris > 0) d.cachedTris -= std::min<uint32_t>(d.cachedTris, 11);   // 528 B
                 else d.cachedNodes -= std::min<uint32_t>(d.cachedNodes, 16);                  // 512 B
-                castLds = stackLds + (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * 48;
+                launchLds = stackLds + (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * 48;
             }
         }
         scene = d;
-        sceneCompact = d;
-        sceneCompact.stackRows = d.stackSize + 1u;
-        sceneCompact.pushCapRows = d.stackSize;
-        castLdsFull = castLds + (compactStack ? (size_t)castBlock * 4 : 0);
+        // every kernel but the ring cast launches with the whole stack (stackSize + 2 rows) in
+        // front of the same cache
+        castLdsFull = castLds + (launchLds - stackLds);
+        castLds = launchLds;
     }
     {
         // The persistent traversal kernels run exactly one resident wave of workgroups.
         hipDeviceProp_t prop;
         HIPCHECK(hipGetDeviceProperties(&prop, device));
         int perCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, CastKernel(false, false, castAllCached, castPair, castIdent), (int)castBlock, castLds));
-        else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, extension_kernel<false, false>, (int)castBlock, castLds));
-        perCU = std::min(perCU, LdsResident(castLds));
+        CHECKED(castOccupancy(CastKernel(false, false, castAllCached, castPair, castIdent, ringRows != 0), castLds, &perCU));
         if (const char* b = std::getenv("DCRT_CAST_BLOCKS_PER_CU")) {   // tuning experiments
             const int v = std::atoi(b);
             if (v >= 1 && v < perCU) perCU = v;
         }
-        castResident = (uint32_t)std::max(1, perCU) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        castPerCU = (uint32_t)std::max(1, perCU);
+        castResident = castPerCU * (uint32_t)std::max(1, prop.multiProcessorCount);
         if (const char* m = std::getenv("DCRT_CAST_GRID_MUL")) {   // (A/B: k x resident, workgroups retire in k rounds)
             const int k = std::atoi(m);
             if (k >= 2 && k <= 16) castResident *= (uint32_t)k;
         }
         int opacityPerCU = 0;
-        if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, CastKernel(false, true, castAllCached, castPair), (int)castBlock, castLdsFull));
-        else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&opacityPerCU, extension_kernel<false, true>, (int)castBlock, castLdsFull));
-        castResidentOpacity = (uint32_t)std::max(1, std::min(std::min(opacityPerCU, LdsResident(castLdsFull)), perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        CHECKED(castOccupancy(CastKernel(false, true, castAllCached, castPair), castLdsFull, &opacityPerCU));
+        castResidentOpacity = (uint32_t)std::max(1, std::min(opacityPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int megaPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel<false>, (int)castBlock, castLdsFull));
         megaResident = (uint32_t)std::max(1, std::min(megaPerCU, LdsResident(castLdsFull))) * (uint32_t)std::max(1, prop.multiProcessorCount);
@@ -923,6 +933,16 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&drainPerCU, materialCaps == kCapOpaqueDelta ? drain_kernel<kCapOpaqueDelta> : drain_kernel<kCapAll>,
                                                               (int)castBlock, castLdsFull));
         drainResident = (uint32_t)std::max(1, std::min(drainPerCU, LdsResident(castLdsFull))) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        if (ringRows) {
+            // the spill columns: stackSize entries per lane of the persistent ring grid
+            uint32_t* spill = nullptr;
+            CHECKED(DeviceAlloc(&spill, (size_t)castResident * castBlock * scene.stackSize, &sceneAllocs));
+            HIPCHECK(hipMemsetAsync(spill, 0, (size_t)castResident * castBlock * scene.stackSize * 4, stream));
+            sceneRing = scene;
+            sceneRing.stackRows = ringRows;
+            sceneRing.ringRows = ringRows;
+            sceneRing.spill = spill;
+        }
     }
     HIPCHECK(hipStreamSynchronize(stream));
     hasScene = true;
@@ -1157,10 +1177,11 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     if (timed) CHECKED(TimedPair(kTimedCast, &e0, &e1));
     // kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER
     if (mergedCasts) {
-        auto cast = CastKernel(instrCounters, opacity, castAllCached, castPair, castIdent);
-        const bool compact = compactStack && !instrCounters && !opacity;   // (the compact pair kernel)
-        hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), compact ? castLds : castLdsFull, stream, e0, e1, 0, pool,
-                              compact ? sceneCompact : scene,
+        const bool ring = ringRows != 0 && !instrCounters && !opacity;   // (the ring kernel; the counting and
+                                                                        // any-hit kernels keep the whole stack)
+        auto cast = CastKernel(instrCounters, opacity, castAllCached, castPair, castIdent, ring);
+        hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), ring ? castLds : castLdsFull, stream, e0, e1, 0, pool,
+                              ring ? sceneRing : scene,
                               (const FrameConstants*)dFrame, cnt, next, dGlobals, dInstr);
     } else {
         auto ext = instrCounters ? (opacity ? extension_kernel<true, true> : extension_kernel<true, false>)
@@ -1609,6 +1630,23 @@ DCRT_API int dcrt_tracer_get_info(dcrt_tracer* t, dcrt_tracer_info* out)
     out->cast_grid = t->castResident;
     out->material_lds = t->materialLds;
     out->cast_identity = t->castIdent ? 1u : 0u;
+    out->stack_lds_rows = t->hasScene ? (t->ringRows ? t->ringRows : t->scene.stackRows) : 0u;
+    out->ring_rows = t->hasScene ? t->ringRows : 0u;
+    out->cast_waves_per_cu = t->castPerCU * (t->castBlock / 64u);
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_debug_ring_spills(dcrt_tracer* t, uint64_t* out)
+{
+    TRACER_GUARD(t);
+    if (!out) return DCRT_E_INVALID_ARG;
+    *out = 0;
+    if (!t->hasScene || !t->ringRows) return DCRT_OK;
+    const size_t n = (size_t)t->castResident * t->castBlock * t->scene.stackSize;
+    std::vector<uint32_t> h(n);
+    HIPCHECK(hipStreamSynchronize(t->stream));
+    HIPCHECK(hipMemcpy(h.data(), t->sceneRing.spill, n * 4, hipMemcpyDeviceToHost));
+    for (const uint32_t w : h) *out += w != 0u;
     return DCRT_OK;
 }
 

@@ -174,6 +174,12 @@ class WavefrontPathTracer:
         check(self._lib.dcrt_tracer_get_info(self._h, C.byref(s)), "GetInfo")
         return {k: getattr(s, k) for k, _ in _abi.TracerInfo._fields_}
 
+    def ring_spills(self) -> int:
+        """Stack entries the spilling-stack cast kernel moved to its global columns (test hook)."""
+        n = C.c_uint64(0)
+        check(self._lib.dcrt_tracer_debug_ring_spills(self._h, C.byref(n)), "DebugRingSpills")
+        return int(n.value)
+
     def reset_stats(self) -> None:
         check(self._lib.dcrt_tracer_reset_stats(self._h), "ResetStats")
 

@@ -288,6 +288,11 @@ typedef struct dcrt_tracer_info {
     uint32_t material_lds;        /* bytes of MATERIAL's LDS scene copy (0: not used)      */
     uint32_t cast_identity;       /* 1: the cache-only cast kernel without instance space
                                      (every instance's inverse exactly the identity)       */
+    uint32_t stack_lds_rows;      /* LDS stack rows per lane of the launched cast kernel: traversal_stack + 2,
+                                     or ring_rows                                          */
+    uint32_t ring_rows;           /* 0, or the LDS window (rows) of a spilling traversal stack: deeper
+                                     entries live in a per-lane global column              */
+    uint32_t cast_waves_per_cu;   /* resident waves per CU of the launched cast kernel      */
 } dcrt_tracer_info;
 
 typedef struct dcrt_tracer dcrt_tracer;
@@ -499,6 +504,10 @@ DCRT_API int dcrt_tracer_set_instrumentation(dcrt_tracer* tracer, int counters, 
 DCRT_API int dcrt_tracer_traversal_stats(dcrt_tracer* tracer, dcrt_traversal_stats* out_stats);
 DCRT_API int dcrt_tracer_reset_stats(dcrt_tracer* tracer);
 DCRT_API int dcrt_tracer_get_info(dcrt_tracer* tracer, dcrt_tracer_info* out_info);
+/* Test hook of the spilling traversal stack (dcrt_tracer_info.ring_rows): the stack entries the
+   ring cast kernel has moved to its spill columns since the scene upload (nonzero words of the
+   zero-initialised columns; no stack entry is 0). 0 when the scene keeps its whole stack in LDS. */
+DCRT_API int dcrt_tracer_debug_ring_spills(dcrt_tracer* tracer, uint64_t* out_words);
 DCRT_API int dcrt_tracer_synchronize(dcrt_tracer* tracer);
 DCRT_API int dcrt_tracer_get_luts(dcrt_tracer* tracer, dcrt_bxdf_luts* out_luts);
 DCRT_API int dcrt_tracer_set_luts(dcrt_tracer* tracer, const dcrt_bxdf_luts* luts);

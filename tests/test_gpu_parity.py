@@ -83,14 +83,17 @@ def _assert_cast_grid_resident(info):
     """The persistent cast grid holds no more workgroups per CU than the LDS does: gfx950
     allocates a workgroup's LDS in 1280-B granules (the HIP occupancy query rounds to 512 B, and
     a grid sized by it ran one workgroup per CU as a tail; tracer.hip LdsResident). Global-memory
-    kernels: stack rows (traversal_stack + 2) x block x 4 B + cached nodes x 32 + triangles x 48."""
+    kernels: stack rows (traversal_stack + 2, or the spilling stack's LDS window) x block x 4 B +
+    cached nodes x 32 + triangles x 48; the resident waves the info reports are that grid's."""
     if info["scene_in_lds"]:
         return
     cus = 256   # MI355X compute units (the cast grid is workgroups per CU x CUs)
     assert info["cast_grid"] % cus == 0, info["cast_grid"]
     per_cu = info["cast_grid"] // cus
-    lds = (info["traversal_stack"] + 2) * info["cast_block"] * 4 + info["cached_nodes"] * 32 + info["cached_triangles"] * 48
+    assert info["stack_lds_rows"] == (info["ring_rows"] or info["traversal_stack"] + 2)
+    lds = info["stack_lds_rows"] * info["cast_block"] * 4 + info["cached_nodes"] * 32 + info["cached_triangles"] * 48
     assert per_cu >= 1 and per_cu * ((lds + 1279) // 1280 * 1280) <= 163840, (per_cu, lds)
+    assert info["cast_waves_per_cu"] == per_cu * info["cast_block"] // 64
 
 
 def _render_and_compare(tracer, oracle_mod, luts, scene, seeds):
@@ -650,18 +653,64 @@ def test_config_scenes_bit_exact(gpu_tracer, golden_luts, oracle_mod, name, cube
     _assert_cast_grid_resident(gpu_tracer.info())
 
 
-@pytest.mark.parametrize("framing", ["wide", "close"])
-def test_full_size_spaceship_mesh_bit_exact(gpu_tracer, golden_luts, oracle_mod, tmp_path, framing):
+@pytest.mark.parametrize("framing,ring", [("wide", None), ("close", None), ("close", "8")])
+def test_full_size_spaceship_mesh_bit_exact(gpu_tracer, golden_luts, oracle_mod, tmp_path, monkeypatch, framing, ring):
     """configs[3] at its full mesh size (261 120 triangles x 8 instances, 522 k BVH nodes,
     stack depth 30: most nodes outside the LDS scene cache), 320x180, 8 bounces, 1 spp; both
-    framings (the close one: hulls fill the frame, paths bounce between them)."""
+    framings (the close one: hulls fill the frame, paths bounce between them). The scene's
+    default is the spilling stack (a 16-row LDS window over per-lane global columns: 6 instead
+    of 4 workgroups per CU); ring "8" forces an 8-row window, so most deep entries spill and
+    come back (ring_maintain). Either way the entries must move: ring_spills() > 0."""
     from directcomputeraytracing_amd import Scene, scenes
+    if ring:
+        monkeypatch.setenv("DCRT_STACK_RING", ring)
     s = Scene((320, 180))
     s.load_from_file(scenes.write_spaceship(tmp_path, 320, 180, nu=512, nv=256, ships=8, framing=framing))
     assert s.bvh_info()["total_nodes"] > 500_000
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [3]))
-    assert gpu_tracer.info()["pair_traversal"] == 1   # (beyond an XCD's L2: trav_visit_pair)
-    _assert_cast_grid_resident(gpu_tracer.info())
+    info = gpu_tracer.info()
+    assert info["pair_traversal"] == 1   # (beyond an XCD's L2: trav_visit_pair)
+    assert info["ring_rows"] == int(ring or 16) and info["stack_lds_rows"] == info["ring_rows"]
+    assert info["cast_waves_per_cu"] >= 24 if ring is None else True
+    assert gpu_tracer.ring_spills() > 0
+    _assert_cast_grid_resident(info)
+
+
+@pytest.mark.parametrize("kernel", ["pair", "global", "ident", "split"])
+@pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
+def test_stack_ring_and_split_casts_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, scene_name, kernel):
+    """The spilling traversal stack forced onto small scenes (DCRT_STACK_RING=8: an 8-row LDS
+    window, entries beyond it in per-lane global columns) in the pair, global-memory and
+    identity-space (IDENT) cast kernels, and the reference's two separate cast kernels
+    (DCRT_SPLIT_CASTS=1: extension_kernel, then shadow_kernel, whole stack): samples, RNG
+    state and ray counts against the oracle."""
+    from conftest import GOLDEN
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer
+    monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+    monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1" if kernel == "pair" else "0")
+    monkeypatch.setenv("DCRT_IDENT_CAST", "1" if kernel == "ident" else "0")
+    if kernel == "split":
+        monkeypatch.setenv("DCRT_SPLIT_CASTS", "1")
+    else:
+        monkeypatch.setenv("DCRT_STACK_RING", "8")
+    if scene_name == "cornell":
+        s = cornell(96, 64, 8)
+    else:
+        s = Scene((48, 40))
+        s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
+    t = WavefrontPathTracer(path_pool_size=1 << 13, debug_rng=True)
+    try:
+        rays = [0, 0]
+        for c, c_ref in _render_and_compare(t, oracle_mod, golden_luts, s, [0, 5]):
+            rays = [rays[0] + c_ref["extension_rays"], rays[1] + c_ref["shadow_rays"]]   # (the tracer's counts accumulate)
+            assert [c["extension_rays"], c["shadow_rays"]] == rays
+        info = t.info()
+        assert info["pair_traversal"] == (1 if kernel == "pair" else 0)
+        assert info["ring_rows"] == (0 if kernel == "split" else 8)
+        if kernel == "ident":
+            assert info["cast_identity"] == (1 if scene_name == "cornell" else 0)
+    finally:
+        t.destroy()
 
 
 @pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
