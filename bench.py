@@ -229,7 +229,7 @@ def main():
         torch.cuda.set_device(device)
 
     import numpy as np
-    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, render_images_concurrently, scenes
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, make_pipelines, render_images_concurrently, scenes
     luts_arrays = dict(np.load(ROOT / "tests" / "golden" / "bxdf_luts.npz"))
 
     scene = Scene((args.width, args.height))
@@ -245,7 +245,7 @@ def main():
     # (the coffee scene without configs[2]'s multiscattering is its own workload)
     config_name = args.config + ("_noms" if args.config == "coffee" and args.no_multiscattering else "")
     filt = scene.filter_params()
-    from directcomputeraytracing_amd.partition import halo_for_radius, pipeline_pool, render_rows, stream_partition
+    from directcomputeraytracing_amd.partition import halo_for_radius, render_rows
     halo = max(1, halo_for_radius(filt.radius, args.height))
 
     def make_tracer(pool, part):
@@ -260,14 +260,11 @@ def main():
     # K concurrent pipelines per GPU (--streams): tracer s renders the rank's stripes dealt
     # to it (partition.stream_partition), on its own stream, from its own host thread; the
     # K films have disjoint supports and are summed on the device (add_film_device).
+    # (a pipeline's pool just short of a whole number of batches grows by <= 8 %: one drain less)
     K = max(1, args.streams)
-    tracers = []
-    for s_ in range(K):
-        part = stream_partition(args.height, world, rank, K, s_, args.stripe) if (K > 1 or world > 1) else None
-        # (a pool just short of a whole number of batches grows by <= 5 %: one drain less)
-        rows = len(render_rows(args.height, *part, halo)) if part is not None else args.height
-        pool = pipeline_pool(args.pool // K, rows, args.width, args.steps * world) if not args.image_batch else args.pool // K
-        tracers.append(make_tracer(pool, part))
+    tracers = make_pipelines(scene, args.pool, streams=K, images=args.steps * world, iterations=args.iterations,
+                             world=world, rank=rank, stripe=args.stripe, mode=args.mode, image_batch=args.image_batch,
+                             device=device)
     tracer = tracers[0]
 
     def render_all(first, count):

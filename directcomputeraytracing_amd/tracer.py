@@ -241,6 +241,38 @@ def device_count() -> int:
     return n.value
 
 
+def make_pipelines(scene, pool: int, streams: int = 2, images: int = 1, iterations: int = 16, world: int = 1,
+                   rank: int = 0, stripe: int = 64, mode: str = "wavefront", image_batch: int = 0, device: int = 0,
+                   debug_rng: bool = False) -> list:
+    """The concurrent wavefront pipelines bench.py renders with (one GPU: `streams` horizontal
+    bands; N GPUs: this rank's stripes dealt to its pipelines, partition.stream_partition), each
+    a tracer with its share of `pool` slots (grown to whole batches of `images` images,
+    partition.pipeline_pool), the filter's halo rows, its own stream. Their films have disjoint
+    supports: add_film_device sums them into the rank's film bit for bit."""
+    from .partition import halo_for_radius, pipeline_pool, render_rows, stream_partition
+    W, H = scene.resolution
+    halo = max(1, halo_for_radius(scene.filter_params().radius, H))
+    K = max(1, streams)
+    tracers = []
+    try:
+        for s_ in range(K):
+            part = stream_partition(H, world, rank, K, s_, stripe) if (K > 1 or world > 1) else None
+            rows = len(render_rows(H, *part, halo)) if part is not None else H
+            p = pipeline_pool(pool // K, rows, W, images) if not image_batch else pool // K
+            t = WavefrontPathTracer(path_pool_size=p, iterations_per_render=iterations, device=device, debug_rng=debug_rng)
+            tracers.append(t)
+            t.on_scene_loaded(scene)
+            t.set_mode(mode)
+            t.set_image_batch(image_batch)
+            if part is not None:
+                t.set_film_partition(*part, halo)
+    except BaseException:
+        for t in tracers:
+            t.destroy()
+        raise
+    return tracers
+
+
 def render_images_concurrently(tracers, first_seed: int, count: int, filter_params=None) -> None:
     """render_images on several tracers at once (one host thread each; the C ABI runs with
     the GIL released and every tracer owns its stream), then synchronize them all. An
