@@ -434,6 +434,79 @@ def write_anyhit(directory: Path | str, width: int = 64, height: int = 48) -> Pa
 CONFIGS = ("cornell", "coffee", "spaceship", "lamp", "spaceship_close")
 
 
+# ---- analytic scenes (tier 6: checks whose answer does not come from the renderer) ----
+# Six rectangles (SceneXMLLoading.cpp:1358-1378: one shared rectangle mesh, an instance per face)
+# form the cube [-1, 1]^3, each face's front (the rectangle's +z) pointing `inward` or outward.
+_CUBE_FACES = [((0, 0, 1), 180, 0), ((0, 0, -1), 0, 0), ((0, 1, 0), 0, 90), ((0, -1, 0), 0, -90),
+               ((1, 0, 0), -90, 0), ((-1, 0, 0), 90, 0)]   # (centre, yaw, pitch): fronts facing the centre
+
+
+def _cube_shapes(inner: str, inward: bool, scale: float = 1.0) -> str:
+    out = ""
+    for (c, yaw, pitch) in _CUBE_FACES:
+        t = tuple(scale * v for v in c)
+        m = mitsuba_matrix(t, yaw=yaw + (0 if inward else 180) if pitch == 0 else yaw, pitch=pitch if inward or pitch == 0 else -pitch,
+                           scale=(scale, scale, 1))
+        out += f'  <shape type="rectangle">{inner}<transform name="to_world"><matrix value="{m}"/></transform></shape>\n'
+    return out
+
+
+def write_emissive_box(directory: Path | str, width: int = 64, height: int = 64, albedo: float = 0.5,
+                       radiance: float = 1.0, max_bounce: int = 8) -> Path:
+    """The camera inside a closed cube whose six faces are diffuse (albedo rho) AND emit Le towards
+    the inside. Every path vertex lies on a wall, so the expected radiance of every pixel is
+    Le * (1 + rho + ... + rho^B) for B bounces: emission seen directly plus, at each of the B
+    vertices that continue, the next vertex's emission weighted by the albedo (cosine-sampled
+    Lambertian: weight rho; light sampling + MIS: the same expectation)."""
+    d = Path(directory)
+    d.mkdir(parents=True, exist_ok=True)
+    inner = (f'<bsdf type="diffuse"><rgb name="reflectance" value="{albedo}, {albedo}, {albedo}"/></bsdf>'
+             f'<emitter type="area"><rgb name="radiance" value="{radiance}, {radiance}, {radiance}"/></emitter>')
+    xml = _xml(f'  <integrator type="path"><integer name="max_depth" value="{max_bounce}"/></integrator>\n'
+               + _sensor("perspective", width, height, mitsuba_matrix((0.1, -0.05, 0.2), yaw=20, pitch=10),
+                         extra='    <float name="fov" value="90"/>\n', rfilter='<rfilter type="box"/>')
+               + _cube_shapes(inner, inward=True))
+    path = d / "emissive_box.xml"
+    path.write_text(xml)
+    return path
+
+
+def write_lit_plane(directory: Path | str, width: int = 64, height: int = 64, albedo: float = 0.6) -> Path:
+    """A diffuse plane (the rectangle [-4, 4]^2 at y = 0, front +y) seen from above, no light and no
+    bounce (max_depth 0): the caller adds a point light, whose direct lighting is then the whole
+    image (known irradiance, tests/test_physics.py)."""
+    d = Path(directory)
+    d.mkdir(parents=True, exist_ok=True)
+    xml = _xml('  <integrator type="path"><integer name="max_depth" value="0"/></integrator>\n'
+               + _sensor("perspective", width, height, mitsuba_matrix((0.0, 3.0, -1.0), pitch=55),
+                         extra='    <float name="fov" value="60"/>\n', rfilter='<rfilter type="box"/>')
+               + f'  <bsdf type="diffuse" id="plane"><rgb name="reflectance" value="{albedo}, {albedo}, {albedo}"/></bsdf>\n'
+               + f'  <shape type="rectangle"><ref id="plane"/><transform name="to_world"><matrix value="{mitsuba_matrix((0, 0, 0), pitch=-90, scale=(4, 4, 1))}"/></transform></shape>\n')
+    path = d / "lit_plane.xml"
+    path.write_text(xml)
+    return path
+
+
+def write_furnace(directory: Path | str, width: int = 64, height: int = 64, bsdf: str | None = None,
+                  radiance: float = 1.0, max_bounce: int = 8) -> Path:
+    """White furnace: a closed cube, fronts outward, under a constant environment of radiance Le,
+    the camera outside at a corner so the cube fills the frame. The cube is convex, so a ray leaving
+    its surface sees the environment: with an energy-conserving BSDF of albedo 1 (diffuse
+    reflectance 1) the expected radiance of every pixel is Le. `bsdf` replaces the material
+    (e.g. a rough conductor, for the Kulla-Conty energy check)."""
+    d = Path(directory)
+    d.mkdir(parents=True, exist_ok=True)
+    inner = bsdf or '<bsdf type="diffuse"><rgb name="reflectance" value="1, 1, 1"/></bsdf>'
+    xml = _xml(f'  <integrator type="path"><integer name="max_depth" value="{max_bounce}"/></integrator>\n'
+               + _sensor("perspective", width, height, mitsuba_matrix((-1.35, 1.3, -1.45), yaw=42, pitch=35),
+                         extra='    <float name="fov" value="30"/>\n', rfilter='<rfilter type="box"/>')
+               + _cube_shapes(inner, inward=False)
+               + f'  <emitter type="constant"><rgb name="radiance" value="{radiance}, {radiance}, {radiance}"/></emitter>\n')
+    path = d / "furnace.xml"
+    path.write_text(xml)
+    return path
+
+
 def setup_config(scene, name: str, scene_dir: Path | str, small: bool = False, multiscattering: bool = True) -> str:
     """BASELINE.json configs[1..4] as procedural scenes (written into `scene_dir`), loaded
     into `scene` at their resolutions; returns a workload description.
