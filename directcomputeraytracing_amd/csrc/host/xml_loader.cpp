@@ -189,6 +189,25 @@ struct Value {
     bool GetBool(const char* n, bool d) const { Value* x = Field(n); return x && x->type == VT::Boolean ? x->b : d; }
     std::string GetString(const char* n, const std::string& d) const { Value* x = Field(n); return x && x->type == VT::String ? x->s : d; }
     Float3 GetVec(const char* n, Float3 d) const { Value* x = Field(n); return x && x->type == VT::Vector ? x->v : d; }
+    // SValue::m_Float read whatever the value holds -- the reference's unchecked reads (alpha :888,
+    // aperture_radius :1241, focus_distance :1244) see the union's first word: an integer's or a
+    // boolean's bits (SValue() zeroes the word, m_Boolean sets its low byte), a vector's x, a
+    // matrix's _11. (A string's or an object's first word is a pointer: undefined, 0 here.)
+    float UnionFloat() const
+    {
+        uint32_t w = 0;
+        switch (type) {
+        case VT::Float: return f;
+        case VT::Integer: std::memcpy(&w, &i, 4); break;
+        case VT::Boolean: w = b ? 1u : 0u; break;
+        case VT::Vector: return v.x;
+        case VT::Matrix: return m.m[0][0];
+        default: return 0.0f;
+        }
+        float r;
+        std::memcpy(&r, &w, 4);
+        return r;
+    }
 };
 
 // strncmp(a, literal, len(a)) == 0 as the reference writes its keyword tests: a
@@ -499,7 +518,7 @@ bool MaterialContext::Translate(const Value& bsdf, SMaterial* m, bool twoSided, 
         m->internalScatteringMode = bsdf.GetBool("nonlinear", false) ? DCRT_INTERNAL_SCATTERING_MULTIPLE : DCRT_INTERNAL_SCATTERING_SINGLE;
     if (rough) {
         Value* a = bsdf.Field("alpha");
-        const float alpha = a ? a->f : 0.1f;
+        const float alpha = a ? a->UnionFloat() : 0.1f;
         m->roughness = std::sqrt(alpha);
     }
     if (dielectricIor) {
@@ -677,9 +696,9 @@ bool LoadMitsubaXML(CScene* scene, const std::string& path)
                 }
             } else if (S.cameraType == ECameraType::ThinLens) {
                 Value* ar = obj.Field("aperture_radius");
-                S.relativeAperture = ar ? S.focalLength / (ar->f * 2) : 8.0f;
+                S.relativeAperture = ar ? S.focalLength / (ar->UnionFloat() * 2) : 8.0f;
                 Value* fd = obj.Field("focus_distance");
-                S.focalDistance = fd ? fd->f : 2.0f;
+                S.focalDistance = fd ? fd->UnionFloat() : 2.0f;
             }
         } else if (KeywordIs(tag, "bsdf")) {
             uint32_t id = 0;
