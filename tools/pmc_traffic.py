@@ -4,7 +4,10 @@
 * PMC passes: FETCH_SIZE and WRITE_SIZE are in KiB (1 KiB = 16 x 64-B
   TCC_EA0_RDREQ, checked against the TCC_EA0_RDREQ_sum pass). Per the MI355X
   guide, gfx950 FETCH_SIZE tallies 128-B requests at 64 B, so read bytes are
-  doubled; WRITE_SIZE is taken as is. Traffic is averaged per launch over the
+  doubled; WRITE_SIZE is taken as is. The doubling holds for the traversal's scattered
+  16/32/64/128-B dependent fetches too: every L2 read request to the fabric is a 128-B
+  request whatever the access width (tools/probe/fetch_calib.hip, tools/fetch_calib.py,
+  profiles/r05_fetch_calibration.txt: FETCH_SIZE x 2 = TCC_EA0_RDREQ_128B x 128 B to 0.2 %). Traffic is averaged per launch over the
   same whole-image launch mix the bench's roofline leg uses.
 
 Usage: python tools/pmc_traffic.py gpurun_out/prof profiles/r02_i20   (-> profiles/r02_i20_pmc_traffic.json)
