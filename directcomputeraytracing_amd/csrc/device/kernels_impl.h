@@ -143,6 +143,11 @@ __global__ void set_idle_kernel(PathPool pool, Counters* counters, Globals* g, u
 
 // Preset the shard cursors for a batch start (see Globals::staticFill): shard s's first
 // min(waves of its CONTROL workgroups, its blocks) blocks are taken statically.
+// Invariant the batch start relies on: every slot is idle when staticFill is set -- the two
+// callers are begin_images_kernel (right after BeginImage's set_idle_kernel) and
+// advance_image_kernel (only once the batch completed: no path was live entering the last
+// iteration and none was started, end_iteration). The static claims (and the virtual start's
+// pixel / flag writes, control_kernel) overwrite the slots without checking them.
 __device__ __forceinline__ void begin_batch_claims(Globals* g)
 {
     const uint32_t G = g->staticGrid, wavesPerGroup = kControlBlock >> 6;

@@ -134,10 +134,19 @@ CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair, bool iden
 // on the persistent cast grid (one workgroup per resident slot): 6 x 26944 B and 5 x 32768 B per CU
 // ran with 5 and 4 workgroups resident (the last one as a tail: cast launches +26 % / +29 %), while
 // 6 x 26608 B ran with 6 -- the 1280-B rounding predicts all three (profiles/r04_ab_round4.txt).
-constexpr size_t kLdsPerCU = 163840, kLdsGranule = 1280;
-int LdsResident(size_t lds)
+// `lds` counts a workgroup's dynamic LDS; the kernel's static LDS (hipFuncAttributes
+// sharedSizeBytes, e.g. the megakernel's claim words) comes on top of it. The per-CU total is the
+// device's (maxSharedMemoryPerMultiProcessor: 160 KiB on gfx950, the only target this library is
+// built for); the 1280-B granule is gfx950's.
+size_t g_ldsPerCU = 163840;
+constexpr size_t kLdsGranule = 1280;
+int LdsResident(size_t lds, const void* kernel = nullptr)
 {
-    return lds ? (int)(kLdsPerCU / ((lds + kLdsGranule - 1) / kLdsGranule * kLdsGranule)) : 1 << 20;
+    if (kernel) {
+        hipFuncAttributes attr{};
+        if (hipFuncGetAttributes(&attr, kernel) == hipSuccess) lds += attr.sharedSizeBytes;
+    }
+    return lds ? (int)(g_ldsPerCU / ((lds + kLdsGranule - 1) / kLdsGranule * kLdsGranule)) : 1 << 20;
 }
 
 // The LDS stack depth traversal of the uploaded tree needs: the most interior nodes on
@@ -501,6 +510,7 @@ int dcrt_tracer::Create(const dcrt_tracer_config& cfg)
         // workgroup (A/B overrides).
         hipDeviceProp_t prop;
         HIPCHECK(hipGetDeviceProperties(&prop, device));
+        if (prop.maxSharedMemoryPerMultiProcessor > 0) g_ldsPerCU = prop.maxSharedMemoryPerMultiProcessor;
         int cPerCU = 0, mPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&cPerCU, control_kernel, (int)kControlBlock, 0));
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&mPerCU, material_kernel<kCapAll, 0>, (int)kMaterialBlock, 0));
@@ -774,7 +784,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         int n = 0;
         if (mergedCasts) HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, (int)castBlock, lds));
         else HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extension_kernel<false, false>, (int)castBlock, lds));
-        *out = std::min(n, LdsResident(lds));
+        *out = std::min(n, LdsResident(lds, mergedCasts ? (const void*)k : (const void*)extension_kernel<false, false>));
         return DCRT_OK;
     };
     {
@@ -782,7 +792,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         // CU's 160 KiB per workgroup: BVH nodes first, then pre-gathered triangles
         int regPerCU = 0;
         CHECKED(castOccupancy(cast_kernel<false, false, false, false>, castLds, &regPerCU));
-        const size_t perBlock = ((size_t)163840 / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
+        const size_t perBlock = (g_ldsPerCU / (size_t)std::max(1, regPerCU)) & ~(size_t)15;
         size_t budget = castLds < perBlock ? perBlock - castLds : 0;
         uint32_t nodeCount = s.bvh_node_count;
         d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
@@ -853,7 +863,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
 #endif
         size_t reserve = DCRT_CAST_LDS_RESERVE;
         if (const char* e = std::getenv("DCRT_CAST_LDS_RESERVE")) reserve = (size_t)std::max(0, std::atoi(e));
-        reserve = std::min<size_t>(reserve, 163840);
+        reserve = std::min<size_t>(reserve, g_ldsPerCU);
         const CastFn launched = CastKernel(false, false, castAllCached, castPair, castIdent, ringRows != 0);
         // the launched kernel's stack bytes: the ring window, or the whole stack
         const size_t stackLds = ringRows ? (size_t)ringRows * castBlock * 4 : castLds;
@@ -861,7 +871,7 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
             // the cache budget from the occupancy of the kernel that launches
             int perCU = 0;
             CHECKED(castOccupancy(launched, stackLds, &perCU));
-            const size_t perBlockR = ((163840 - reserve) / (size_t)std::max(1, perCU)) & ~(size_t)15;
+            const size_t perBlockR = ((g_ldsPerCU - reserve) / (size_t)std::max(1, perCU)) & ~(size_t)15;
             budget = stackLds < perBlockR ? perBlockR - stackLds : 0;
             d.cachedNodes = (uint32_t)std::min<size_t>(nodeCount, budget / 32);
             d.cachedTris = (uint32_t)std::min<size_t>(s.triangle_count, (budget - d.cachedNodes * 32) / 48);
@@ -928,11 +938,15 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         castResidentOpacity = (uint32_t)std::max(1, std::min(opacityPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int megaPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel<false>, (int)castBlock, castLdsFull));
-        megaResident = (uint32_t)std::max(1, std::min(megaPerCU, LdsResident(castLdsFull))) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        megaResident = (uint32_t)std::max(1, std::min(megaPerCU, LdsResident(castLdsFull, (const void*)megakernel<false>))) *
+                       (uint32_t)std::max(1, prop.multiProcessorCount);
         int drainPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&drainPerCU, materialCaps == kCapOpaqueDelta ? drain_kernel<kCapOpaqueDelta> : drain_kernel<kCapAll>,
                                                               (int)castBlock, castLdsFull));
-        drainResident = (uint32_t)std::max(1, std::min(drainPerCU, LdsResident(castLdsFull))) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        drainResident = (uint32_t)std::max(1, std::min(drainPerCU, LdsResident(castLdsFull, materialCaps == kCapOpaqueDelta
+                                                                                                 ? (const void*)drain_kernel<kCapOpaqueDelta>
+                                                                                                 : (const void*)drain_kernel<kCapAll>))) *
+                        (uint32_t)std::max(1, prop.multiProcessorCount);
         if (ringRows) {
             // the spill columns: stackSize entries per lane of the persistent ring grid
             uint32_t* spill = nullptr;

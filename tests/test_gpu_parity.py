@@ -958,3 +958,47 @@ def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle
     bad = np.count_nonzero(~same_bits(film, ref).all(-1))
     assert bad == 0, f"{bad} film pixels differ"
     assert (ext, shadow) == (ext_ref, shadow_ref)
+
+
+KNOB_CASES = [
+    # (id, scene, env): scheduling / sizing knobs of dcrt_tracer::UploadScene and persistent_trace
+    ("block64_global", "xml_mix", {"DCRT_CAST_BLOCK": "64", "DCRT_NO_LDS_CACHE": "1"}),
+    ("block128_pair", "xml_mix", {"DCRT_CAST_BLOCK": "128", "DCRT_NO_LDS_CACHE": "1", "DCRT_PAIR_TRAVERSAL": "1"}),
+    ("blocks_per_cu_2", "lamp", {"DCRT_CAST_BLOCKS_PER_CU": "2"}),
+    ("grid_mul_3", "lamp", {"DCRT_CAST_GRID_MUL": "3"}),
+    ("lds_reserve_0_no_trim", "lamp", {"DCRT_CAST_LDS_RESERVE": "0", "DCRT_LDS_TRIM": "0"}),
+    ("material_lds_not_partial", "lamp", {"DCRT_MATERIAL_LDS_PARTIAL": "0"}),
+    ("top_nodes_64", "spaceship", {"DCRT_PAIR_TRAVERSAL": "1", "DCRT_TOP_NODES": "64"}),
+    ("tune_8_4", "cornell", {"DCRT_TRAVERSAL_TUNE": "8,4"}),
+    ("tune_64_64", "cornell", {"DCRT_TRAVERSAL_TUNE": "64,64", "DCRT_NO_LDS_CACHE": "1"}),
+]
+
+
+@pytest.mark.parametrize("case,scene_name,env", KNOB_CASES, ids=[c[0] for c in KNOB_CASES])
+def test_tuning_knobs_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, case, scene_name, env):
+    """Every A/B knob the tracer reads (workgroup size, resident workgroups per CU, grid multiple,
+    the LDS cache's reserve and trim, MATERIAL's partial LDS copy, the pair order's breadth-first
+    prefix, the refill / park thresholds) changes scheduling or sizing only: the wavefront render
+    stays bit-exact against the oracle."""
+    from conftest import GOLDEN
+    from directcomputeraytracing_amd import Scene, WavefrontPathTracer
+    from test_oracle import load_fixture_scene
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    if scene_name == "cornell":
+        s = cornell(64, 48, 6)
+    elif scene_name == "xml_mix":
+        s = Scene((32, 32))
+        s.load_from_file(GOLDEN / "xml_mix" / "scene.xml")
+    else:
+        s = load_fixture_scene(scene_name)
+    t = WavefrontPathTracer(path_pool_size=1 << 14, debug_rng=True)
+    try:
+        list(_render_and_compare(t, oracle_mod, golden_luts, s, [0, 3]))
+        info = t.info()
+        if "DCRT_CAST_BLOCK" in env:
+            assert info["cast_block"] == int(env["DCRT_CAST_BLOCK"])
+        if "DCRT_CAST_BLOCKS_PER_CU" in env:
+            assert info["cast_grid"] == 2 * 256
+    finally:
+        t.destroy()
