@@ -104,6 +104,42 @@ def build_native(force: bool = False, verbose: bool = False, out: Path | None = 
     return lib_path
 
 
+SANITIZED_LIB = PKG_DIR / "_build_asan" / "libdcrt_asan.so"
+
+
+def build_sanitized(force: bool = False) -> Path:
+    """TEST TOOLING: libdcrt.so with the host code under AddressSanitizer + UBSan (the OBJ / XML
+    parsers, the BVH builder, the scene and C-ABI code; the tracer's host side through
+    -Xarch_host, the device code unchanged). tools/sanitize_host.sh runs the CPU suite against
+    it (DCRT_LIB) with clang's ASan runtime preloaded."""
+    san = ["-fsanitize=address", "-fsanitize=undefined"]
+    sources = HOST_SOURCES + DEVICE_SOURCES
+    digest = _digest(sources + HEADERS) + "asan"
+    stamp = SANITIZED_LIB.with_suffix(".so.sha256")
+    if not force and SANITIZED_LIB.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+        return SANITIZED_LIB
+    objdir = SANITIZED_LIB.parent
+    objdir.mkdir(exist_ok=True)
+    objs, procs = [], []
+    for src in sources:
+        obj = objdir / (src.stem + (".dev.o" if src.suffix == ".hip" else ".o"))
+        if src.suffix == ".cpp":
+            cmd = [_hipcc(), *[f for f in HIPCC_FLAGS if f not in ("--offload-arch=gfx950", "-fno-gpu-rdc", "-O3")], "-O1", "-g",
+                   "-fno-omit-frame-pointer", *san, "-x", "c++", "-c", str(src), "-o", str(obj)]
+        else:
+            cmd = [_hipcc(), *HIPCC_FLAGS, "-g", *[x for f in san for x in ("-Xarch_host", f)], "-c", str(src), "-o", str(obj)]
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        objs.append(obj)
+    for src, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError(f"sanitized build failed: {src}\n{out.decode(errors='replace')}")
+    subprocess.run([_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *san, "-shared-libasan", "-o", str(SANITIZED_LIB),
+                    *map(str, objs)], check=True)
+    stamp.write_text(digest)
+    return SANITIZED_LIB
+
+
 EXAMPLE_SRC = ROOT / "examples" / "dcrt_render.cpp"
 EXAMPLE_BIN = ROOT / "examples" / "dcrt_render"
 

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -94,6 +96,44 @@ FilterConsts MakeFilter(const dcrt_filter_params& p)   // SampleConvolution.cpp:
 // (SampleConvolution.hlsl:77-81), with the kernel's float arithmetic
 // (film_pixel_window): floor(r + 0.5) in exact arithmetic, one more where py + 0.5 + r
 // rounds up to the next integer (r just below k + 0.5).
+// roctx ranges around the host-side passes, named like the reference's PIX annotations
+// (SCOPED_RENDER_ANNOTATION, WavefrontPathTracer.cpp:443-1083): visible in rocprofv3
+// --marker-trace next to the kernels. libroctx64 is opened at run time (no link dependency;
+// absent, or DCRT_ROCTX=0: no ranges). Iterations captured into a hipGraph are annotated by
+// their replay ("RenderImages" / graph chunks), not per kernel.
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+    Roctx()
+    {
+        if (const char* e = std::getenv("DCRT_ROCTX")) {
+            if (std::atoi(e) == 0) return;
+        }
+        void* h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("libroctx64.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+        pop = (int (*)())dlsym(h, "roctxRangePop");
+        if (!push || !pop) push = nullptr, pop = nullptr;
+    }
+};
+const Roctx& roctx()
+{
+    static const Roctx r;
+    return r;
+}
+struct Annotation {
+    bool on;
+    explicit Annotation(const char* name, bool enabled = true) : on(enabled && roctx().push)
+    {
+        if (on) roctx().push(name);
+    }
+    ~Annotation()
+    {
+        if (on) roctx().pop();
+    }
+};
+
 uint32_t FilterSupportRows(float r, uint32_t H)
 {
     if (!(r < (float)H)) return H;
@@ -338,6 +378,7 @@ struct dcrt_tracer {
     Counters* hCounters = nullptr;     // pinned [2]
 
     bool newImage = true;
+    bool capturing = false;            // LaunchIteration is being captured into a graph (no host annotations)
     bool imageComplete = false;
     bool filmClearTrigger = false;
     uint32_t parity = 0;
@@ -609,6 +650,7 @@ int dcrt_tracer::BuildLuts()
 
 int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
 {
+    Annotation an("UploadScene");
     if (!s.vertices || !s.triangles || !s.bvh_nodes || !s.material_ids || !s.instance_transforms || !s.materials ||
         !s.instance_light_indices || !s.instance_flags || !s.instance_material_overrides || s.triangle_count == 0 ||
         s.bvh_node_count == 0 || s.instance_count == 0 || s.material_count == 0) {
@@ -1109,6 +1151,7 @@ int dcrt_tracer::SetPartition(const dcrt_film_partition& p)
 // ResetImage + SET_IDLE + constant upload for one image (WavefrontPathTracer.cpp:441-468)
 int dcrt_tracer::BeginImage()
 {
+    Annotation an("Reset", !capturing);
     FrameConstants fc;
     std::memset(&fc, 0, sizeof(fc));
     std::memcpy(fc.camera, frame.camera_transform, sizeof(fc.camera));
@@ -1157,6 +1200,7 @@ int dcrt_tracer::BeginImage()
 // this iteration completed an image (RenderImages runs images back to back).
 int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
 {
+    Annotation an("Iteration", !capturing);
     Counters* cnt = dCounters + par;
     Counters* next = dCounters + (par ^ 1u);   // (the previous iteration's; the casts clear them for the next)
     PathPool pool = this->pool;
@@ -1178,18 +1222,25 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     // (hipExtLaunchKernelGGL), so the duration is the kernel's, as rocprofv3 reports it.
     hipEvent_t c0 = nullptr, c1 = nullptr, m0 = nullptr, m1 = nullptr, e0 = nullptr, e1 = nullptr;
     if (timed) CHECKED(TimedPair(kTimedControl, &c0, &c1));
-    hipExtLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, c0, c1, 0, pool, film,
-                          (const FrameConstants*)dFrame, cnt, (const Counters*)next, dGlobals, (uint32_t)(film.debugRng != nullptr));
+    {
+        Annotation a("Control", !capturing);
+        hipExtLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, c0, c1, 0, pool, film,
+                              (const FrameConstants*)dFrame, cnt, (const Counters*)next, dGlobals, (uint32_t)(film.debugRng != nullptr));
+    }
     auto material = materialCaps == kCapOpaqueDelta
                         ? (materialLdsMode == 1 ? material_kernel<kCapOpaqueDelta, 1>
                                                 : materialLdsMode == 2 ? material_kernel<kCapOpaqueDelta, 2> : material_kernel<kCapOpaqueDelta, 0>)
                         : (materialLdsMode == 1 ? material_kernel<kCapAll, 1>
                                                 : materialLdsMode == 2 ? material_kernel<kCapAll, 2> : material_kernel<kCapAll, 0>);
     if (timed) CHECKED(TimedPair(kTimedMaterial, &m0, &m1));
-    hipExtLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), materialLds, stream, m0, m1, 0, pool, scene,
-                          (const FrameConstants*)dFrame, cnt, (const Counters*)next, (const SampleOut*)dSampleOut);
+    {
+        Annotation a("Material", !capturing);
+        hipExtLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), materialLds, stream, m0, m1, 0, pool, scene,
+                              (const FrameConstants*)dFrame, cnt, (const Counters*)next, (const SampleOut*)dSampleOut);
+    }
     if (timed) CHECKED(TimedPair(kTimedCast, &e0, &e1));
     // kernel variant: instrumented counts x ALLOW_ANYHIT_SHADER
+    Annotation castAnnotation(mergedCasts ? "Extension + shadow ray cast" : "Extension ray cast, shadow ray cast", !capturing);
     if (mergedCasts) {
         const bool ring = ringRows != 0 && !instrCounters && !opacity;   // (the ring kernel; the counting and
                                                                         // any-hit kernels keep the whole stack)
@@ -1227,6 +1278,7 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
 static uint32_t GraphSlot(bool sequenced, uint32_t iters) { return !sequenced ? 0u : (iters == kTailChunk ? 2u : 1u); }
 int dcrt_tracer::LaunchGraph(bool sequenced, uint32_t iters)
 {
+    Annotation an(sequenced ? "Iterations (graph, sequenced images)" : "Iterations (graph)");
     CHECKED(BuildGraph(sequenced, iters));
     HIPCHECK(hipGraphLaunch(graphs[GraphSlot(sequenced, iters)].exec, stream));
     return DCRT_OK;
@@ -1243,7 +1295,9 @@ int dcrt_tracer::BuildGraph(bool sequenced, uint32_t iters)
         hipGraph_t g = nullptr;
         HIPCHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
         int rc = DCRT_OK;
+        capturing = true;
         for (uint32_t i = 0; i < iters && rc == DCRT_OK; ++i) rc = LaunchIteration(i & 1u, false, sequenced);
+        capturing = false;
         hipError_t ec = hipStreamEndCapture(stream, &g);
         if (rc != DCRT_OK) return rc;
         HIPCHECK(ec);
@@ -1324,6 +1378,7 @@ int dcrt_tracer::UploadFilter(const dcrt_filter_params& f)
 
 int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
 {
+    Annotation an("SampleConvolution");
     if (!film.accum) { SetLastError("no film"); return DCRT_E_INVALID_ARG; }
     CHECKED(UploadFilter(f));
     hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
@@ -1337,6 +1392,7 @@ int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
 // host only enqueues graphs and polls a pinned "stopped" word two graphs behind.
 int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_filter_params& filter)
 {
+    Annotation an("RenderImages");
     if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
     if (count == 0) return DCRT_OK;
