@@ -98,8 +98,9 @@ FilterConsts MakeFilter(const dcrt_filter_params& p)   // SampleConvolution.cpp:
 // rounds up to the next integer (r just below k + 0.5).
 // roctx ranges around the host-side passes, named like the reference's PIX annotations
 // (SCOPED_RENDER_ANNOTATION, WavefrontPathTracer.cpp:443-1083): visible in rocprofv3
-// --marker-trace next to the kernels. libroctx64 is opened at run time (no link dependency;
-// absent, or DCRT_ROCTX=0: no ranges). Iterations captured into a hipGraph are annotated by
+// --marker-trace next to the kernels. rocprofiler-sdk's roctx (the one rocprofv3 intercepts;
+// the legacy libroctx64 as a fallback) is opened at run time (no link dependency; absent, or
+// DCRT_ROCTX=0: no ranges). Iterations captured into a hipGraph are annotated by
 // their replay ("RenderImages" / graph chunks), not per kernel.
 struct Roctx {
     int (*push)(const char*) = nullptr;
@@ -109,8 +110,8 @@ struct Roctx {
         if (const char* e = std::getenv("DCRT_ROCTX")) {
             if (std::atoi(e) == 0) return;
         }
-        void* h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
-        if (!h) h = dlopen("libroctx64.so", RTLD_NOW | RTLD_LOCAL);
+        void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_LOCAL);
         if (!h) return;
         push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
         pop = (int (*)())dlsym(h, "roctxRangePop");
