@@ -21,7 +21,7 @@ rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 # (the SQ + GRBM pass: VALU issue per cast launch for the bench's compute statement)
 for ctr in FETCH_SIZE WRITE_SIZE TCC_EA0_RDREQ_sum "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES GRBM_GUI_ACTIVE" ${EXTRA_PMC:-}; do
   tag=$(echo "$ctr" | tr ' ' '+')
-  timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -f csv -d "$OUT" -o "pmc_$tag" -- \
+  timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-trace -f csv -d "$OUT" -o "pmc_$tag" -- \
       python3 "$ROOTDIR/bench.py" $ARGS > "$OUT/pmc_${tag}.log" 2>&1
   rc=$?; echo "pmc $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
