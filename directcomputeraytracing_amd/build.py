@@ -10,6 +10,8 @@ GPU path and the oracle produce the same bits ("Numerics").
 """
 from __future__ import annotations
 
+import contextlib
+import fcntl
 import hashlib
 import os
 import shutil
@@ -64,14 +66,40 @@ def _digest(paths) -> str:
     return h.hexdigest()
 
 
+@contextlib.contextmanager
+def _build_lock(name: str):
+    """One build of an output at a time across processes (pytest-xdist workers, a test and a
+    tool): its object directory and stamp are shared, and two compilers writing one object
+    file leave a corrupt library. Different outputs build concurrently."""
+    PKG_DIR.mkdir(exist_ok=True)
+    with open(PKG_DIR / f".build.{name}.lock", "w") as fh:
+        fcntl.flock(fh, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(fh, fcntl.LOCK_UN)
+
+
+def _fresh(lib: Path, stamp: Path, digest: str) -> bool:
+    return lib.exists() and stamp.exists() and stamp.read_text().strip() == digest
+
+
 def build_native(force: bool = False, verbose: bool = False, out: Path | None = None, extra_flags=()) -> Path:
     """Compile libdcrt.so (or an experimental variant at `out` with `extra_flags`)."""
     lib_path = Path(out) if out else LIB_PATH
     sources = HOST_SOURCES + DEVICE_SOURCES
     digest = _digest(sources + HEADERS) + " ".join(extra_flags)
     stamp = lib_path.with_suffix(".so.sha256")
-    if not force and lib_path.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+    if not force and _fresh(lib_path, stamp, digest):
         return lib_path
+    with _build_lock(lib_path.stem):
+        if not force and _fresh(lib_path, stamp, digest):   # (another process built it meanwhile)
+            return lib_path
+        return _build_native_locked(lib_path, stamp, digest, out, verbose, extra_flags)
+
+
+def _build_native_locked(lib_path: Path, stamp: Path, digest: str, out, verbose: bool, extra_flags) -> Path:
+    sources = HOST_SOURCES + DEVICE_SOURCES
     objdir = PKG_DIR / ("_build" if out is None else "_build_" + lib_path.stem)
     objdir.mkdir(exist_ok=True)
     objs = []
@@ -116,8 +144,15 @@ def build_sanitized(force: bool = False) -> Path:
     sources = HOST_SOURCES + DEVICE_SOURCES
     digest = _digest(sources + HEADERS) + "asan"
     stamp = SANITIZED_LIB.with_suffix(".so.sha256")
-    if not force and SANITIZED_LIB.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+    if not force and _fresh(SANITIZED_LIB, stamp, digest):
         return SANITIZED_LIB
+    with _build_lock("asan"):
+        if not force and _fresh(SANITIZED_LIB, stamp, digest):
+            return SANITIZED_LIB
+        return _build_sanitized_locked(san, sources, stamp, digest)
+
+
+def _build_sanitized_locked(san, sources, stamp: Path, digest: str) -> Path:
     objdir = SANITIZED_LIB.parent
     objdir.mkdir(exist_ok=True)
     objs, procs = [], []
@@ -149,13 +184,16 @@ def build_examples(force: bool = False) -> Path:
     lib = build_native()
     digest = _digest([EXAMPLE_SRC, ROOT / "include" / "dcrt.h", lib])
     stamp = EXAMPLE_BIN.with_suffix(".sha256")
-    if not force and EXAMPLE_BIN.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+    if not force and _fresh(EXAMPLE_BIN, stamp, digest):
         return EXAMPLE_BIN
-    cxx = shutil.which("g++") or "g++"
-    cmd = [cxx, "-O2", "-std=c++17", "-Wall", str(EXAMPLE_SRC), "-I", str(ROOT / "include"), "-L", str(PKG_DIR), "-ldcrt",
-           "-Wl,-rpath,$ORIGIN/../directcomputeraytracing_amd", "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(EXAMPLE_BIN)]
-    subprocess.run(cmd, check=True)
-    stamp.write_text(digest)
+    with _build_lock("examples"):
+        if not force and _fresh(EXAMPLE_BIN, stamp, digest):
+            return EXAMPLE_BIN
+        cxx = shutil.which("g++") or "g++"
+        cmd = [cxx, "-O2", "-std=c++17", "-Wall", str(EXAMPLE_SRC), "-I", str(ROOT / "include"), "-L", str(PKG_DIR), "-ldcrt",
+               "-Wl,-rpath,$ORIGIN/../directcomputeraytracing_amd", "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(EXAMPLE_BIN)]
+        subprocess.run(cmd, check=True)
+        stamp.write_text(digest)
     return EXAMPLE_BIN
 
 
@@ -166,11 +204,14 @@ def build_oracle(force: bool = False) -> Path:
            ORACLE_DIR / "Makefile", ROOT / "include" / "dcrt.h"]
     digest = _digest(src)
     stamp = ORACLE_LIB.with_suffix(".so.sha256")
-    if not force and ORACLE_LIB.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+    if not force and _fresh(ORACLE_LIB, stamp, digest):
         return ORACLE_LIB
-    subprocess.run(["make", "-C", str(ORACLE_DIR), f"OUT={ORACLE_LIB.parent}"], check=True,
-                   stdout=subprocess.DEVNULL)
-    stamp.write_text(digest)
+    with _build_lock("oracle"):
+        if not force and _fresh(ORACLE_LIB, stamp, digest):
+            return ORACLE_LIB
+        subprocess.run(["make", "-C", str(ORACLE_DIR), f"OUT={ORACLE_LIB.parent}"], check=True,
+                       stdout=subprocess.DEVNULL)
+        stamp.write_text(digest)
     return ORACLE_LIB
 
 
@@ -184,12 +225,13 @@ def build_reference_checkers() -> Path | None:
     oracle/_ref/librefobj.so (oracle/ref_obj/Makefile). tests/test_obj_pin.py uses it."""
     if not (REFERENCE / "tinyobjloader" / "tiny_obj_loader.h").exists():
         return None
-    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR / "ref_obj"), f"REF={REFERENCE}"], check=True,
-                   stdout=subprocess.DEVNULL)
-    # ... and its vendored RapidXml for tests/test_xml_pin.py (oracle/ref_xml/Makefile)
-    if (REFERENCE / "RapidXml" / "rapidxml.hpp").exists():
-        subprocess.run(["make", "-s", "-C", str(ORACLE_DIR / "ref_xml"), f"REF={REFERENCE}"], check=True,
+    with _build_lock("reference"):
+        subprocess.run(["make", "-s", "-C", str(ORACLE_DIR / "ref_obj"), f"REF={REFERENCE}"], check=True,
                        stdout=subprocess.DEVNULL)
+        # ... and its vendored RapidXml for tests/test_xml_pin.py (oracle/ref_xml/Makefile)
+        if (REFERENCE / "RapidXml" / "rapidxml.hpp").exists():
+            subprocess.run(["make", "-s", "-C", str(ORACLE_DIR / "ref_xml"), f"REF={REFERENCE}"], check=True,
+                           stdout=subprocess.DEVNULL)
     return ORACLE_DIR / "_ref" / "librefobj.so"
 
 
