@@ -1,3 +1,7 @@
+#!/bin/bash
+# Traversal refill / park threshold sweep on the default Cornell bench (GPU box):
+# DCRT_TRAVERSAL_TUNE="refill,park" per run; prints ms/spp and the cast launch time per setting.
+#   TUNES="32,24 36,24" bash tools/sweep_tune.sh
 set -u
 mkdir -p gpurun_out
 for t in ${TUNES:-16,32 24,32 32,32 40,32 48,32 32,24 32,40 32,48}; do
