@@ -898,31 +898,38 @@ def test_anyhit_megakernel_bit_exact(native_lib, golden_luts, oracle_mod, name):
         t.destroy()
 
 
-@pytest.mark.parametrize("config,images", [("cornell", 4), ("coffee", 1)])
+@pytest.mark.parametrize("config,images", [("cornell", 4), ("coffee", 1), ("spaceship", 1), ("spaceship_close", 1), ("lamp", 1)])
 def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle_mod, tmp_path, config, images):
-    """The headline's own configuration at full size, built by the bench's own code
-    (make_pipelines, as bench.py does): 1920x1080, 8 bounces, the 2^24-slot pool split over two
-    concurrent stream-partitioned pipelines, virtual batch starts, the GPU-built LUTs, the default
-    cast kernel (Cornell: the cache-only IDENT kernel; coffee: configs[2] with Kulla-Conty on, the
-    global-memory kernel); images 0..N-1 rendered concurrently, the two films summed on the device.
-    The combined film must equal the oracle's film of the same images bit for bit, and the ray
-    counts the oracle's (plus the halo rows both pipelines trace)."""
+    """The bench's own configurations at full size, built by the bench's own code
+    (make_pipelines, as bench.py does): 8 bounces (lamp: its XML's depth), the default pool (2^24
+    slots at 1080p, 2^26 at 4K) split over two concurrent stream-partitioned pipelines, virtual
+    batch starts, the GPU-built LUTs and each config's default cast kernel -- Cornell 1080p: the
+    cache-only IDENT kernel; coffee 1080p (configs[2], Kulla-Conty on): the global-memory kernel;
+    spaceship 4K (configs[3], the 522 k-node hull x 8, wide and close framing): the pair kernel
+    with the LDS stack ring;
+    lamp 4K (configs[4], thin lens, triangle lights). Images 0..N-1 rendered concurrently, the two
+    films summed on the device. The combined film must equal the oracle's film of the same images
+    bit for bit, and the ray counts the oracle's (plus the halo rows both pipelines trace)."""
     from directcomputeraytracing_amd import Scene, make_pipelines, render_images_concurrently, scenes
     s = Scene((1920, 1080))
     if config == "cornell":
         scenes.setup_cornell(s, 1920, 1080, 8)
-    else:
+    elif config == "coffee":
         scenes.setup_config(s, "coffee", str(tmp_path), multiscattering=True)
+    else:
+        scenes.setup_config(s, config, str(tmp_path))
     W, H = s.resolution
-    assert (W, H) == (1920, 1080)
+    assert (W, H) == ((3840, 2160) if config in ("spaceship", "spaceship_close", "lamp") else (1920, 1080))
     filt = s.filter_params()
     ts = make_pipelines(s, scenes.default_pool(W, H), streams=2, images=images, iterations=16)
     try:
         info = ts[0].info()
         if config == "cornell":
             assert info["scene_in_lds"] == 1 and info["cast_identity"] == 1
-        else:
+        elif config == "coffee":
             assert info["scene_in_lds"] == 0 and info["pair_traversal"] == 0
+        elif config.startswith("spaceship"):
+            assert info["pair_traversal"] == 1 and info["ring_rows"] == 16
         for t in ts:
             t.clear_film()
             t.reset_stats()
