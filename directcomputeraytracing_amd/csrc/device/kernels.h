@@ -212,6 +212,23 @@ DEV T& sample_at(T* base, uint32_t i)
 {
     return *(T*)((char*)base + (uint64_t)i * (uint64_t)sizeof(T));
 }
+// The same element stored through a global-address-space pointer: a store through the
+// generic pointer is a flat store, which the wait counters track out of order, so the compiler
+// then waits for every outstanding memory operation before the next register reuse. (Through
+// an integer and clang vector types: a generic -> global pointer cast is folded back into a
+// flat store, and HIP's vector classes have no address-space-qualified assignment.)
+typedef float GlobalF2 __attribute__((ext_vector_type(2)));
+typedef float GlobalF4 __attribute__((ext_vector_type(4)));
+DEV void store_global(float2* base, uint32_t i, float2 v)
+{
+    const GlobalF2 x = {v.x, v.y};
+    *(__attribute__((address_space(1))) GlobalF2*)((uintptr_t)base + (uint64_t)i * 8u) = x;
+}
+DEV void store_global(float4* base, uint32_t i, float4 v)
+{
+    const GlobalF4 x = {v.x, v.y, v.z, v.w};
+    *(__attribute__((address_space(1))) GlobalF4*)((uintptr_t)base + (uint64_t)i * 16u) = x;
+}
 
 // A live path's state travels with its extension ray: one 64-B record at the ray's
 // extension-queue position q (beside the 32-B ray record), written densely by its producer

@@ -20,9 +20,9 @@ namespace dev {
 // waves spend per phase of the persistent loop, summed over all waves:
 // [0] hand-over + result stores + ray set-up, [1] phase A (node visits), [2] phase B
 // (leaf work), [3] loop trips, [4] phase-A checks, [5] phase-B entries.
-// MATERIAL: [8] loads + Li update, [9] HitInfoToIntersection, [10] emission, [11] NEE
-// (light sample, BSDF eval + pdf, shadow ray), [12] BSDF sample + new ray, [13] stores,
-// [14] queue appends, [15] items.
+// MATERIAL: [8] loads + Li update, [9] HitInfoToIntersection, [10] record / sample stores,
+// [11] emission + NEE (BSDF frame, light sample, BSDF eval + pdf, shadow ray), [12] BSDF
+// sample + new ray, [13] end-of-path loads, [14] queue appends (barriers + atomics), [15] items.
 __device__ unsigned long long g_phaseClk[24];
 #define DCRT_PHASE_INIT unsigned long long clk_[6] = {0, 0, 0, 0, 0, 0}; unsigned long long tP_ = __builtin_amdgcn_s_memtime()
 #define DCRT_PHASE(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); clk_[i] += t_ - tP_; tP_ = t_; } while (0)
@@ -31,7 +31,12 @@ __device__ unsigned long long g_phaseClk[24];
 #define DCRT_MCLK_INIT unsigned long long mclk_[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long mT_ = __builtin_amdgcn_s_memtime()
 #define DCRT_MCLK(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); mclk_[i] += t_ - mT_; mT_ = t_; } while (0)
 #define DCRT_MCLK_FLUSH(items) do { mclk_[7] += (items); if ((threadIdx.x & 63u) == 0) for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_phaseClk[8 + i_], mclk_[i_]); } while (0)
+// (shade_path's sections clock into its caller's MATERIAL clocks)
+#define DCRT_MCLK_PARAMS , unsigned long long (&mclk_)[8], unsigned long long& mT_
+#define DCRT_MCLK_ARGS , mclk_, mT_
 #else
+#define DCRT_MCLK_PARAMS
+#define DCRT_MCLK_ARGS
 #define DCRT_MCLK_INIT do {} while (0)
 #define DCRT_MCLK(i) do {} while (0)
 #define DCRT_MCLK_FLUSH(items) do {} while (0)
@@ -329,7 +334,7 @@ template <uint32_t CAPS>
 __device__ __forceinline__ void shade_path(const DeviceScene& sc, const FrameConstants& fc, const HitRecord& hit, V3 dir, Rng& rng,
                                            uint32_t& flags, float4& thr, const F3& li, V3& T, V3& L, V3& lsr, bool& terminate,
                                            bool& hasShadow, V3& nO, V3& nD, float4& sO, V3& sD, float& extOpacity,
-                                           float& shadowOpacity)
+                                           float& shadowOpacity DCRT_MCLK_PARAMS)
 {
     const uint32_t bounce = flags & 0xFFu;
     const uint32_t features = fc.features;
@@ -339,6 +344,7 @@ __device__ __forceinline__ void shade_path(const DeviceScene& sc, const FrameCon
     it.lightIndex = DCRT_LIGHT_INDEX_INVALID; it.triangleIndex = 0;
     it.geometryNormal = mk(0.0f, 0.0f, 0.0f);
     if (hasHit) hit_to_intersection<CAPS>(sc, hit, it);
+    DCRT_MCLK(1);
     T = mk(thr.x, thr.y, thr.z);
     L = mk(li.x, li.y, li.z);
     // Evaluate light :331-349
@@ -375,6 +381,7 @@ __device__ __forceinline__ void shade_path(const DeviceScene& sc, const FrameCon
                 hasShadow = true;
             }
         }
+        DCRT_MCLK(3);
         float bsdfPdf = 0.0f;
         bool isDelta = false;
         {
@@ -569,7 +576,7 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         V3 T, L, lsr;
         DCRT_MCLK(0);
         shade_path<CAPS>(sc, fcv, hit, dir, rng, flags, thr, li, T, L, lsr, terminate, hasShadow, nO, nD, sO, sD,
-                         extOpacity, shadowOpacity);
+                         extOpacity, shadowOpacity DCRT_MCLK_ARGS);
         DCRT_MCLK(4);
         if (fcv.features & DCRT_FEATURE_ALLOW_ANYHIT) {   // :422-430
             if (!terminate) slot(pool.extOpacity, out) = extOpacity;
@@ -599,7 +606,6 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
                 // (behind the barriers and the atomic) they were one more round trip
                 outPos = so.samplePosition;
                 outVal = so.sampleValue;
-                slot(pool.flags, out) = kFlagIdle;
             }
             if (so.debugRng) sample_at(so.debugRng, pix) = make_uint4(rng.s0, rng.s1, rng.s2, rng.s3);
         }
@@ -611,8 +617,20 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
     uint32_t fb;
     block_append3(active && !terminate, qctr(cnt, kQExt, shard), active && hasShadow, qctr(cnt, kQShadow, shard),
                   fin, qctr(cnt, kQFinish, fshard), sm + (round & 1u) * 48u, &es, &ss, &fb);
+    DCRT_MCLK(6);
     const uint32_t qNext = shard * pool.recCap + es;           // the continuing path's records
     const uint32_t fPos = fshard * pool.finCap + fb;           // a finishing path's record
+    // An ended path's sample (and its slot's idle flag) is stored before the records: its
+    // address needs the pixel load, and vmcnt counts loads and stores in issue order, so a
+    // wait for the pixel issued after the record stores waited for all of them too. The empty
+    // asm takes the pixel in every wave (whether or not one of its paths ended), so that wait
+    // is placed here, ahead of every store, and not where the pixel's register is next reused.
+    asm volatile("" ::"v"(pix));
+    if (ends) {
+        store_global(outPos, pix, pixel_sample(fcv, pix));
+        store_global(outVal, pix, sample);
+        slot(pool.flags, path) = kFlagIdle;
+    }
     if (active && !terminate) {
         float4* r = ext_rec(pool.extRec, qNext);
         r[0] = make_float4(nO.x, nO.y, nO.z, 0.0f);
@@ -640,11 +658,7 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
         // opacity sample is per slot)
         if (fcv.features & DCRT_FEATURE_ALLOW_ANYHIT) slot(pool.shadowQueue, sq) = path;
     }
-    if (ends) {
-        sample_at(outPos, pix) = pixel_sample(fcv, pix);
-        sample_at(outVal, pix) = sample;
-    }
-    DCRT_MCLK(6);
+    DCRT_MCLK(2);
     ++round;
     }
     DCRT_MCLK_FLUSH(itemsDone);
@@ -1376,8 +1390,9 @@ __global__ __launch_bounds__(256) void drain_kernel(PathPool pool, DeviceScene s
             V3 T, L, lsr, nO = mk(0.0f, 0.0f, 0.0f), nD = nO, sD = nO;
             float4 sO = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             float extOpacity = 0.0f, shadowOpacity = 0.0f;
+            DCRT_MCLK_INIT;   // (the drain's sections are not reported)
             shade_path<CAPS>(sc, fc, hit, dir, rng, flags, thr, li, T, L, lsr, terminate, hasShadow, nO, nD, sO, sD,
-                             extOpacity, shadowOpacity);
+                             extOpacity, shadowOpacity DCRT_MCLK_ARGS);
             shadowHit = false;
             if (hasShadow) {   // SHADOW_RAY_CAST
                 HitRecord sh;

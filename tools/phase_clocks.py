@@ -62,9 +62,10 @@ def main():
     m = out[8:15].astype(np.float64)
     mt = m.sum()
     print(f"MATERIAL: {int(out[15])} lane-items (waves x items), wave-cycles per wave-item {mt / max(1, out[15]):.0f}")
-    # (material_kernel's DCRT_MCLK sections: 0 loads, 4 shade_path, 5 end-of-path loads, 6 appends + stores)
-    for i, name in ((0, "loads (hit, state halves) + Li update"), (4, "shade_path (HitInfo, emission, NEE, BSDF sample)"),
-                    (5, "end-of-path (pixel, debug RNG)"), (6, "queue appends + record / sample stores")):
+    # (material_kernel's DCRT_MCLK sections; 1-4 inside shade_path)
+    for i, name in ((0, "loads (hit, state halves) + Li update"), (1, "HitInfoToIntersection"),
+                    (3, "emission + NEE (BSDF frame, light sample, eval + pdf, shadow ray)"), (4, "BSDF sample + next ray"),
+                    (5, "end-of-path (pixel, debug RNG)"), (6, "queue appends (barriers + atomics)"), (2, "record / sample stores")):
         print(f"  {name:50s} {m[i] / 1e9:8.3f} Gcycles  {100 * m[i] / mt:5.1f} %")
     tr.destroy()
 
