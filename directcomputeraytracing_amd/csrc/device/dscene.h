@@ -221,7 +221,7 @@ DEV bool tri_watertight(V3 o, const Shear& sh, float tMin, float tMax, V3 v0, V3
     const float det = e0 + e1 + e2;
     p0z = p0z * sh.sz; p1z = p1z * sh.sz; p2z = p2z * sh.sz;
     const float tScaled = e0 * p0z + e1 * p1z + e2 * p2z;
-    const float invDet = 1.0f / det;
+    const float invDet = rcp_ieee(det);
     *t = tScaled * invDet;
     *u = e1 * invDet;
     *v = e2 * invDet;
@@ -252,7 +252,7 @@ DEV bool tri_watertight_rot(const Shear& sh, float tMin, float tMax, float4 q0, 
     const float det = e0 + e1 + e2;
     p0z = p0z * sh.sz; p1z = p1z * sh.sz; p2z = p2z * sh.sz;
     const float tScaled = e0 * p0z + e1 * p1z + e2 * p2z;
-    const float invDet = 1.0f / det;
+    const float invDet = rcp_ieee(det);
     *t = tScaled * invDet;
     *u = e1 * invDet;
     *v = e2 * invDet;
@@ -268,7 +268,7 @@ DEV bool tri_moller(V3 o, V3 d, float tMin, float tMax, V3 v0, V3 v1, V3 v2, flo
     const V3 v0v1 = v1 - v0, v0v2 = v2 - v0;
     const V3 pvec = cross(d, v0v2);
     const float det = dot(v0v1, pvec);
-    const float invDet = 1.0f / det;
+    const float invDet = rcp_ieee(det);
     const V3 tvec = o - v0;
     *u = dot(tvec, pvec) * invDet;
     const V3 qvec = cross(tvec, v0v1);
@@ -278,7 +278,7 @@ DEV bool tri_moller(V3 o, V3 d, float tMin, float tMax, V3 v0, V3 v1, V3 v2, flo
     return fabsf(det) >= 1e-10f && *u >= 0.0f && *u <= 1.0f && *v >= 0.0f && *u + *v <= 1.0f && *t >= tMin && *t < tMax;
 }
 
-DEV V3 inv_dir(V3 d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
+DEV V3 inv_dir(V3 d) { return mk(rcp_ieee(d.x), rcp_ieee(d.y), rcp_ieee(d.z)); }
 
 struct HitRecord {
     float t, u, v;
