@@ -1468,6 +1468,8 @@ __global__ void math_eval_kernel(int function, const float* x, uint32_t n, float
     case 1: y[i] = det_cos(x[i]); break;
     case 2: y[i] = det_exp(x[i]); break;
     case 4: y[i] = det_log(x[i]); break;
+    case 5: y[i] = rcp_ieee(x[i]); break;    // (the fast reciprocal against ...)
+    case 6: y[i] = 1.0f / x[i]; break;       // (... the compiler's IEEE division)
     default: y[i] = det_atan(x[i]); break;
     }
 }

@@ -540,7 +540,8 @@ DCRT_API int dcrt_tracer_resolve_image(dcrt_tracer* tracer, const dcrt_postfx_pa
 /* 24-bit BMP writer ("Save Image to File", SaveImageToFile.cpp:92-182). */
 DCRT_API int dcrt_write_bmp(const char* path, uint32_t width, uint32_t height, const uint8_t* rgba8);
 
-/* Deterministic transcendental helpers shared by kernels (parity tests). */
+/* Deterministic transcendental helpers shared by kernels (parity tests): function 0 sin, 1 cos,
+   2 exp, 3 atan, 4 log (the det_* polynomials), 5 the fast reciprocal rcp_ieee, 6 IEEE 1/x. */
 DCRT_API int dcrt_device_math_eval(dcrt_tracer* tracer, int function, const float* x, uint32_t count, float* out_y);
 
 #ifdef __cplusplus
