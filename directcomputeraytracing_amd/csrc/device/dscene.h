@@ -133,6 +133,23 @@ DEV float4* scene_cache(const DeviceScene& sc, uint32_t* stackMem, uint32_t shif
 {
     return (float4*)(stackMem + (sc.stackRows << shift));
 }
+// 16-B loads through address-space-qualified pointers (ds_read_b128 / global_load_dwordx4):
+// where a node may come from the LDS cache or from memory, the two reads of one generic
+// pointer became a flat load, whose waits count both counters. (The LDS offset is the low 32
+// bits of a generic LDS address.)
+typedef float LoadF4 __attribute__((ext_vector_type(4)));
+DEV float4 lds_load4(const float4* genericLds, uint32_t i)
+{
+    const __attribute__((address_space(3))) LoadF4* p = (const __attribute__((address_space(3))) LoadF4*)(uint32_t)(uintptr_t)genericLds;
+    const LoadF4 v = p[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+DEV float4 global_load4(const float4* g, size_t i)
+{
+    const __attribute__((address_space(1))) LoadF4* p = (const __attribute__((address_space(1))) LoadF4*)(uintptr_t)g;
+    const LoadF4 v = p[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 // Triangles of the cache-only variant (ALL_CACHED kernels) are stored three times, once
 // per watertight-test axis permutation: copy z holds every vertex as (v[z+1], v[z+2], v[z])
 // (mod 3) -- the (kx, ky, kz) of a ray whose dominant axis is z -- so the test reads its
@@ -510,11 +527,11 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         b = c[idx * 2 + 1];
     } else if (idx < sc.cachedNodes) {
         const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
-        a = c[idx * 2];
-        b = c[idx * 2 + 1];
+        a = lds_load4(c, idx * 2);
+        b = lds_load4(c, idx * 2 + 1);
     } else {
-        a = sc.nodes[idx * 2];
-        b = sc.nodes[idx * 2 + 1];
+        a = global_load4(sc.nodes, (size_t)idx * 2);
+        b = global_load4(sc.nodes, (size_t)idx * 2 + 1);
     }
     const bool hit = IDENT ? ray_aabb_raw(s.o, s.invW, s.tMin, s.tMax, a, b) : ray_aabb(s, a, b);
     const uint32_t misc = asu(b.w);
@@ -612,7 +629,9 @@ DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uin
         }
     };
     // (both fetches unconditional: a visit fetches its node twice, the second from L1, which
-    // costs less than the exec-mask branch and the zeroed registers of a conditional fetch)
+    // costs less than the exec-mask branch and the zeroed registers of a conditional fetch;
+    // the LDS-or-memory choice stays one flat load here: split into ds_read / global_load
+    // branches, as trav_visit has them, the pair kernel lost 5 %, profiles/r05_ab_split_loads.txt)
     float4 a0, b0, a1, b1;
     fetch(aRef, a0, b0);
     fetch(s.expand ? bRef : aRef, a1, b1);
@@ -724,11 +743,11 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
                 q0 = c[0]; q1 = c[1]; q2 = c[2];   // permutation z = 2 is the identity
             } else if (p < sc.cachedTris) {
                 const float4* c = scene_cache(sc, lds - threadIdx.x, shift) + sc.cachedNodes * 2u;
-                q0 = c[p * 3]; q1 = c[p * 3 + 1]; q2 = c[p * 3 + 2];
+                q0 = lds_load4(c, p * 3); q1 = lds_load4(c, p * 3 + 1); q2 = lds_load4(c, p * 3 + 2);
             } else {
-                q0 = sc.triVerts[(size_t)p * 3];
-                q1 = sc.triVerts[(size_t)p * 3 + 1];
-                q2 = sc.triVerts[(size_t)p * 3 + 2];
+                q0 = global_load4(sc.triVerts, (size_t)p * 3);
+                q1 = global_load4(sc.triVerts, (size_t)p * 3 + 1);
+                q2 = global_load4(sc.triVerts, (size_t)p * 3 + 2);
             }
             const V3 v0 = mk(q0.x, q0.y, q0.z), v1 = mk(q1.x, q1.y, q1.z), v2 = mk(q2.x, q2.y, q2.z);
             h = watertight ? tri_watertight(spO, s.sh, s.tMin, s.tMax, v0, v1, v2, q0.w != 0.0f, &t, &u, &v, &bf)
