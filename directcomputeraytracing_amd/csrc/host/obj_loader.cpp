@@ -507,10 +507,13 @@ bool CreateMeshFromObjData(const ObjData& d, const ObjShape* shapes, uint32_t sh
         const ObjShape& shape = shapes[s];
         // a corner without position or normal fails the mesh (:212-213); the reference
         // reads such corners' attributes out of bounds in MikkTSpace first, so they and
-        // out-of-range indices are refused before any attribute is read
+        // out-of-range indices are refused before any attribute is read -- a texcoord index
+        // too (only -1 means "none": a relative index reaching before the first texcoord
+        // resolves to another negative value, which the reference reads out of bounds)
         for (const ObjIndex& idx : shape.indices)
             if (idx.v < 0 || idx.vn < 0 || (size_t)idx.v * 3 + 2 >= d.positions.size() ||
-                (size_t)idx.vn * 3 + 2 >= d.normals.size() || (idx.vt >= 0 && (size_t)idx.vt * 2 + 1 >= d.texcoords.size()))
+                (size_t)idx.vn * 3 + 2 >= d.normals.size() ||
+                (idx.vt != -1 && (idx.vt < 0 || (size_t)idx.vt * 2 + 1 >= d.texcoords.size())))
                 return false;
         // a shape MikkTSpace refuses (no triangles) is skipped (WavefrontOBJLoading.cpp:195-199)
         if (!ShapeTangents(d, shape, params.flipTexcoordV, &tangents)) continue;

@@ -4,10 +4,13 @@
 #include "scene.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 
 namespace dcrt {
+
+void SetLastError(const std::string& s);   // (capi_scene.cpp)
 
 void GetDefaultMaterial(SMaterial* m)
 {
@@ -179,6 +182,16 @@ bool CScene::LoadFromFile(const std::string& path)
             materials.push_back(m);
         }
     }
+    // Non-finite vertex positions (an OBJ coordinate past FLT_MAX parses to inf; a transform
+    // can overflow too) are refused: the SAH builder's centroid bounds and bucket indices
+    // are undefined on them -- the reference's build, restated exactly, did not finish on
+    // such a file within a minute (a fuzzed OBJ) -- and no ray can hit such a triangle.
+    for (size_t i = meshIndexBase; i < meshes.size(); ++i)
+        for (const dcrt_vertex& v : meshes[i].vertices)
+            if (!std::isfinite(v.position[0]) || !std::isfinite(v.position[1]) || !std::isfinite(v.position[2])) {
+                SetLastError("non-finite vertex position in mesh " + std::to_string(i));
+                return false;
+            }
     // BLAS per new mesh (Scene.cpp:162-172)
     {
         std::vector<uint32_t> reordered;
@@ -194,6 +207,15 @@ bool CScene::LoadFromFile(const std::string& path)
             if (mesh.bvhNodes.empty()) return false;
             blas[i].box = mesh.bvhNodes[0].box;
             blas[i].transform = instanceTransforms[i].To4x4();
+            // a non-finite instance box (an overflowing transform: a fuzzed XML matrix entry of
+            // 3e9612 never let the TLAS build finish) is refused like a non-finite vertex
+            const BoundingBox world = BoxTransform(blas[i].box, blas[i].transform);
+            const Float3 c = world.center, e = world.extents;
+            if (!std::isfinite(c.x) || !std::isfinite(c.y) || !std::isfinite(c.z) || !std::isfinite(e.x) || !std::isfinite(e.y) ||
+                !std::isfinite(e.z)) {
+                SetLastError("non-finite bounds of instance " + std::to_string(i) + " (its transform)");
+                return false;
+            }
         }
         std::vector<uint32_t> depths(instanceCount);
         originalInstanceIndices.assign(instanceCount, 0);
