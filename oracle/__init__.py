@@ -90,8 +90,50 @@ def load():
     lib.oracle_frame_params.argtypes = [P(A.SceneSettings), U, P(A.FrameParams)]
     lib.oracle_punctual_direction.restype = None
     lib.oracle_punctual_direction.argtypes = [P(C.c_float), P(C.c_float)]
+    lib.oracle_bsdf_eval.restype = None
+    lib.oracle_bsdf_eval.argtypes = [P(A.BxDFLuts), P(OracleBsdfMaterial), P(C.c_float), P(C.c_float), U, P(C.c_float),
+                                     P(C.c_float)]
+    lib.oracle_bsdf_sample.restype = None
+    lib.oracle_bsdf_sample.argtypes = [P(A.BxDFLuts), P(OracleBsdfMaterial), P(C.c_float), P(C.c_float), U, P(C.c_float),
+                                       P(C.c_float), P(C.c_float), P(C.c_int)]
     _lib = lib
     return lib
+
+
+class OracleBsdfMaterial(C.Structure):
+    _fields_ = [("type", C.c_uint32), ("albedo", C.c_float * 3), ("alpha", C.c_float), ("ior", C.c_float),
+                ("two_sided", C.c_int), ("multiscattering", C.c_int), ("internal_scattering", C.c_uint32)]
+
+
+def bsdf_material(type, albedo=(1.0, 1.0, 1.0), alpha=0.5, ior=1.5, two_sided=False, multiscattering=False,
+                  internal_scattering=0):
+    return OracleBsdfMaterial(int(type), (C.c_float * 3)(*albedo), float(alpha), float(ior), int(two_sided),
+                              int(multiscattering), int(internal_scattering))
+
+
+def bsdf_eval(luts, material, wi, wo):
+    """EvaluateBSDF / EvaluateBSDFPdf (BSDFs.inc.hlsl:42-287) of one material in the frame
+    n = (0,0,1), t = (1,0,0): (N, 3) f and (N,) pdf for (N, 3) direction pairs."""
+    wi = np.ascontiguousarray(wi, np.float32).reshape(-1, 3)
+    wo = np.ascontiguousarray(wo, np.float32).reshape(-1, 3)
+    f = np.zeros_like(wi)
+    pdf = np.zeros(len(wi), np.float32)
+    load().oracle_bsdf_eval(C.byref(luts), C.byref(material), _fp(wi), _fp(wo), len(wi), _fp(f), _fp(pdf))
+    return f, pdf
+
+
+def bsdf_sample(luts, material, wo, u):
+    """SampleBSDF (BSDFs.inc.hlsl:289-505): for (N, 3) wo and (N, 3) numbers (sx, sy, sel),
+    the sampled wi (N, 3), f (N, 3), pdf (N,) and delta flags (N,)."""
+    wo = np.ascontiguousarray(wo, np.float32).reshape(-1, 3)
+    u = np.ascontiguousarray(u, np.float32).reshape(-1, 3)
+    wi = np.zeros_like(wo)
+    f = np.zeros_like(wo)
+    pdf = np.zeros(len(wo), np.float32)
+    delta = np.zeros(len(wo), np.int32)
+    load().oracle_bsdf_sample(C.byref(luts), C.byref(material), _fp(wo), _fp(u), len(wo), _fp(wi), _fp(f), _fp(pdf),
+                              delta.ctypes.data_as(C.POINTER(C.c_int)))
+    return wi, f, pdf, delta.astype(bool)
 
 
 class OracleBVHNode(C.Structure):

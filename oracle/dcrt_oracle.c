@@ -1664,6 +1664,52 @@ static void trace_path(const dcrt_flat_scene* sc, const dcrt_frame_params* f, in
     if (outRng) { outRng[0] = s[0]; outRng[1] = s[1]; outRng[2] = s[2]; outRng[3] = s[3]; }
 }
 
+/* Test entries: one material's BSDF in the frame n = (0,0,1), t = (1,0,0) (see dcrt_oracle.h) */
+static isect bsdf_test_isect(const oracle_bsdf_material* m)
+{
+    isect it;
+    memset(&it, 0, sizeof(it));
+    it.albedo = V3(m->albedo[0], m->albedo[1], m->albedo[2]);
+    it.alpha = m->alpha;
+    it.normal = V3(0.0f, 0.0f, 1.0f);
+    it.geometryNormal = V3(0.0f, 0.0f, 1.0f);
+    it.tangent = V3(1.0f, 0.0f, 0.0f);
+    it.ior = V3(m->ior, 1.0f, 1.0f);
+    it.isTwoSided = m->two_sided;
+    it.multiscattering = m->multiscattering;
+    it.internalScatteringMode = m->internal_scattering;
+    it.materialType = m->type;
+    it.lightIndex = DCRT_LIGHT_INDEX_INVALID;
+    return it;
+}
+void oracle_bsdf_eval(const dcrt_bxdf_luts* luts, const oracle_bsdf_material* m, const float* wi, const float* wo,
+                      uint32_t count, float* f_out, float* pdf_out)
+{
+    g_luts = luts;
+    const isect it = bsdf_test_isect(m);
+    for (uint32_t i = 0; i < count; ++i) {
+        const v3 a = V3(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]), b = V3(wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]);
+        const v3 f = evaluate_bsdf(a, b, &it);
+        f_out[3 * i] = f.x; f_out[3 * i + 1] = f.y; f_out[3 * i + 2] = f.z;
+        pdf_out[i] = evaluate_bsdf_pdf(a, b, &it);
+    }
+}
+void oracle_bsdf_sample(const dcrt_bxdf_luts* luts, const oracle_bsdf_material* m, const float* wo, const float* u,
+                        uint32_t count, float* wi_out, float* f_out, float* pdf_out, int* delta_out)
+{
+    g_luts = luts;
+    const isect it = bsdf_test_isect(m);
+    for (uint32_t i = 0; i < count; ++i) {
+        const v3 b = V3(wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]);
+        f2 smp; smp.x = u[3 * i]; smp.y = u[3 * i + 1];
+        v3 wi, f; float pdf; int delta;
+        sample_bsdf(b, smp, u[3 * i + 2], &it, &wi, &f, &pdf, &delta);
+        wi_out[3 * i] = wi.x; wi_out[3 * i + 1] = wi.y; wi_out[3 * i + 2] = wi.z;
+        f_out[3 * i] = f.x; f_out[3 * i + 1] = f.y; f_out[3 * i + 2] = f.z;
+        pdf_out[i] = pdf; delta_out[i] = delta;
+    }
+}
+
 void oracle_generate_camera_ray(const dcrt_frame_params* f, uint32_t px, uint32_t py, float origin[3], float direction[3], uint32_t rng_out[4])
 {
     uint32_t s[4];

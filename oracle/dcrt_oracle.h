@@ -74,6 +74,23 @@ void oracle_generate_camera_ray(const dcrt_frame_params* frame, uint32_t px, uin
 /* function: 0 sin, 1 cos, 2 exp, 3 atan, 4 log */
 void oracle_math_eval(int function, const float* x, uint32_t count, float* y);
 
+/* One material's BSDF (BSDFs.inc.hlsl EvaluateBSDF / EvaluateBSDFPdf / SampleBSDF) in the frame
+   normal = geometric normal = (0,0,1), tangent = (1,0,0), for the BxDF physics pins
+   (tests/test_bsdf_pins.py). material: type, albedo[3], alpha, ior, two-sided, multiscattering,
+   internal scattering mode. eval: f (3 per pair) and pdf for `count` (wi, wo) pairs; sample: for
+   `count` wo and (sx, sy, sel) triples, wi, f, pdf and the delta flag. */
+typedef struct oracle_bsdf_material {
+    uint32_t type;
+    float albedo[3];
+    float alpha, ior;
+    int two_sided, multiscattering;
+    uint32_t internal_scattering;
+} oracle_bsdf_material;
+void oracle_bsdf_eval(const dcrt_bxdf_luts* luts, const oracle_bsdf_material* m, const float* wi, const float* wo,
+                      uint32_t count, float* f_out, float* pdf_out);
+void oracle_bsdf_sample(const dcrt_bxdf_luts* luts, const oracle_bsdf_material* m, const float* wo, const float* u,
+                        uint32_t count, float* wi_out, float* f_out, float* pdf_out, int* delta_out);
+
 /* Post-processing (PostProcessings.hlsl, SumLuminance.hlsl): tone-mapped sRGB8 RGBA. */
 float oracle_sum_log_luminance(const float* film_rgba, uint32_t width, uint32_t height);
 void oracle_resolve_image(const float* film_rgba, uint32_t width, uint32_t height, int enabled, int auto_exposure, float ev100,
