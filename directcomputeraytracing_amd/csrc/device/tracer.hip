@@ -1836,6 +1836,7 @@ DCRT_API int dcrt_tracer_occluded(dcrt_tracer* t, const dcrt_ray* rays, uint32_t
 DCRT_API int dcrt_tracer_trace_rays_device(dcrt_tracer* t, const void* d_rays, uint32_t n, void* d_hits, uint32_t features)
 {
     TRACER_GUARD(t);
+    if ((!d_rays || !d_hits) && n) return DCRT_E_INVALID_ARG;
     return TraceBatch(t, (const dcrt_ray*)d_rays, n, (dcrt_ray_hit*)d_hits, nullptr, false, features);
 }
 
