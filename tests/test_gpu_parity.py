@@ -878,6 +878,31 @@ def test_megakernel_matches_oracle_megakernel(native_lib, golden_luts, oracle_mo
         t.destroy()
 
 
+def test_megakernel_full_size_cornell_bit_exact(native_lib, golden_luts, oracle_mod):
+    """The megakernel mode (bench.py --mode megakernel) at the headline size: Cornell 1920x1080,
+    8 bounces, the bench's default pool, image 0 -- every sample and the ray counts equal the
+    oracle's MegakernelPathTracing restatement."""
+    from directcomputeraytracing_amd import WavefrontPathTracer, scenes
+    s = cornell(1920, 1080, 8)
+    t = WavefrontPathTracer(path_pool_size=scenes.default_pool(1920, 1080))
+    try:
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        t.set_mode("megakernel")
+        t.reset_stats()
+        t.render_images(0, 1)
+        pos, val = t.read_samples()
+        c = t.counters()
+    finally:
+        t.destroy()
+    p_ref, v_ref, _, c_ref = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, oracle_mod.frame_params(s, 0),
+                                               oracle_mod.MEGAKERNEL)
+    assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
+    bad = np.count_nonzero(~same_bits(val, v_ref).all(-1))
+    assert bad == 0, f"{bad} of {val.shape[0] * val.shape[1]} pixels differ"
+    assert (c["extension_rays"], c["shadow_rays"]) == (c_ref["extension_rays"], c_ref["shadow_rays"]), (c, c_ref)
+
+
 # ---- ALLOW_ANYHIT_SHADER ------------------------------------------------------------------
 def _anyhit_scenes():
     from directcomputeraytracing_amd import FEATURE_ALLOW_ANYHIT
