@@ -1,0 +1,91 @@
+"""Seeded random scenes (tests/random_scenes.py): triangle soups with shared edges, flat patches,
+zero-area and coincident triangles, transformed and identity instances, every BSDF type and light
+kind, pinhole and thin-lens cameras.
+
+CPU: the product's XML translation equals the oracle's restatement over the reference's own
+RapidXml / tinyobjloader / MikkTSpace (where oracle/_ref is built), and the product's flattened
+scene (BVH build included) equals the oracle's own flattening, array for array, bit for bit.
+GPU: every cast kernel variant the tracer can pick for such a scene -- the LDS-cached one (the
+cache-only IDENT kernel for the OBJ scenes), the global-memory one, the pair traversal and the
+8-row stack ring that spills -- and the megakernel render the oracle's image bit for bit."""
+import numpy as np
+import pytest
+
+import random_scenes as R
+from test_xml_translation_pin import REFOBJ, REFXML, check, oracle_xml  # noqa: F401 (oracle_xml: a fixture)
+
+SEEDS = range(6)
+
+
+def _scene(kind, seed, tmp_path):
+    from directcomputeraytracing_amd import Scene
+    s = Scene((48, 36))
+    if kind == "obj":
+        R.setup_obj_scene(s, R.write_obj_scene(tmp_path, seed), seed)
+    else:
+        s.load_from_file(R.write_xml_scene(tmp_path, seed))
+    return s
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.skipif(not (REFXML.exists() and REFOBJ.exists()), reason="oracle/_ref reference checkers not built (no /root/reference)")
+def test_random_xml_translation_matches_oracle(oracle_xml, seed, tmp_path):
+    o = check(oracle_xml, R.write_xml_scene(tmp_path, seed))
+    assert o is not None and len(o["instances"]) >= 4
+
+
+@pytest.mark.parametrize("kind", ["obj", "xml"])
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_scene_flattening_matches_oracle(native_lib, oracle_mod, tmp_path, kind, seed):
+    from test_scene_pin import _flat_arrays
+    s = _scene(kind, seed, tmp_path)
+    prod = _flat_arrays(s.flat())
+    own = _flat_arrays(oracle_mod.flatten_scene(s))
+    for k in prod:
+        assert prod[k].shape == own[k].shape and np.array_equal(prod[k], own[k]), (kind, seed, k)
+    a, b = s.frame_params(seed), oracle_mod.frame_params(s, seed)
+    assert bytes(a) == bytes(b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cache", ["lds", "global", "pair", "ring8", "megakernel"])
+@pytest.mark.parametrize("kind", ["obj", "xml"])
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_scenes_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, tmp_path, kind, seed, cache):
+    from test_gpu_parity import _render_and_compare, same_bits
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    if cache in ("global", "pair"):
+        monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+    monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1" if cache == "pair" else "0")
+    if cache == "ring8":
+        monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+        monkeypatch.setenv("DCRT_STACK_RING", "8")
+    s = _scene(kind, seed, tmp_path)
+    t = WavefrontPathTracer(path_pool_size=1 << 12, debug_rng=True)
+    try:
+        if cache == "megakernel":
+            t.set_luts(golden_luts)
+            t.on_scene_loaded(s)
+            t.set_mode("megakernel")
+            for fs in (0, 5):
+                t.clear_film()
+                t.render_images(fs, 1)
+                pos, val = t.read_samples()
+                p_ref, v_ref, _, _ = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, oracle_mod.frame_params(s, fs),
+                                                       oracle_mod.MEGAKERNEL)
+                assert np.array_equal(pos.view(np.uint32), p_ref.view(np.uint32))
+                bad = np.count_nonzero(~same_bits(val, v_ref).all(-1))
+                assert bad == 0, f"{kind} seed {seed} frame {fs}: {bad} pixels differ"
+            return
+        rays = [0, 0]
+        for c, c_ref in _render_and_compare(t, oracle_mod, golden_luts, s, [0, 5]):
+            rays = [rays[0] + c_ref["extension_rays"], rays[1] + c_ref["shadow_rays"]]   # (the tracer's counts accumulate)
+            assert [c["extension_rays"], c["shadow_rays"]] == rays
+        info = t.info()
+        assert info["pair_traversal"] == (1 if cache == "pair" else 0)
+        if cache == "lds" and kind == "obj":   # (the XML scenes' soup is partly cached: nodes in LDS, the rest global)
+            assert info["scene_in_lds"] == 1 and info["cast_identity"] == 1
+        if cache == "ring8":
+            assert info["ring_rows"] == 8
+    finally:
+        t.destroy()
