@@ -89,3 +89,55 @@ def test_random_scenes_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatc
             assert info["ring_rows"] == 8
     finally:
         t.destroy()
+
+
+def _aimed_rays(flat_arrays, seed, n_origins=24):
+    """Rays aimed at the scene's vertices and edge midpoints as every instance places them (exact
+    vertex / shared-edge hits: several triangles at one distance), from random origins and from
+    the vertices themselves (tMin = 0 on the surface), plus axis-aligned rays through vertices."""
+    from directcomputeraytracing_amd import make_rays
+    rng = np.random.default_rng(seed)
+    pos = flat_arrays["vertices"][:, :3].view(np.float32).astype(np.float64)
+    tri = flat_arrays["triangles"].astype(np.int64)
+    mids = 0.5 * (pos[tri[:, 0]] + pos[tri[:, 1]])
+    pts = np.concatenate([pos, mids])
+    xf = flat_arrays["instance_transforms"].view(np.float32).astype(np.float64)
+    n_inst = len(xf) // 2
+    world = np.concatenate([np.c_[pts, np.ones(len(pts))] @ xf[i].reshape(4, 3) for i in range(n_inst)])
+    world = world[rng.choice(len(world), min(len(world), 4000), replace=False)]
+    o = rng.uniform([-3, -0.2, -5], [3, 3, 3], (n_origins, 3))
+    above = world + np.array([0.0, 2.0, 0.0])
+    O = np.concatenate([np.repeat(o, len(world), 0), world, above])
+    T = np.concatenate([np.tile(world, (n_origins, 1)), world[rng.permutation(len(world))], world])
+    D = T - O                                      # (the last block: straight down through every vertex)
+    keep = np.linalg.norm(D, axis=1) > 1e-9
+    O, D = O[keep], D[keep]
+    D /= np.linalg.norm(D, axis=1, keepdims=True)
+    r = make_rays(O.astype(np.float32), D.astype(np.float32), 0.0, np.inf)
+    k = len(r) // 4
+    r["t_max"][:k] = rng.uniform(0.05, 3.0, k)
+    return r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("features", [0x0D, 0x05])
+@pytest.mark.parametrize("kind", ["obj", "xml"])
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_scene_aimed_rays_bit_exact(gpu_tracer, oracle_mod, tmp_path, kind, seed, features):
+    """trace_rays / occluded (the closest-hit and any-hit casts) on rays aimed exactly at
+    vertices and shared edges: hits, distances, barycentrics, triangle and instance ids and the
+    occlusion bits equal the oracle's (its visit order settles every tie)."""
+    from test_scene_pin import _flat_arrays
+    s = _scene(kind, seed, tmp_path)
+    gpu_tracer.on_scene_loaded(s)
+    flat = oracle_mod.flat_with_own_bvh(s)
+    rays = _aimed_rays(_flat_arrays(flat), seed)
+    assert len(rays) > 10000
+    h_gpu = gpu_tracer.trace_rays(rays, features)
+    h_cpu, _ = oracle_mod.trace_rays(flat, rays, features)
+    bad = np.nonzero((h_gpu.view(np.uint8).reshape(len(rays), -1) != h_cpu.view(np.uint8).reshape(len(rays), -1)).any(1))[0]
+    assert len(bad) == 0, f"{len(bad)} of {len(rays)} hits differ, first {bad[:5]}"
+    assert np.array_equal(gpu_tracer.occluded(rays, features), oracle_mod.occluded(flat, rays, features)[0])
+    hit = np.isfinite(h_cpu["t"]) if "t" in (h_cpu.dtype.names or ()) else None
+    if hit is not None:
+        assert hit.mean() > 0.05   # (the rays do reach the geometry)
