@@ -141,3 +141,57 @@ def test_random_scene_aimed_rays_bit_exact(gpu_tracer, oracle_mod, tmp_path, kin
     hit = np.isfinite(h_cpu["t"]) if "t" in (h_cpu.dtype.names or ()) else None
     if hit is not None:
         assert hit.mean() > 0.05   # (the rays do reach the geometry)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["obj", "xml"])
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_scene_pipelines_bit_exact(native_lib, golden_luts, oracle_mod, tmp_path, kind, seed):
+    """The bench's construction (make_pipelines: two stream-partitioned pipelines with halo rows,
+    virtual batch starts, image batches) on a random scene, 64x160 so both pipelines own
+    stripes: the device-summed film of images 0..2 equals the oracle's film, and the ray counts
+    its counts (halo rows traced by both pipelines counted twice)."""
+    from test_gpu_parity import same_bits
+    from directcomputeraytracing_amd import Scene, make_pipelines, render_images_concurrently
+    from directcomputeraytracing_amd.partition import halo_for_radius, render_rows, stream_partition
+    W, H, images = 64, 160, 3
+    s = Scene((W, H))
+    if kind == "obj":
+        R.setup_obj_scene(s, R.write_obj_scene(tmp_path, seed), seed, W, H)
+    else:
+        s.load_from_file(R.write_xml_scene(tmp_path, seed, W, H))
+    assert tuple(s.resolution) == (W, H)
+    filt = s.filter_params()
+    ts = make_pipelines(s, 1 << 12, streams=2, images=images, iterations=8)
+    try:
+        for t in ts:   # (the tracers' own GPU-built LUTs: bit-identical to the golden ones)
+            t.clear_film()
+            t.reset_stats()
+        render_images_concurrently(ts, 0, images, filt)
+        ts[0].add_film_device(ts[1].film_device_ptr())
+        ts[0].synchronize()
+        film = ts[0].read_film()
+        ext = sum(t.counters()["extension_rays"] for t in ts)
+        shadow = sum(t.counters()["shadow_rays"] for t in ts)
+    finally:
+        for t in ts:
+            t.destroy()
+    flat = oracle_mod.flat_with_own_bvh(s)
+    ref = np.zeros_like(film)
+    halo = max(1, halo_for_radius(filt.radius, H))
+    a, b = (set(render_rows(H, *stream_partition(H, 1, 0, 2, k, 64), halo)) for k in range(2))
+    twice = sorted(a & b)
+    ext_ref = shadow_ref = 0
+    for fs in range(images):
+        fr = oracle_mod.frame_params(s, fs)
+        p, v, _, c = oracle_mod.render(flat, golden_luts, fr, oracle_mod.WAVEFRONT)
+        oracle_mod.sample_convolution(filt, p, v, ref)
+        ext_ref += c["extension_rays"]
+        shadow_ref += c["shadow_rays"]
+        for y in twice:
+            _, _, _, c = oracle_mod.render(flat, golden_luts, fr, oracle_mod.WAVEFRONT, rect=(0, y, W, 1))
+            ext_ref += c["extension_rays"]
+            shadow_ref += c["shadow_rays"]
+    bad = np.count_nonzero(~same_bits(film, ref).all(-1))
+    assert bad == 0, f"{kind} seed {seed}: {bad} film pixels differ"
+    assert (ext, shadow) == (ext_ref, shadow_ref)
