@@ -48,7 +48,7 @@ def test_random_scene_flattening_matches_oracle(native_lib, oracle_mod, tmp_path
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cache", ["lds", "global", "pair", "ring8", "megakernel"])
+@pytest.mark.parametrize("cache", ["lds", "global", "pair", "ring8", "megakernel", "anyhit"])
 @pytest.mark.parametrize("kind", ["obj", "xml"])
 @pytest.mark.parametrize("seed", SEEDS)
 def test_random_scenes_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, tmp_path, kind, seed, cache):
@@ -61,6 +61,12 @@ def test_random_scenes_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatc
         monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
         monkeypatch.setenv("DCRT_STACK_RING", "8")
     s = _scene(kind, seed, tmp_path)
+    if cache == "anyhit":   # ALLOW_ANYHIT_SHADER with translucent materials: the OPACITY kernels
+        rng = np.random.default_rng(seed + 77)
+        s.features = s.features | 0x10
+        for i in range(s.material_count):
+            if rng.random() < 0.6:
+                s.set_material_opacity(i, float(rng.uniform(0.2, 0.9)))
     t = WavefrontPathTracer(path_pool_size=1 << 12, debug_rng=True)
     try:
         if cache == "megakernel":
