@@ -8,13 +8,15 @@ scene (BVH build included) equals the oracle's own flattening, array for array, 
 GPU: every cast kernel variant the tracer can pick for such a scene -- the LDS-cached one (the
 cache-only IDENT kernel for the OBJ scenes), the global-memory one, the pair traversal and the
 8-row stack ring that spills -- and the megakernel render the oracle's image bit for bit."""
+import os
+
 import numpy as np
 import pytest
 
 import random_scenes as R
 from test_xml_translation_pin import REFOBJ, REFXML, check, oracle_xml  # noqa: F401 (oracle_xml: a fixture)
 
-SEEDS = range(6)
+SEEDS = range(int(os.environ.get("DCRT_RANDOM_SCENE_SEEDS", "6")))   # (more for a soak run)
 
 
 def _scene(kind, seed, tmp_path):
