@@ -82,11 +82,11 @@ def _c(rng):
     return ", ".join(f"{v:.3f}" for v in rng.uniform(0.05, 0.95, 3))
 
 
-def write_xml_scene(directory, seed: int, width: int = 48, height: int = 36) -> Path:
+def write_xml_scene(directory, seed: int, width: int = 48, height: int = 36, n_grid: int = 6, n_loose: int = 12) -> Path:
     rng = np.random.default_rng(seed)
     d = Path(directory)
     d.mkdir(parents=True, exist_ok=True)
-    _write_soup(d / "soup.obj", *soup(rng))
+    _write_soup(d / "soup.obj", *soup(rng, n_grid, n_loose))
     n_b = len(_BSDFS)
     picks = rng.choice(n_b, 4, replace=False)
     bsdfs = "".join("  " + _BSDFS[k].format(id=f"b{i}", c=_c(rng), a=f"{rng.uniform(0.02, 0.8):.3f}") + "\n"
