@@ -153,4 +153,10 @@ def setup_obj_scene(scene, path, seed: int, width: int = 48, height: int = 36):
         scene.set_environment_light(tuple(rng.uniform(0.1, 0.6, 3)))
     scene.set_camera((float(rng.uniform(-0.3, 0.3)), 1.6, -3.2), (float(rng.uniform(0.2, 0.35)), 0.0, 0.0))
     scene.set_max_bounce(int(rng.integers(2, 7)))
+    # the lens (Scene.cpp:837-847, RayTracingCommon.inc.hlsl:38-86): pinhole or thin lens, disk
+    # (blades <= 2) or polygonal aperture, any rotation
+    scene.set_lens(camera_type=int(rng.integers(0, 2)), fov_x=float(rng.uniform(0.6, 1.4)),
+                   focal_length=float(rng.uniform(0.03, 0.07)), focal_distance=float(rng.uniform(2.0, 6.0)),
+                   relative_aperture=float(rng.uniform(1.4, 16.0)), blade_count=int(rng.choice([0, 1, 2, 3, 5, 6, 8])),
+                   aperture_rotation=float(rng.uniform(0.0, 6.3)))
     return scene
