@@ -5,9 +5,10 @@ a jittered height field (shared edges, exactly flat axis-aligned patches), loose
 triangles, zero-area triangles (a repeated vertex, collinear vertices) and exact duplicates
 (coincident triangles: equal hit distances, so the reference's visit order decides the hit) --
 into a Mitsuba XML scene with several transformed instances of it, rectangles, random BSDFs
-(every type the loader knows), an area light, and optionally a constant environment and a
+(every type the loader knows, an albedo bitmap on some), an area light, and optionally a constant environment and a
 directional light; or into an OBJ scene (identity instances, the cache-only IDENT kernel) with a
-point light. Inputs are generated here; the expected outputs come from the oracle."""
+point light, a random lens and sometimes an environment cube map. Inputs are generated here; the expected
+outputs come from the oracle."""
 from pathlib import Path
 
 import numpy as np
@@ -91,13 +92,23 @@ def write_xml_scene(directory, seed: int, width: int = 48, height: int = 36, n_g
     picks = rng.choice(n_b, 4, replace=False)
     bsdfs = "".join("  " + _BSDFS[k].format(id=f"b{i}", c=_c(rng), a=f"{rng.uniform(0.02, 0.8):.3f}") + "\n"
                     for i, k in enumerate(picks))
+    if rng.random() < 0.5:   # an albedo bitmap (binary PPM) on the last material: texture sampling in MATERIAL
+        m = int(rng.integers(2, 9))
+        img = rng.integers(0, 256, (m, m + 1, 3), dtype=np.uint8)
+        (d / "albedo.ppm").write_bytes(f"P6 {m + 1} {m} 255\n".encode() + img.tobytes())
+        kind = "diffuse" if rng.random() < 0.5 else "roughplastic"
+        field = "reflectance" if kind == "diffuse" else "diffuse_reflectance"
+        bsdfs += (f'  <bsdf type="{kind}" id="bt"><texture name="{field}" type="bitmap"><string name="filename" '
+                  'value="albedo.ppm"/></texture></bsdf>\n')
+    textured = "bt" in bsdfs
     shapes = []
     for k in range(int(rng.integers(2, 5))):
         m = mitsuba_matrix(tuple(rng.uniform([-1.5, -0.3, -1.5], [1.5, 0.5, 1.5])), yaw=float(rng.uniform(0, 360)),
                            pitch=float(rng.choice([0.0, rng.uniform(-30, 30)])), scale=(float(rng.uniform(0.6, 1.4)),) * 3)
         if k == 0:
             m = mitsuba_matrix()                       # one identity instance beside the transformed ones
-        shapes.append(f'  <shape type="obj" id="soup{k}"><string name="filename" value="soup.obj"/><ref id="b{k % 4}"/>'
+        ref = "bt" if textured and k == 1 else f"b{k % 4}"
+        shapes.append(f'  <shape type="obj" id="soup{k}"><string name="filename" value="soup.obj"/><ref id="{ref}"/>'
                       f'<transform name="to_world"><matrix value="{m}"/></transform></shape>\n')
     shapes.append(f'  <shape type="rectangle" id="floor"><ref id="b{int(rng.integers(0, 4))}"/><transform name="to_world">'
                   f'<matrix value="{mitsuba_matrix((0, -0.31, 0), pitch=-90, scale=(4, 4, 1))}"/></transform></shape>\n')
@@ -150,7 +161,8 @@ def setup_obj_scene(scene, path, seed: int, width: int = 48, height: int = 36):
                            bool(t in (1, 2, 3) and rng.random() < 0.5), bool(rng.random() < 0.5))
     scene.add_point_light(tuple(rng.uniform([-1, 1.5, -1], [1, 2.5, 1])), (6.0, 5.5, 5.0))
     if rng.random() < 0.5:
-        scene.set_environment_light(tuple(rng.uniform(0.1, 0.6, 3)))
+        from directcomputeraytracing_amd.scenes import env_cube
+        scene.set_environment_light(tuple(rng.uniform(0.1, 0.6, 3)), env_cube(8, seed) if rng.random() < 0.5 else None)
     scene.set_camera((float(rng.uniform(-0.3, 0.3)), 1.6, -3.2), (float(rng.uniform(0.2, 0.35)), 0.0, 0.0))
     scene.set_max_bounce(int(rng.integers(2, 7)))
     # the lens (Scene.cpp:837-847, RayTracingCommon.inc.hlsl:38-86): pinhole or thin lens, disk
