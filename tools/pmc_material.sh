@@ -1,4 +1,6 @@
 #!/bin/bash
+# MATERIAL's VALU lane utilisation (rocprofv3 PMC VALUUtilization, one pass per mode) on
+# tools/material_probe.py's default and all-diffuse scenes (GPU box); output under gpurun_out/mat.
 set -u
 ROOTDIR="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOTDIR/gpurun_out/mat"

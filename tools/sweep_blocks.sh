@@ -1,4 +1,6 @@
 #!/bin/bash
+# Cast workgroups per CU sweep (DCRT_CAST_BLOCKS_PER_CU = 1..5) on the default bench (GPU box);
+# one log per setting under gpurun_out/blk_*.log.
 set -u
 mkdir -p gpurun_out
 for b in 1 2 3 4 5; do
