@@ -7,7 +7,9 @@ RapidXml / tinyobjloader / MikkTSpace (where oracle/_ref is built), and the prod
 scene (BVH build included) equals the oracle's own flattening, array for array, bit for bit.
 GPU: every cast kernel variant the tracer can pick for such a scene -- the LDS-cached one (the
 cache-only IDENT kernel for the OBJ scenes), the global-memory one, the pair traversal and the
-8-row stack ring that spills -- and the megakernel render the oracle's image bit for bit."""
+8-row stack ring that spills, the opacity kernels, the split EXT / SHADOW casts, CONTROL-written
+batch starts and the drain-completion kernel -- and the megakernel render the oracle's image bit
+for bit."""
 import os
 
 import numpy as np
@@ -50,7 +52,7 @@ def test_random_scene_flattening_matches_oracle(native_lib, oracle_mod, tmp_path
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cache", ["lds", "global", "pair", "ring8", "megakernel", "anyhit"])
+@pytest.mark.parametrize("cache", ["lds", "global", "pair", "ring8", "megakernel", "anyhit", "split", "no_virtual", "drain"])
 @pytest.mark.parametrize("kind", ["obj", "xml"])
 @pytest.mark.parametrize("seed", SEEDS)
 def test_random_scenes_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, tmp_path, kind, seed, cache):
@@ -62,6 +64,14 @@ def test_random_scenes_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatc
     if cache == "ring8":
         monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
         monkeypatch.setenv("DCRT_STACK_RING", "8")
+    # the reference's two cast kernels (EXT, then SHADOW), batch starts written out by CONTROL,
+    # and the drain-completion kernel for the last few hundred paths
+    if cache == "split":
+        monkeypatch.setenv("DCRT_SPLIT_CASTS", "1")
+    if cache == "no_virtual":
+        monkeypatch.setenv("DCRT_VIRTUAL_START", "0")
+    if cache == "drain":
+        monkeypatch.setenv("DCRT_DRAIN_PATHS", "300")
     s = _scene(kind, seed, tmp_path)
     if cache == "anyhit":   # ALLOW_ANYHIT_SHADER with translucent materials: the OPACITY kernels
         rng = np.random.default_rng(seed + 77)
