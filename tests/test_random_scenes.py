@@ -243,3 +243,39 @@ def test_random_large_scenes_bit_exact(native_lib, golden_luts, oracle_mod, monk
             assert info["ring_rows"] == 8 and t.ring_spills() > 0
     finally:
         t.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["flat", "pairs"])
+@pytest.mark.parametrize("kind", ["obj", "xml"])
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_scene_traversal_counters_match_oracle(native_lib, golden_luts, oracle_mod, monkeypatch, tmp_path, kind, seed,
+                                                      order):
+    """The counting cast kernels walk the reference's order node for node on random scenes too:
+    node visits, triangle tests and BLAS entries of the extension and shadow rays equal the
+    oracle's (BVHAccel.inc.hlsl's iterationCounter and friends), on PackBVH's node order and on the
+    device's child-pair order."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    if order == "pairs":
+        monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
+        monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1")
+    s = _scene(kind, seed, tmp_path)
+    t = WavefrontPathTracer(path_pool_size=1 << 12)
+    try:
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        assert t.info()["pair_traversal"] == (1 if order == "pairs" else 0)
+        t.set_instrumentation(True, True)
+        t.reset_stats()
+        t.render_images(4, 1)
+        st = t.traversal_stats()
+        c = t.counters()
+    finally:
+        t.destroy()
+    _, _, _, ref = oracle_mod.render(oracle_mod.flat_with_own_bvh(s), golden_luts, oracle_mod.frame_params(s, 4), oracle_mod.WAVEFRONT)
+    assert (c["extension_rays"], c["shadow_rays"]) == (ref["extension_rays"], ref["shadow_rays"])
+    got = [st[k] for k in ("ext_node_visits", "ext_triangle_tests", "ext_blas_entries", "shadow_node_visits",
+                           "shadow_triangle_tests", "shadow_blas_entries")]
+    want = [ref[k] for k in ("node_visits", "triangle_tests", "blas_entries", "shadow_node_visits", "shadow_triangle_tests",
+                             "shadow_blas_entries")]
+    assert got == want
