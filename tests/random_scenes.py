@@ -83,7 +83,8 @@ def _c(rng):
     return ", ".join(f"{v:.3f}" for v in rng.uniform(0.05, 0.95, 3))
 
 
-def write_xml_scene(directory, seed: int, width: int = 48, height: int = 36, n_grid: int = 6, n_loose: int = 12) -> Path:
+def write_xml_scene(directory, seed: int, width: int = 48, height: int = 36, n_grid: int = 6, n_loose: int = 12,
+                    n_instances: int = 0) -> Path:
     rng = np.random.default_rng(seed)
     d = Path(directory)
     d.mkdir(parents=True, exist_ok=True)
@@ -102,7 +103,7 @@ def write_xml_scene(directory, seed: int, width: int = 48, height: int = 36, n_g
                   'value="albedo.ppm"/></texture></bsdf>\n')
     textured = "bt" in bsdfs
     shapes = []
-    for k in range(int(rng.integers(2, 5))):
+    for k in range(n_instances or int(rng.integers(2, 5))):
         m = mitsuba_matrix(tuple(rng.uniform([-1.5, -0.3, -1.5], [1.5, 0.5, 1.5])), yaw=float(rng.uniform(0, 360)),
                            pitch=float(rng.choice([0.0, rng.uniform(-30, 30)])), scale=(float(rng.uniform(0.6, 1.4)),) * 3)
         if k == 0:
