@@ -539,6 +539,8 @@ def setup_config(scene, name: str, scene_dir: Path | str, small: bool = False, m
 
 
 def default_pool(width: int, height: int) -> int:
-    """Path-pool slots for several images in flight: 2^24 at 1080p, 2^26 at 4K."""
-    return 1 << 24 if width * height <= (1 << 21) else 1 << 26
+    """Path-pool slots for several images in flight: 2^25 at 1080p (16 images, 8 per pipeline of
+    the bench's two; 2^24 measured 1.0-1.8 % slower on Cornell and 3.6 % on coffee,
+    profiles/r05_ab_pool.txt), 2^26 at 4K (the most 32-bit pool offsets allow)."""
+    return 1 << 25 if width * height <= (1 << 21) else 1 << 26
 

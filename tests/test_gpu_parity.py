@@ -979,7 +979,7 @@ def test_anyhit_megakernel_bit_exact(native_lib, golden_luts, oracle_mod, name):
 @pytest.mark.parametrize("config,images", [("cornell", 4), ("coffee", 1), ("spaceship", 1), ("spaceship_close", 1), ("lamp", 1)])
 def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle_mod, tmp_path, config, images):
     """The bench's own configurations at full size, built by the bench's own code
-    (make_pipelines, as bench.py does): 8 bounces (lamp: its XML's depth), the default pool (2^24
+    (make_pipelines, as bench.py does): 8 bounces (lamp: its XML's depth), the default pool (2^25
     slots at 1080p, 2^26 at 4K) split over two concurrent stream-partitioned pipelines, virtual
     batch starts, the GPU-built LUTs and each config's default cast kernel -- Cornell 1080p: the
     cache-only IDENT kernel; coffee 1080p (configs[2], Kulla-Conty on): the global-memory kernel;

@@ -108,7 +108,7 @@ def main():
     ap.add_argument("--configs", default="cornell,coffee,spaceship,spaceship_close,lamp")
     ap.add_argument("--scene-dir", default="/tmp/dcrt_scenes")
     ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines (bench.py --streams)")
-    ap.add_argument("--pool", type=int, default=0, help="path pool slots (0: 2^24 at 1080p, 2^26 at 4K)")
+    ap.add_argument("--pool", type=int, default=0, help="path pool slots (0: scenes.default_pool: 2^25 at 1080p, 2^26 at 4K)")
     ap.add_argument("--small", action="store_true", help="small meshes (CI smoke)")
     args = ap.parse_args()
     for name in args.configs.split(","):

@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--streams", type=int, default=2)
     ap.add_argument("--stripe", type=int, default=64)
     ap.add_argument("--images", type=int, default=16)
-    ap.add_argument("--pool", type=int, default=1 << 24)
+    ap.add_argument("--pool", type=int, default=1 << 25)
     args = ap.parse_args()
     from directcomputeraytracing_amd import Scene, WavefrontPathTracer, scenes
     from directcomputeraytracing_amd.partition import halo_for_radius, stream_partition

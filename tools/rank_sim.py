@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--image-batch", type=int, default=0)
     ap.add_argument("--stripe", type=int, default=64)
-    ap.add_argument("--pool", type=int, default=1 << 24)
+    ap.add_argument("--pool", type=int, default=1 << 25)
     ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines per rank (bench.py --streams)")
     ap.add_argument("--rank0-only", action="store_true", help="time rank 0's share only (sweeps)")
     ap.add_argument("--fixed-pool", action="store_true", help="pool // streams per pipeline (no pipeline_pool sizing)")
