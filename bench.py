@@ -60,8 +60,9 @@ def parse():
                     help="path pool slots (0: 2^25 at 1080p = 16 images in flight, 8 per pipeline; 2^26 at 4K)")
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="concurrent wavefront pipelines per GPU (film partitions on their own streams)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="concurrent wavefront pipelines per GPU (film partitions on their own streams); 0: 3 for the "
+                         "one-GPU Cornell headline, 2 otherwise (profiles/r05_ab_pool.txt)")
     ap.add_argument("--image-batch", type=int, default=0, help="images per wavefront batch (0 = automatic)")
     ap.add_argument("--roofline-images", type=int, default=0,
                     help="images of the roofline leg (0 = the timed images, so its launches are the timed region's)")
@@ -241,7 +242,12 @@ def main():
         desc = scenes.setup_config(scene, args.config, args.scene_dir, multiscattering=not args.no_multiscattering)
         args.width, args.height = scene.resolution
         workload = f"{desc}, {{spp}} spp ({world} spp/step, film stripes across {world} GPU(s)), wavefront"
-    args.pool = args.pool or scenes.default_pool(args.width, args.height)
+    # pipelines per GPU: three on the one-GPU Cornell headline (its LDS-resident, VALU-bound cast and
+    # memory-bound MATERIAL overlap best three ways: -1 to -3 %), two elsewhere (coffee +2-3 % with
+    # three; a rank of N > 1 renders thin stripes, where a third pipeline adds halo rows)
+    if args.streams <= 0:
+        args.streams = 3 if (args.config == "cornell" and world == 1) else 2
+    args.pool = args.pool or scenes.default_pool(args.width, args.height, args.streams)
     # (the coffee scene without configs[2]'s multiscattering is its own workload)
     config_name = args.config + ("_noms" if args.config == "coffee" and args.no_multiscattering else "")
     filt = scene.filter_params()
@@ -629,11 +635,11 @@ def spaceship_leg(args, luts_arrays) -> dict:
     scene = Scene((3840, 2160))
     desc = scenes.setup_config(scene, "spaceship", args.scene_dir)
     W, H = scene.resolution
-    pool = scenes.default_pool(W, H)
+    pool = scenes.default_pool(W, H, 2)
     filt = scene.filter_params()
     halo = max(1, halo_for_radius(filt.radius, H))
     n = args.spaceship_spp
-    K = max(1, args.streams)
+    K = 2   # (the configs[3] leg keeps its two pipelines whatever the headline runs)
     subs = []
     try:
         for s_ in range(K):

@@ -538,9 +538,10 @@ def setup_config(scene, name: str, scene_dir: Path | str, small: bool = False, m
     raise ValueError(f"unknown config {name!r} (one of {', '.join(CONFIGS)})")
 
 
-def default_pool(width: int, height: int) -> int:
-    """Path-pool slots for several images in flight: 2^25 at 1080p (16 images, 8 per pipeline of
-    the bench's two; 2^24 measured 1.0-1.8 % slower on Cornell and 3.6 % on coffee,
-    profiles/r05_ab_pool.txt), 2^26 at 4K (the most 32-bit pool offsets allow)."""
-    return 1 << 25 if width * height <= (1 << 21) else 1 << 26
+def default_pool(width: int, height: int, streams: int = 2) -> int:
+    """Path-pool slots for several images in flight, split over `streams` pipelines: 2^24 per
+    pipeline at 1080p (8 images per batch: 2^23 measured 1-2 % slower on Cornell and 3.6 % on
+    coffee, 2^25 slower again, profiles/r05_ab_pool.txt), 2^26 in all at 4K (two pipelines of
+    2^25: the most 32-bit pool offsets allow one tracer is 2^26)."""
+    return max(1, streams) << 24 if width * height <= (1 << 21) else 1 << 26
 
