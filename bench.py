@@ -59,7 +59,8 @@ def parse():
     ap.add_argument("--pool", type=int, default=0,
                     help="path pool slots (0: 2^25 at 1080p = 16 images in flight, 8 per pipeline; 2^26 at 4K)")
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
-    ap.add_argument("--stripe", type=int, default=64, help="film stripe height for N>1")
+    ap.add_argument("--stripe", type=int, default=256,
+                    help="film stripe height for N>1 (256: fewer halo rows than 64, -1 to -2 %% per rank at N = 2 / 4, profiles/r05_ab_pool.txt)")
     ap.add_argument("--streams", type=int, default=0,
                     help="concurrent wavefront pipelines per GPU (film partitions on their own streams); 0: 3 for the "
                          "one-GPU Cornell headline, 2 otherwise (profiles/r05_ab_pool.txt)")

@@ -19,7 +19,7 @@ sys.path.insert(0, str(ROOT))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--streams", type=int, default=2)
-    ap.add_argument("--stripe", type=int, default=64)
+    ap.add_argument("--stripe", type=int, default=256)
     ap.add_argument("--images", type=int, default=16)
     ap.add_argument("--pool", type=int, default=1 << 25)
     args = ap.parse_args()

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--gpus", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--image-batch", type=int, default=0)
-    ap.add_argument("--stripe", type=int, default=64)
+    ap.add_argument("--stripe", type=int, default=256)
     ap.add_argument("--pool", type=int, default=1 << 25)
     ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines per rank (bench.py --streams)")
     ap.add_argument("--rank0-only", action="store_true", help="time rank 0's share only (sweeps)")

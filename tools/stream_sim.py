@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--streams", default="1,2,3,4")
     ap.add_argument("--steps", type=int, default=32)
-    ap.add_argument("--stripe", type=int, default=64)
+    ap.add_argument("--stripe", type=int, default=256)
     ap.add_argument("--pool", type=int, default=1 << 25, help="total path-pool slots, split over the streams")
     ap.add_argument("--check", action="store_true", help="compare the summed film with the 1-stream film")
     ap.add_argument("--world", type=int, default=1, help="emulate rank --rank of an N-GPU film split")
