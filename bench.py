@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--snapshot-spp", type=int, default=0,
                     help="progressive: reduce the film onto rank 0 every K images (configs[4]); 0 = once at the end")
     ap.add_argument("--pool", type=int, default=0,
-                    help="path pool slots (0: 2^25 at 1080p = 16 images in flight, 8 per pipeline; 2^26 at 4K)")
+                    help="path pool slots (0: 2^24 per pipeline at 1080p = 8 images in flight each; 2^26 at 4K)")
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=256,
                     help="film stripe height for N>1 (256: fewer halo rows than 64, -1 to -2 %% per rank at N = 2 / 4, profiles/r05_ab_pool.txt)")
