@@ -246,6 +246,7 @@ def main():
     # pipelines per GPU: three on the one-GPU Cornell headline (its LDS-resident, VALU-bound cast and
     # memory-bound MATERIAL overlap best three ways: -1 to -3 %), two elsewhere (coffee +2-3 % with
     # three; a rank of N > 1 renders thin stripes, where a third pipeline adds halo rows)
+    args.streams_explicit = args.streams > 0   # (the configs[3] leg follows an explicit --streams)
     if args.streams <= 0:
         args.streams = 3 if (args.config == "cornell" and world == 1) else 2
     args.pool = args.pool or scenes.default_pool(args.width, args.height, args.streams)
@@ -636,11 +637,12 @@ def spaceship_leg(args, luts_arrays) -> dict:
     scene = Scene((3840, 2160))
     desc = scenes.setup_config(scene, "spaceship", args.scene_dir)
     W, H = scene.resolution
-    pool = scenes.default_pool(W, H, 2)
+    # two pipelines unless --streams was given (the headline's automatic count is Cornell's)
+    K = args.streams if getattr(args, "streams_explicit", False) else 2
+    pool = scenes.default_pool(W, H, K)
     filt = scene.filter_params()
     halo = max(1, halo_for_radius(filt.radius, H))
     n = args.spaceship_spp
-    K = 2   # (the configs[3] leg keeps its two pipelines whatever the headline runs)
     subs = []
     try:
         for s_ in range(K):

@@ -15,6 +15,7 @@ LIB_PATH = PKG_DIR / "libdcrt.so"
 
 # ---- status codes / flags (dcrt.h) -----------------------------------------
 DCRT_OK = 0
+ABI_VERSION = 2          # DCRT_ABI_VERSION: load_library refuses a libdcrt.so of another
 ERRORS = {-1: "DCRT_E_INVALID_ARG", -2: "DCRT_E_HIP", -3: "DCRT_E_NO_SCENE", -4: "DCRT_E_IO",
           -5: "DCRT_E_LIMIT", -6: "DCRT_E_NO_DEVICE"}
 LIGHT_INDEX_INVALID = 0xFFFFFFFF
@@ -179,6 +180,7 @@ _I = C.c_int
 _U = C.c_uint32
 _FP = C.POINTER(C.c_float)
 SIGNATURES = [
+    ("dcrt_abi_version", _I, []),
     ("dcrt_version", C.c_char_p, []),
     ("dcrt_last_error", C.c_char_p, []),
     ("dcrt_device_count", _I, [C.POINTER(C.c_int)]),
@@ -239,6 +241,7 @@ SIGNATURES = [
     ("dcrt_tracer_read_samples", _I, [_P, _FP, _FP]),
     ("dcrt_tracer_read_rng", _I, [_P, C.POINTER(C.c_uint32)]),
     ("dcrt_tracer_film_device_ptr", _I, [_P, C.POINTER(_P)]),
+    ("dcrt_tracer_sample_device_ptrs", _I, [_P, C.POINTER(_P), C.POINTER(_P)]),
     ("dcrt_tracer_copy_film_device", _I, [_P, _P]),
     ("dcrt_tracer_add_film_device", _I, [_P, _P]),
     ("dcrt_tracer_prepare_images", _I, [_P, C.c_uint32]),
@@ -281,6 +284,8 @@ def load_library(path: os.PathLike | str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.dcrt_abi_version() != ABI_VERSION:
+        raise DCRTError(f"{p}: ABI version {lib.dcrt_abi_version()}, this binding expects {ABI_VERSION}")
     _lib = lib
     return lib
 

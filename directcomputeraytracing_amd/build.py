@@ -176,13 +176,16 @@ def _build_sanitized_locked(san, sources, stamp: Path, digest: str) -> Path:
 
 
 EXAMPLE_SRC = ROOT / "examples" / "dcrt_render.cpp"
+EXAMPLE_SOURCES = [EXAMPLE_SRC, ROOT / "examples" / "mi355x_path_tracer.cpp"]
+EXAMPLE_HEADERS = [ROOT / "examples" / "mi355x_path_tracer.h", ROOT / "examples" / "renderer_loop.h"]
 EXAMPLE_BIN = ROOT / "examples" / "dcrt_render"
 
 
 def build_examples(force: bool = False) -> Path:
-    """examples/dcrt_render: a C++ host of libdcrt.so through the C ABI alone."""
+    """examples/dcrt_render: a C++ host of libdcrt.so through the C ABI alone -- the reference's
+    CPathTracer plugin slot filled by CMI355XPathTracer, driven by its frame loop."""
     lib = build_native()
-    digest = _digest([EXAMPLE_SRC, ROOT / "include" / "dcrt.h", lib])
+    digest = _digest([*EXAMPLE_SOURCES, *EXAMPLE_HEADERS, ROOT / "include" / "dcrt.h", lib])
     stamp = EXAMPLE_BIN.with_suffix(".sha256")
     if not force and _fresh(EXAMPLE_BIN, stamp, digest):
         return EXAMPLE_BIN
@@ -190,7 +193,8 @@ def build_examples(force: bool = False) -> Path:
         if not force and _fresh(EXAMPLE_BIN, stamp, digest):
             return EXAMPLE_BIN
         cxx = shutil.which("g++") or "g++"
-        cmd = [cxx, "-O2", "-std=c++17", "-Wall", str(EXAMPLE_SRC), "-I", str(ROOT / "include"), "-L", str(PKG_DIR), "-ldcrt",
+        cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wextra", *map(str, EXAMPLE_SOURCES), "-I", str(ROOT / "include"),
+               "-L", str(PKG_DIR), "-ldcrt",
                "-Wl,-rpath,$ORIGIN/../directcomputeraytracing_amd", "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(EXAMPLE_BIN)]
         subprocess.run(cmd, check=True)
         stamp.write_text(digest)

@@ -731,18 +731,20 @@ constexpr uint32_t kNoItem = 0xFFFFFFFFu;   // a fetch's "no ray for this item"
 // a per-lane global column (sc.spill). Before every batch of kVisitsPerCheck node visits the wave
 // checks that each lane's window can take the batch: a visit writes the row above its top (push or
 // not), so the window must hold at most ringRows - 1 entries before each visit, i.e. at most
-// ringRows - 3 before the batch; and a visit (or the following leaf work) pops at most one entry,
+// ringRows - kVisitsPerCheck before the batch; and a visit (or the following leaf work) pops at most one entry,
 // so with entries spilled below the window it must hold at least kVisitsPerCheck + 1. A lane
 // outside those bounds moves entries between the window and its spill column until the window
-// holds ringRows / 2 (or every entry). The entries' values and order are untouched: traversal,
+// holds ringRows / 2 (or every entry); the host keeps ringRows >= 2 * (kVisitsPerCheck + 1), so
+// that window passes both checks (kMinRingRows). The entries' values and order are untouched: traversal,
 // hits and counts are those of the whole-stack kernels bit for bit.
+constexpr uint32_t kMinRingRows = 2u * ((uint32_t)kVisitsPerCheck + 1u);
 template <bool RING>
 __device__ __forceinline__ void ring_maintain(const DeviceScene& sc, TravState& s, bool active, uint32_t* lds, uint32_t shift)
 {
     if constexpr (RING) {
         const uint32_t stride = 4u << shift;
         const uint32_t live = s.sp - s.base;
-        const bool spill = active && live > (sc.ringRows - 3u) * stride;
+        const bool spill = active && live > (sc.ringRows - (uint32_t)kVisitsPerCheck) * stride;
         const bool fill = active && s.base != 0u && live <= (uint32_t)kVisitsPerCheck * stride;
         if (__builtin_expect(__ballot(spill | fill) != 0ull, 0)) {
             const uint32_t lanes = gridDim.x * blockDim.x;

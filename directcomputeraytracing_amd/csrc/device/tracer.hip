@@ -466,9 +466,13 @@ struct dcrt_tracer {
     uint32_t drainResident = 0;        // drain_kernel grid (resident workgroups)
     uint32_t drainPaths = 0;           // drain_kernel threshold (DCRT_DRAIN_PATHS; 0: no drain launches -- the default: profiles/r04_ab_virtual_drain.txt)
     int mode = 0;                      // 0 wavefront (WavefrontPathTracer), 1 megakernel (MegakernelPathTracer)
+    uint32_t castResidentInstr = 0;    // the same for the counting kernels (whole stack: castLdsFull)
+    uint32_t castResidentInstrOpacity = 0;
     uint32_t CastGrid(uint32_t block, bool opacity) const
     {
-        return std::min<uint32_t>((poolSize + block - 1) / block, opacity ? castResidentOpacity : castResident);
+        const uint32_t resident = instrCounters ? (opacity ? castResidentInstrOpacity : castResidentInstr)
+                                                : (opacity ? castResidentOpacity : castResident);
+        return std::min<uint32_t>((poolSize + block - 1) / block, resident);
     }
 };
 
@@ -886,11 +890,15 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
             int forced = -1;
             if (const char* e = std::getenv("DCRT_STACK_RING")) forced = std::atoi(e);
             const uint32_t K = forced > 0 ? (uint32_t)forced : 16u;
-            const bool validK = K >= 8u && K <= 64u && (K & (K - 1u)) == 0u;
-            if (forced > 0 && !validK) { SetLastError("DCRT_STACK_RING: a power of two in [8, 64]"); return DCRT_E_INVALID_ARG; }
+            // (the window must take a batch of kVisitsPerCheck visits after a refill to half: kMinRingRows)
+            const bool validK = K >= std::max(8u, kMinRingRows) && K <= 64u && (K & (K - 1u)) == 0u;
+            if (forced > 0 && !validK) {
+                SetLastError("DCRT_STACK_RING: a power of two in [max(8, 2 * (visits per check + 1)), 64]");
+                return DCRT_E_INVALID_ARG;
+            }
             if (forced > 0) {
                 ringRows = K;
-            } else if (forced < 0 && K < d.stackSize + 2u) {
+            } else if (forced < 0 && validK && K < d.stackSize + 2u) {
                 int whole = 0, ring = 0;
                 CHECKED(castOccupancy(CastKernel(false, false, false, castPair, castIdent, false), castLds, &whole));
                 CHECKED(castOccupancy(CastKernel(false, false, false, castPair, castIdent, true), (size_t)K * castBlock * 4, &ring));
@@ -979,6 +987,13 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         int opacityPerCU = 0;
         CHECKED(castOccupancy(CastKernel(false, true, castAllCached, castPair), castLdsFull, &opacityPerCU));
         castResidentOpacity = (uint32_t)std::max(1, std::min(opacityPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        // the counting kernels keep the whole stack (castLdsFull): their own resident grid, so an
+        // instrumented run has no second partial round of workgroups the shipped kernel lacks
+        int instrPerCU = 0, instrOpacityPerCU = 0;
+        CHECKED(castOccupancy(CastKernel(true, false, castAllCached, castPair, castIdent, false), castLdsFull, &instrPerCU));
+        CHECKED(castOccupancy(CastKernel(true, true, castAllCached, castPair), castLdsFull, &instrOpacityPerCU));
+        castResidentInstr = (uint32_t)std::max(1, std::min(instrPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
+        castResidentInstrOpacity = (uint32_t)std::max(1, std::min(instrOpacityPerCU, perCU)) * (uint32_t)std::max(1, prop.multiProcessorCount);
         int megaPerCU = 0;
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&megaPerCU, megakernel<false>, (int)castBlock, castLdsFull));
         megaResident = (uint32_t)std::max(1, std::min(megaPerCU, LdsResident(castLdsFull, (const void*)megakernel<false>))) *
@@ -1634,6 +1649,17 @@ DCRT_API int dcrt_tracer_film_device_ptr(dcrt_tracer* t, void** out)
     TRACER_GUARD(t);
     if (!out) return DCRT_E_INVALID_ARG;
     *out = t->film.accum;
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_sample_device_ptrs(dcrt_tracer* t, void** pos, void** val)
+{
+    TRACER_GUARD(t);
+    if (!pos || !val) return DCRT_E_INVALID_ARG;
+    if (!t->film.sampleValue) { SetLastError("no frame parameters: the sample textures are not allocated"); return DCRT_E_INVALID_ARG; }
+    const size_t o = (size_t)t->filmW * t->filmH * t->lastSlot;   // the last image's slot
+    *pos = (void*)(t->film.samplePosition + o);
+    *val = (void*)(t->film.sampleValue + o);
     return DCRT_OK;
 }
 

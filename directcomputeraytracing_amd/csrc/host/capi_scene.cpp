@@ -42,6 +42,7 @@ using dcrt::SetLastError;
 
 extern "C" {
 
+DCRT_API int dcrt_abi_version(void) { return DCRT_ABI_VERSION; }
 DCRT_API const char* dcrt_version(void) { return "dcrt-mi355x 0.1.0 (gfx950)"; }
 DCRT_API const char* dcrt_last_error(void) { return dcrt::g_lastError.c_str(); }
 

@@ -138,6 +138,13 @@ class WavefrontPathTracer:
         check(self._lib.dcrt_tracer_film_device_ptr(self._h, C.byref(p)), "FilmDevicePtr")
         return p.value or 0
 
+    def sample_device_ptrs(self) -> tuple[int, int]:
+        """Device pointers of the current image's sample textures (R32G32F positions, RGBA32F
+        values): what the reference's SampleConvolution pass reads."""
+        pos, val = C.c_void_p(), C.c_void_p()
+        check(self._lib.dcrt_tracer_sample_device_ptrs(self._h, C.byref(pos), C.byref(val)), "SampleDevicePtrs")
+        return pos.value or 0, val.value or 0
+
     def copy_film_device(self, d_dst: int) -> None:
         check(self._lib.dcrt_tracer_copy_film_device(self._h, C.c_void_p(d_dst)), "CopyFilmDevice")
 

@@ -299,6 +299,12 @@ typedef struct dcrt_tracer dcrt_tracer;
 typedef struct dcrt_scene dcrt_scene;
 
 /* ===== version / device ================================================== */
+/* ABI version of this header: bumped whenever a struct changes size or an entry point its
+ * meaning (2: dcrt_tracer_info grew cast_waves_per_cu / ring_rows / stack_lds_rows). A caller
+ * compiled against another header checks dcrt_abi_version() == DCRT_ABI_VERSION before it
+ * passes any struct (a smaller dcrt_tracer_info would be written past its end). */
+#define DCRT_ABI_VERSION 2
+DCRT_API int dcrt_abi_version(void);
 DCRT_API const char* dcrt_version(void);
 DCRT_API const char* dcrt_last_error(void);
 DCRT_API int dcrt_device_count(int* out_count);
@@ -487,6 +493,13 @@ DCRT_API int dcrt_tracer_read_film(dcrt_tracer* tracer, float* out_rgba);       
 DCRT_API int dcrt_tracer_read_samples(dcrt_tracer* tracer, float* out_position, float* out_value); /* W*H*2, W*H*4 */
 DCRT_API int dcrt_tracer_read_rng(dcrt_tracer* tracer, uint32_t* out_state);                   /* W*H*4 (debug_rng) */
 DCRT_API int dcrt_tracer_film_device_ptr(dcrt_tracer* tracer, void** out_ptr);
+/* The current image's sample textures in device memory (m_SamplePositionTexture R32G32F and
+ * m_SampleValueTexture RGBA32F, row-major W x H of the frame resolution; Scene.cpp:863-885),
+ * written by CONTROL / MATERIAL (WriteSample, RayTracingCommon.inc.hlsl:118-122): what the
+ * reference's L1 SampleConvolution pass reads (SampleConvolution.cpp:89-170,
+ * LaunchRendererLoop.cpp:295-297). Valid until the resolution or the image batch changes;
+ * dcrt_tracer_accumulate_film is that pass on the tracer's own film. */
+DCRT_API int dcrt_tracer_sample_device_ptrs(dcrt_tracer* tracer, void** out_position, void** out_value);
 /* Device-to-device copy of the RGBA32F film (W*H*4 floats) into d_dst, e.g. an
  * RCCL buffer for the multi-GPU reduce; synchronous with the tracer stream. */
 DCRT_API int dcrt_tracer_copy_film_device(dcrt_tracer* tracer, void* d_dst);

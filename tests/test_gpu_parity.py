@@ -853,6 +853,73 @@ def test_cpp_host_example_matches_python_host(native_lib, tmp_path):
     assert out["frame"] == out["batch"] == (tmp_path / "py.bmp").read_bytes()
 
 
+def _run_frame_loop(exe, tmp_path, tag, W, H, spp, bounces, *extra):
+    import json
+    import subprocess
+    from directcomputeraytracing_amd import scenes
+    px, col = scenes.POINT_LIGHT_POSITION, scenes.POINT_LIGHT_COLOR
+    film, samples = tmp_path / f"{tag}.film", tmp_path / f"{tag}.samples"
+    args = [str(exe), str(scenes.CORNELL_OBJ), str(W), str(H), str(spp), str(bounces), str(tmp_path / f"{tag}.bmp"),
+            "--point", *map(str, px), *map(str, col), "--pool", str(1 << 16), "--film", str(film), "--samples", str(samples),
+            *extra]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    n = W * H
+    raw = np.fromfile(samples, np.float32)
+    return info, np.fromfile(film, np.float32).reshape(H, W, 4), raw[:2 * n].reshape(H, W, 2), raw[2 * n:].reshape(H, W, 4)
+
+
+@pytest.mark.parametrize("policy", ["sample-count", "frame-index", "fixed"])
+def test_cpathtracer_frame_loop_seed_policies(native_lib, tmp_path, policy):
+    """CMI355XPathTracer (examples/mi355x_path_tracer.h: the reference's eight-virtual CPathTracer
+    slot, PathTracer.h:6-26, over the C ABI alone) driven by the reference's frame loop
+    (examples/renderer_loop.h: LaunchRendererLoop.cpp:159-298). The first frame after the load is
+    the film-dirty quarter-resolution preview (:206-213, :405-406), convolved and then cleared by
+    the resolution change; the frame seed is CScene::m_FrameSeed (WavefrontPathTracer.cpp:412)
+    under each EFrameSeedType policy (:229-264); SampleConvolution runs once per completed image
+    (:295-297). With 3 iterations per frame an image spans several Render calls.
+      * SampleCount: the film of the spp images is render_images(0, spp)'s, bit for bit;
+      * FrameIndex: the seed is not reset after the preview, so the images are first_seed ..;
+      * Fixed (seed 5): every image repeats seed 5's samples; the film is render_images(5, 1)
+        convolved spp times."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    from directcomputeraytracing_amd.build import build_examples
+    exe = build_examples()
+    W, H, spp, bounces = 96, 64, 3, 4
+    # (FrameIndex: 16 iterations per frame, so the 24 x 16 preview image completes in its frame)
+    extra = ["--seed-type", policy, "--iterations", "16" if policy == "frame-index" else "3"]
+    if policy == "fixed":
+        extra += ["--fixed-seed", "5"]
+    info, film, pos, val = _run_frame_loop(exe, tmp_path, policy, W, H, spp, bounces, *extra)
+    assert info["mode"] == "frame_loop" and info["preview_frames"] == 1 and info["images"] == spp
+    s = cornell(W, H, bounces)
+    t = WavefrontPathTracer(path_pool_size=1 << 16)
+    try:
+        t.on_scene_loaded(s)
+        t.clear_film()
+        if policy == "sample-count":
+            assert info["seeds"] == list(range(spp))
+            t.render_images(0, spp)
+        elif policy == "frame-index":
+            # the preview completed its image at seed 0 and advanced the seed; FrameIndex does
+            # not reset it, so the full-resolution images are seeds 1 ..
+            first = info["first_seed"]
+            assert first == 1 and info["seeds"] == list(range(first, first + spp))
+            t.render_images(first, spp)
+        else:
+            assert info["seeds"] == [5] * spp
+            t.render_images(5, 1)
+            for _ in range(spp - 1):
+                t.accumulate_film()
+        ref_pos, ref_val = t.read_samples()
+        ref_film = t.read_film()
+    finally:
+        t.destroy()
+    assert same_bits(pos, ref_pos).all() and same_bits(val, ref_val).all()
+    assert same_bits(film, ref_film).all()
+
+
 def test_postfx_resolve_bit_exact(native_lib, golden_luts, oracle_mod):
     """Exposure (manual / auto via the two-stage log-luminance reduction) + Reinhard + sRGB8."""
     from directcomputeraytracing_amd import PostFxParams, WavefrontPathTracer, srgb_thresholds
