@@ -1043,7 +1043,9 @@ def test_anyhit_megakernel_bit_exact(native_lib, golden_luts, oracle_mod, name):
         t.destroy()
 
 
-@pytest.mark.parametrize("config,images", [("cornell", 4), ("coffee", 1), ("spaceship", 1), ("spaceship_close", 1), ("lamp", 1)])
+# (cornell-20: the driver's timed configuration, bench.py --steps 20 -- one 20-image batch per pipeline)
+@pytest.mark.parametrize("config,images", [("cornell", 4), ("cornell", 20), ("coffee", 1), ("spaceship", 1),
+                                           ("spaceship_close", 1), ("lamp", 1)])
 def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle_mod, tmp_path, config, images):
     """The bench's own configurations at full size, built by the bench's own code
     (make_pipelines, as bench.py does): 8 bounces (lamp: its XML's depth), the default pool (2^24
@@ -1115,6 +1117,60 @@ def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle
             shadow_ref += c["shadow_rays"]
     bad = np.count_nonzero(~same_bits(film, ref).all(-1))
     assert bad == 0, f"{bad} film pixels differ"
+    assert (ext, shadow) == (ext_ref, shadow_ref)
+
+
+def test_rank_share_full_size_bit_exact(native_lib, golden_luts, oracle_mod):
+    """One rank's share of the N = 8 Cornell bench exactly as bench.py builds it on that rank
+    (make_pipelines: world 8, rank 3, the 256-row stripe target, two pipelines per rank of N > 1),
+    image 0 at 1920x1080 / 8 bounces: the rank's film equals the oracle's film on the rows the rank
+    owns and is zero elsewhere, and its ray counts are the oracle's over the rows its pipelines
+    path-trace (owned rows plus the filter's halo)."""
+    from directcomputeraytracing_amd import Scene, make_pipelines, render_images_concurrently, scenes
+    from directcomputeraytracing_amd.partition import halo_for_radius, owned_rows, render_rows, row_runs, stream_partition
+    W, H, world, rank, K, stripe = 1920, 1080, 8, 3, 2, 256
+    s = Scene((W, H))
+    scenes.setup_cornell(s, W, H, 8)
+    filt = s.filter_params()
+    halo = max(1, halo_for_radius(filt.radius, H))
+    ts = make_pipelines(s, scenes.default_pool(W, H, K), streams=K, images=1, iterations=16, world=world, rank=rank,
+                        stripe=stripe)
+    try:
+        for t in ts:
+            t.clear_film()
+            t.reset_stats()
+        render_images_concurrently(ts, 0, 1, filt)
+        for t in ts[1:]:
+            ts[0].add_film_device(t.film_device_ptr())
+        ts[0].synchronize()
+        film = ts[0].read_film()
+        ext = sum(t.counters()["extension_rays"] for t in ts)
+        shadow = sum(t.counters()["shadow_rays"] for t in ts)
+    finally:
+        for t in ts:
+            t.destroy()
+    parts = [stream_partition(H, world, rank, K, k, stripe) for k in range(K)]
+    owned = np.zeros(H, bool)
+    for part in parts:
+        owned |= owned_rows(H, *part)
+    assert 0 < owned.sum() < H // 4
+    flat = oracle_mod.flat_with_own_bvh(s)
+    fr = oracle_mod.frame_params(s, 0)
+    pos = np.zeros((H, W, 2), np.float32)
+    val = np.zeros((H, W, 4), np.float32)
+    ext_ref = shadow_ref = 0
+    for part in parts:
+        for y0, y1 in row_runs(render_rows(H, *part, halo)):
+            p, v, _, c = oracle_mod.render(flat, golden_luts, fr, oracle_mod.WAVEFRONT, rect=(0, y0, W, y1 - y0))
+            pos[y0:y1], val[y0:y1] = p[y0:y1], v[y0:y1]
+            ext_ref += c["extension_rays"]
+            shadow_ref += c["shadow_rays"]
+    ref = np.zeros_like(film)
+    for y0, y1 in row_runs(np.nonzero(owned)[0]):
+        oracle_mod.sample_convolution(filt, pos, val, ref, rows=(y0, y1))
+    assert not film[~owned].any(), "the rank wrote rows it does not own"
+    bad = np.count_nonzero(~same_bits(film[owned], ref[owned]).all(-1))
+    assert bad == 0, f"{bad} owned film pixels differ"
     assert (ext, shadow) == (ext_ref, shadow_ref)
 
 
