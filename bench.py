@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--iterations", type=int, default=16, help="wavefront iterations per graph launch")
     ap.add_argument("--stripe", type=int, default=256,
                     help="film stripe height for N>1 (256: fewer halo rows than 64, -1 to -2 %% per rank at N = 2 / 4, profiles/r05_ab_pool.txt)")
+    ap.add_argument("--partition", choices=["balanced", "stripes"], default="balanced",
+                    help="film tiling over ranks and pipelines: balanced = contiguous equal-cost bands cut from the "
+                         "row-cost probe (rays per film row of one probe image, identical on every rank); stripes = "
+                         "equal-height round-robin stripes of --stripe rows")
     ap.add_argument("--streams", type=int, default=0,
                     help="concurrent wavefront pipelines per GPU (film partitions on their own streams); 0: 3 for the "
                          "one-GPU Cornell headline, 2 otherwise (profiles/r05_ab_pool.txt)")
@@ -256,23 +260,36 @@ def main():
     from directcomputeraytracing_amd.partition import halo_for_radius, render_rows
     halo = max(1, halo_for_radius(filt.radius, args.height))
 
-    def make_tracer(pool, part):
+    def make_tracer(pool, part, bands=None):
         t = WavefrontPathTracer(path_pool_size=pool, iterations_per_render=args.iterations, device=device)
         t.on_scene_loaded(scene)
         t.set_mode(args.mode)
         t.set_image_batch(args.image_batch)
-        if part is not None:
+        if bands is not None:
+            t.set_film_bands(bands, halo)
+        elif part is not None:
             t.set_film_partition(*part, halo)
         return t
+
+    # cost-balanced film bands: the rays per film row of one probe image, the same
+    # on every rank (exact, schedule-independent), cut into world x K contiguous equal-cost bands;
+    # pipeline s of rank r takes band r * K + s. Not timed (it precedes the warm-up).
+    K = max(1, args.streams)
+    row_cost = None
+    rank_bands = None
+    if args.partition == "balanced" and world * K > 1 and args.mode == "wavefront":
+        from directcomputeraytracing_amd import probe_row_cost
+        from directcomputeraytracing_amd.partition import balanced_bands
+        row_cost = probe_row_cost(scene, device=device)
+        rank_bands = balanced_bands(row_cost, world * K, halo)[rank * K:(rank + 1) * K]
 
     # K concurrent pipelines per GPU (--streams): tracer s renders the rank's stripes dealt
     # to it (partition.stream_partition), on its own stream, from its own host thread; the
     # K films have disjoint supports and are summed on the device (add_film_device).
     # (a pipeline's pool just short of a whole number of batches grows by <= 8 %: one drain less)
-    K = max(1, args.streams)
     tracers = make_pipelines(scene, args.pool, streams=K, images=args.steps * world, iterations=args.iterations,
                              world=world, rank=rank, stripe=args.stripe, mode=args.mode, image_batch=args.image_batch,
-                             device=device)
+                             device=device, row_cost=row_cost)
     tracer = tracers[0]
 
     def render_all(first, count):
@@ -421,7 +438,8 @@ def main():
     if K > 1:
         for t in tracers:
             t.destroy()
-        tracer = make_tracer(args.pool, (world, rank, args.stripe) if world > 1 else None)
+        tracer = make_tracer(args.pool, (world, rank, args.stripe) if world > 1 else None,
+                             rank_bands if (rank_bands is not None and world > 1) else None)
     roof = cast_roofline(tracer, R, filt, {"config": config_name, "resolution": [args.width, args.height], "images": R,
                                            "path_pool": args.pool, "world": world}, args.traffic_json)
     st, cr, tm = roof.pop("_stats"), roof.pop("_counters"), roof.pop("_timing")
@@ -458,8 +476,11 @@ def main():
                    "resolution": [args.width, args.height], "spp": images,
                    "max_bounce": args.bounces if args.config == "cornell" else scene.frame_params(0).max_bounce_count,
                    "path_pool": args.pool, "streams_per_gpu": K, "snapshot_spp": args.snapshot_spp or images,
-                   "parallelism": (f"film stripes x{world}" if world > 1 else "single GPU")
-                                  + (f", {K} concurrent pipelines per GPU" if K > 1 else ""),
+                   "parallelism": (f"film {'cost-balanced bands' if rank_bands is not None else 'stripes'} x{world}"
+                                   if world > 1 else "single GPU")
+                                  + (f", {K} concurrent pipelines per GPU" if K > 1 else "")
+                                  + (" (cost-balanced bands)" if rank_bands is not None and world == 1 else ""),
+                   "partition": args.partition if rank_bands is not None else ("stripes" if world * K > 1 else "none"),
                    "rays": int(rays)},
         "roofline": roof,
         "pipeline_roofline": pipeline_roofline(pmc, pmc_src, images / world / elapsed, pipe_achieved, pipe_bytes_R / R),
@@ -469,8 +490,13 @@ def main():
     if per_rank is not None:
         # diagnosable first 8-GPU run: every rank's render time (its stripes + halo rows) and the
         # RCCL film reduce, medians over the repeats; the halo overhead is rows rendered / owned
-        owned = len(render_rows(args.height, world, rank, args.stripe, 0))
-        rendered = len(render_rows(args.height, world, rank, args.stripe, halo))
+        if rank_bands is not None:
+            from directcomputeraytracing_amd.partition import band_render_rows
+            owned = sum(b - a for a, b in rank_bands)
+            rendered = sum(len(band_render_rows(args.height, [b], halo)) for b in rank_bands)
+        else:
+            owned = len(render_rows(args.height, world, rank, args.stripe, 0))
+            rendered = len(render_rows(args.height, world, rank, args.stripe, halo))
         result["multi_gpu"] = {"world_size": world, "per_rank_render_ms": [round(r[0] * 1e3, 3) for r in per_rank],
                                "per_rank_reduce_ms": [round(r[1] * 1e3, 3) for r in per_rank],
                                "reduce": "torch.distributed.reduce(SUM) of the RGBA32F film, "

@@ -228,6 +228,9 @@ SIGNATURES = [
     ("dcrt_tracer_upload_scene", _I, [_P, C.POINTER(FlatScene)]),
     ("dcrt_tracer_set_frame_params", _I, [_P, C.POINTER(FrameParams)]),
     ("dcrt_tracer_set_film_partition", _I, [_P, C.POINTER(FilmPartition)]),
+    ("dcrt_tracer_set_film_bands", _I, [_P, C.POINTER(C.c_uint32), _U, _U]),
+    ("dcrt_tracer_set_row_cost_probe", _I, [_P, _I]),
+    ("dcrt_tracer_read_row_cost", _I, [_P, C.POINTER(C.c_uint32)]),
     ("dcrt_tracer_render", _I, [_P, _U]),
     ("dcrt_tracer_render_images", _I, [_P, _U, _U, C.POINTER(FilterParams)]),
     ("dcrt_tracer_set_mode", _I, [_P, _I]),

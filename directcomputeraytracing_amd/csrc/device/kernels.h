@@ -324,6 +324,7 @@ struct SampleOut {
     float2* samplePosition;
     float4* sampleValue;
     uint4* debugRng;
+    uint32_t* rowRays;        // probe (dcrt_tracer_set_row_cost_probe): rays cast per film row, or nullptr
 };
 
 // A path's sub-pixel position (NEW_PATH's first two draws, WavefrontPathTracing.hlsl:213-214)

@@ -434,7 +434,8 @@ static_assert(DCRT_MATERIAL_BLOCK % 64 == 0 && DCRT_MATERIAL_BLOCK <= 960, "MATE
 // lights: small scenes, material_lds_bytes within the host's budget); 2: all but the triangles
 // (larger scenes: the hit -> triangle fetch stays global, the triangle -> material one and the
 // light sample's reads become LDS reads); 0: none.
-template <uint32_t CAPS, int SCENE_LDS>
+// PROBE: counts the rays per film row (the row-cost probe); launched only while it is on.
+template <uint32_t CAPS, int SCENE_LDS, bool PROBE = false>
 __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void material_kernel(PathPool pool, DeviceScene sc, const FrameConstants* __restrict__ fcr, Counters* cnt,
                                                                              const Counters* prev, const SampleOut* __restrict__ sampleOut)
 {
@@ -583,6 +584,15 @@ __global__ __launch_bounds__(DCRT_MATERIAL_BLOCK) DCRT_MATERIAL_OCCUPANCY void m
             if (hasShadow) slot(pool.shadowOpacity, out) = shadowOpacity;
         }
         ends = terminate && !hasShadow;
+        // the row-cost probe (PROBE: the variant dcrt_tracer_set_row_cost_probe launches): the rays
+        // of this pass per film row -- the extension ray this item shades and the shadow ray it
+        // casts -- for cost-balanced film bands (partition.balanced_bands)
+        if constexpr (PROBE) {
+            uint32_t* rowRays = sampleOut->rowRays;
+            const uint32_t p = virt ? newPixel : slot(pool.pixel, out);
+            const uint32_t W = fcv.resolution[0], wh = W * fcv.resolution[1];
+            atomicAdd(&rowRays[(p % wh) / W], hasShadow ? 2u : 1u);
+        }
         // (the state written below goes to the queue positions the appends return)
         pathFlags = flags;
         sThr = thr;

@@ -49,12 +49,28 @@ constexpr uint32_t kDefaultIterations = 8;
 // RenderImages' chunks of iterations once its final batch is in flight: a chunk launched after
 // the images completed finds no work, and two chunks are in flight when the host sees it
 constexpr uint32_t kTailChunk = 4;
-constexpr uint32_t kMaxImageBatch = 64;               // images in flight per RenderImages batch (sample textures: 24 B/px each)
+constexpr uint32_t kMaxImageBatch = 256;              // images in flight per RenderImages batch (sample textures: 24 B/px each)
 #ifndef DCRT_MATERIAL_BLOCK
 #define DCRT_MATERIAL_BLOCK 256
 #endif
 constexpr uint32_t kMaterialBlock = DCRT_MATERIAL_BLOCK;   // MATERIAL workgroup (one queue-append atomic each)
 constexpr uint32_t kMaxPersistentBlocks = 256 * 8;   // CUs x resident workgroups
+
+// (A/B knobs of AutoBatch)
+uint32_t kMaxImageBatchAuto()
+{
+    static const uint32_t v = [] {
+        const char* e = std::getenv("DCRT_MAX_BATCH");
+        const int x = e ? std::atoi(e) : (int)kMaxImageBatch;
+        return (uint32_t)std::min<int>(std::max<int>(x, 1), (int)kMaxImageBatch);
+    }();
+    return v;
+}
+bool BatchPoolLimit()
+{
+    static const bool v = [] { const char* e = std::getenv("DCRT_BATCH_POOL_LIMIT"); return !e || std::atoi(e) != 0; }();
+    return v;
+}
 
 template <typename T>
 int DeviceAlloc(T** p, size_t count, std::vector<void*>* owner)
@@ -367,6 +383,7 @@ struct dcrt_tracer {
     uint32_t batchImages = 0;          // RenderImages batch size (0: automatic)
     uint32_t lastSlot = 0;             // sample slot of the last completed image
     dcrt_film_partition partition{ 1, 0, 64, 0 };
+    std::vector<uint32_t> bands;       // explicit film bands [y0, y1) pairs (dcrt_tracer_set_film_bands), or empty
 
     dcrt_frame_params frame{};
     bool hasFrame = false;
@@ -397,6 +414,8 @@ struct dcrt_tracer {
     hipEvent_t stopEvents[4] = {};
     bool instrCounters = false;
     bool extTiming = false;
+    bool rowProbe = false;             // the row-cost probe: MATERIAL's PROBE variant counts rays per film row
+    uint32_t* dRowRays = nullptr;      // [filmH] (rowAllocs: follows the film)
     // timed launches (ext_timing): start / stop event pairs and the kernel each pair timed
     enum TimedKind : uint8_t { kTimedCast = 0, kTimedMaterial = 1, kTimedControl = 2, kTimedKinds = 3 };
     std::vector<hipEvent_t> events;
@@ -435,8 +454,11 @@ struct dcrt_tracer {
     int UploadScene(const dcrt_flat_scene& s);
     int SetFrame(const dcrt_frame_params& p);
     int SetPartition(const dcrt_film_partition& p);
+    int SetBands(const uint32_t* b, uint32_t count, uint32_t halo);
     int EnsureFilm(uint32_t w, uint32_t h);
     int BuildRows();
+    int UploadSampleOut();
+    int SetRowProbe(bool on);
     int EnsureSamples(uint32_t images);
     uint32_t AutoBatch(uint32_t count) const;
     int BeginImage();
@@ -1055,7 +1077,7 @@ int dcrt_tracer::EnsureSamples(uint32_t images)
     HIPCHECK(hipMemsetAsync(film.samplePosition, 0, n * sizeof(float2), stream));
     HIPCHECK(hipMemsetAsync(film.sampleValue, 0, n * sizeof(float4), stream));
     if (film.debugRng) HIPCHECK(hipMemsetAsync(film.debugRng, 0, n * sizeof(uint4), stream));
-    hSampleOut = SampleOut{film.samplePosition, film.sampleValue, film.debugRng};
+    hSampleOut = SampleOut{film.samplePosition, film.sampleValue, film.debugRng, rowProbe ? dRowRays : nullptr};
     HIPCHECK(hipMemcpyAsync(dSampleOut, &hSampleOut, sizeof(SampleOut), hipMemcpyHostToDevice, stream));
     HIPCHECK(hipStreamSynchronize(stream));
     sampleImages = images;
@@ -1072,17 +1094,20 @@ int dcrt_tracer::EnsureSamples(uint32_t images)
 uint32_t dcrt_tracer::AutoBatch(uint32_t count) const
 {
     uint32_t b = batchImages;
+    // (sample index p = image * W*H + y * W + x stays below 2^31)
+    const uint32_t cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kMaxImageBatchAuto(), ((uint64_t)1 << 31) / ((uint64_t)filmW * filmH)));
     if (b == 0) {
         // the slots an image takes: whole 8x8 pixel blocks (a wave each), partial bands and
         // columns included, so a batch that "fits" never waits for slots to free up
         const uint64_t pixels = std::max<uint64_t>(1, (uint64_t)bandCount * kBlockH * ((filmW + kBlockW - 1) / kBlockW) * kBlockW);
-        b = (uint32_t)std::min<uint64_t>(kMaxImageBatch, std::max<uint64_t>(1, poolSize / pixels));
+        b = (uint32_t)std::min<uint64_t>(cap, std::max<uint64_t>(1, poolSize / pixels));
+        if (!BatchPoolLimit()) b = cap;
         // equal batches: as many batches as the cap needs, each as large as the others (a
         // small last batch would pay a whole drain for a sparse wavefront)
         const uint32_t batches = (count + b - 1) / b;
         b = (count + batches - 1) / batches;
     }
-    return std::max<uint32_t>(1, std::min(b, count));
+    return std::max<uint32_t>(1, std::min(std::min(b, cap), count));
 }
 
 // Rows this tracer renders. One tracer: every row. Partitioned film: the
@@ -1096,7 +1121,20 @@ int dcrt_tracer::BuildRows()
     const uint32_t H = filmH;
     std::vector<uint32_t> rows;
     std::vector<uint32_t> owned;
-    if (partition.world_size <= 1) {
+    if (!bands.empty()) {
+        // explicit film bands (dcrt_tracer_set_film_bands): their rows plus the halo beyond each
+        const uint32_t halo = partition.halo_rows ? partition.halo_rows : 2u;
+        owned.assign(H, 0);
+        std::vector<uint8_t> need(H, 0);
+        for (size_t i = 0; i + 1 < bands.size(); i += 2) {
+            const uint32_t y0 = std::min(bands[i], H), y1 = std::min(bands[i + 1], H);
+            for (uint32_t y = y0; y < y1; ++y) owned[y] = 1;
+            if (y0 >= y1) continue;
+            const uint32_t lo = y0 >= halo ? y0 - halo : 0, hi = std::min(H, y1 + halo);
+            for (uint32_t y = lo; y < hi; ++y) need[y] = 1;
+        }
+        for (uint32_t y = 0; y < H; ++y) if (need[y]) rows.push_back(y);
+    } else if (partition.world_size <= 1) {
         for (uint32_t y = 0; y < H; ++y) rows.push_back(y);
     } else {
         const uint32_t N = partition.world_size, halo = partition.halo_rows ? partition.halo_rows : 2u;
@@ -1129,7 +1167,34 @@ int dcrt_tracer::BuildRows()
     film.rowY = dRows;
     film.rowOwned = dOwned;
     film.rowCount = rowCount;
+    dRowRays = nullptr;
+    if (rowProbe) {   // (the probe's counters follow the film's height)
+        CHECKED(DeviceAlloc(&dRowRays, filmH, &rowAllocs));
+        HIPCHECK(hipMemsetAsync(dRowRays, 0, (size_t)filmH * 4, stream));
+        CHECKED(UploadSampleOut());
+    }
     return DCRT_OK;
+}
+
+int dcrt_tracer::UploadSampleOut()
+{
+    hSampleOut.rowRays = rowProbe ? dRowRays : nullptr;
+    HIPCHECK(hipMemcpyAsync(dSampleOut, &hSampleOut, sizeof(SampleOut), hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    return DCRT_OK;
+}
+
+// The row-cost probe: while on, MATERIAL's PROBE variant adds each pass's rays (the extension ray
+// it shades, the shadow ray it casts) to a counter per film row -- the per-row cost that
+// partition.balanced_bands cuts equal-cost film bands from. Turning it on or off re-captures
+// the iteration graphs; on clears the counters.
+int dcrt_tracer::SetRowProbe(bool on)
+{
+    HIPCHECK(hipStreamSynchronize(stream));
+    InvalidateGraph();
+    rowProbe = on;
+    if (on && filmH) return BuildRows();   // (allocates and clears the counters)
+    return UploadSampleOut();
 }
 
 int dcrt_tracer::SetFrame(const dcrt_frame_params& p)
@@ -1155,6 +1220,31 @@ int dcrt_tracer::SetPartition(const dcrt_film_partition& p)
         return DCRT_E_INVALID_ARG;
     }
     partition = p;
+    bands.clear();
+    if (filmW) {
+        HIPCHECK(hipStreamSynchronize(stream));
+        InvalidateGraph();
+        CHECKED(BuildRows());
+    }
+    newImage = true;
+    return DCRT_OK;
+}
+
+// Explicit film bands: this tracer owns rows [b[2i], b[2i+1]) (ascending, disjoint, non-empty),
+// path-traces them plus `halo` rows beyond each band and convolves only its own rows. Any cut
+// of the film into bands dealt to tracers sums to the one-tracer film bit for bit, as the
+// stripes do; cost-balanced cuts come from the row-cost probe (partition.balanced_bands).
+int dcrt_tracer::SetBands(const uint32_t* b, uint32_t count, uint32_t halo)
+{
+    if (count == 0 || !b) { SetLastError("no film bands"); return DCRT_E_INVALID_ARG; }
+    for (uint32_t i = 0; i < count; ++i) {
+        if (b[2 * i] >= b[2 * i + 1] || (i > 0 && b[2 * i] < b[2 * i - 1])) {
+            SetLastError("film bands: ascending, disjoint, non-empty [y0, y1) ranges");
+            return DCRT_E_INVALID_ARG;
+        }
+    }
+    bands.assign(b, b + 2 * count);
+    partition = dcrt_film_partition{1, 0, 64, halo};
     if (filmW) {
         HIPCHECK(hipStreamSynchronize(stream));
         InvalidateGraph();
@@ -1197,7 +1287,7 @@ int dcrt_tracer::BeginImage()
     fc.virtualStart = virtualStart && mergedCasts && !(frame.features & DCRT_FEATURE_ALLOW_ANYHIT) ? 1u : 0u;
     // drain completion (drain_kernel): not with ALLOW_ANYHIT_SHADER, and not while the cast
     // kernels are instrumented (the roofline leg's counts and launch times are the wavefront's)
-    fc.drainPaths = !(frame.features & DCRT_FEATURE_ALLOW_ANYHIT) && !instrCounters && !extTiming ? drainPaths : 0u;
+    fc.drainPaths = !(frame.features & DCRT_FEATURE_ALLOW_ANYHIT) && !instrCounters && !extTiming && !rowProbe ? drainPaths : 0u;
     hipLaunchKernelGGL(set_frame_kernel, dim3(1), dim3(1), 0, stream, dFrame, fc);
     const uint32_t total = fc.blocksPerImage;
     const uint32_t idleThreads = std::max<uint32_t>(poolSize, 2u * (uint32_t)(sizeof(Counters) / 4));
@@ -1243,7 +1333,8 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
         hipExtLaunchKernelGGL(control_kernel, dim3(controlGrid), dim3(kControlBlock), 0, stream, c0, c1, 0, pool, film,
                               (const FrameConstants*)dFrame, cnt, (const Counters*)next, dGlobals, (uint32_t)(film.debugRng != nullptr));
     }
-    auto material = materialCaps == kCapOpaqueDelta
+    auto material = rowProbe ? material_kernel<kCapAll, 0, true>
+                  : materialCaps == kCapOpaqueDelta
                         ? (materialLdsMode == 1 ? material_kernel<kCapOpaqueDelta, 1>
                                                 : materialLdsMode == 2 ? material_kernel<kCapOpaqueDelta, 2> : material_kernel<kCapOpaqueDelta, 0>)
                         : (materialLdsMode == 1 ? material_kernel<kCapAll, 1>
@@ -1251,7 +1342,7 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     if (timed) CHECKED(TimedPair(kTimedMaterial, &m0, &m1));
     {
         Annotation a("Material", !capturing);
-        hipExtLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), materialLds, stream, m0, m1, 0, pool, scene,
+        hipExtLaunchKernelGGL(material, dim3(materialGrid), dim3(kMaterialBlock), rowProbe ? 0u : materialLds, stream, m0, m1, 0, pool, scene,
                               (const FrameConstants*)dFrame, cnt, (const Counters*)next, (const SampleOut*)dSampleOut);
     }
     if (timed) CHECKED(TimedPair(kTimedCast, &e0, &e1));
@@ -1412,7 +1503,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
     if (count == 0) return DCRT_OK;
-    if (partition.world_size > 1) {
+    if (partition.world_size > 1 || !bands.empty()) {
         // a partitioned film's convolution reads the filter's window rows beyond its stripes
         const uint32_t halo = partition.halo_rows ? partition.halo_rows : 2u;
         if (!(filter.radius >= 0.0f) || FilterSupportRows(filter.radius, filmH) > halo) {
@@ -1561,6 +1652,12 @@ DCRT_API int dcrt_tracer_set_film_partition(dcrt_tracer* t, const dcrt_film_part
     return t->SetPartition(*p);
 }
 
+DCRT_API int dcrt_tracer_set_film_bands(dcrt_tracer* t, const uint32_t* bands, uint32_t band_count, uint32_t halo_rows)
+{
+    TRACER_GUARD(t);
+    return t->SetBands(bands, band_count, halo_rows);
+}
+
 DCRT_API int dcrt_tracer_render(dcrt_tracer* t, uint32_t max_iterations)
 {
     TRACER_GUARD(t);
@@ -1660,6 +1757,23 @@ DCRT_API int dcrt_tracer_sample_device_ptrs(dcrt_tracer* t, void** pos, void** v
     const size_t o = (size_t)t->filmW * t->filmH * t->lastSlot;   // the last image's slot
     *pos = (void*)(t->film.samplePosition + o);
     *val = (void*)(t->film.sampleValue + o);
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_set_row_cost_probe(dcrt_tracer* t, int enable)
+{
+    TRACER_GUARD(t);
+    if (enable && t->mode != 0) { SetLastError("the row-cost probe counts the wavefront's MATERIAL passes"); return DCRT_E_INVALID_ARG; }
+    return t->SetRowProbe(enable != 0);
+}
+
+DCRT_API int dcrt_tracer_read_row_cost(dcrt_tracer* t, uint32_t* out_rows)
+{
+    TRACER_GUARD(t);
+    if (!out_rows) return DCRT_E_INVALID_ARG;
+    if (!t->rowProbe || !t->dRowRays) { SetLastError("the row-cost probe is off"); return DCRT_E_INVALID_ARG; }
+    HIPCHECK(hipMemcpyAsync(out_rows, t->dRowRays, (size_t)t->filmH * 4, hipMemcpyDeviceToHost, t->stream));
+    HIPCHECK(hipStreamSynchronize(t->stream));
     return DCRT_OK;
 }
 
@@ -1875,7 +1989,7 @@ DCRT_API int dcrt_tracer_prepare_images(dcrt_tracer* t, uint32_t image_count)
 DCRT_API int dcrt_tracer_set_image_batch(dcrt_tracer* t, uint32_t images)
 {
     TRACER_GUARD(t);
-    if (images > kMaxImageBatch) { SetLastError("image batch too large (max 64)"); return DCRT_E_INVALID_ARG; }
+    if (images > kMaxImageBatch) { SetLastError("image batch too large (max 256)"); return DCRT_E_INVALID_ARG; }
     t->batchImages = images;
     return DCRT_OK;
 }

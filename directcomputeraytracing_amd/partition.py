@@ -60,7 +60,88 @@ def stream_partition(height: int, world_size: int, rank: int, streams: int, stre
     return v, stream * world_size + rank, max(1, round(height / (v * k)))
 
 
-def pipeline_pool(pool: int, rows: int, width: int, images: int, max_batch: int = 64, slack: float = 0.08) -> int:
+def band_render_rows(height: int, bands, halo: int = DEFAULT_HALO) -> list:
+    """Rows a tracer with explicit film bands path-traces (dcrt_tracer::BuildRows): its bands'
+    rows plus `halo` rows beyond each, ascending."""
+    need = np.zeros(height, bool)
+    for y0, y1 in bands:
+        y0, y1 = min(y0, height), min(y1, height)
+        if y0 < y1:
+            need[max(0, y0 - halo):min(height, y1 + halo)] = True
+    return [int(y) for y in np.nonzero(need)[0]]
+
+
+def band_owned_rows(height: int, bands) -> np.ndarray:
+    own = np.zeros(height, bool)
+    for y0, y1 in bands:
+        own[min(y0, height):min(y1, height)] = True
+    return own
+
+
+def band_cost(prefix: np.ndarray, y0: int, y1: int, halo: int) -> float:
+    """Cost of path-tracing band [y0, y1) with its halo rows: the rows' summed cost."""
+    h = len(prefix) - 1
+    return float(prefix[min(h, y1 + halo)] - prefix[max(0, y0 - halo)])
+
+
+def balanced_bands(row_cost, parts: int, halo: int = DEFAULT_HALO) -> list:
+    """Cut the film's rows into `parts` contiguous bands [y0, y1) whose largest cost -- the
+    summed per-row cost of the band and of the halo rows its tracer also path-traces -- is as
+    small as contiguous cuts allow (balance scene-dependent cost). Row costs come
+    from the tracer's row-cost probe (rays per row, tracer.probe_row_cost). Deterministic: ranks
+    that probe the same scene get the same cuts. Returns `parts` bands covering every row once."""
+    c = np.maximum(np.asarray(row_cost, np.float64), 0.0)
+    H = len(c)
+    parts = max(1, min(int(parts), H))
+    if parts == 1:
+        return [(0, H)]
+    c = c + 1e-9 * max(1.0, c.max())   # (every row costs something: empty rows still take slots)
+    P = np.concatenate([[0.0], np.cumsum(c)])
+
+    def greedy(T):
+        """Bands of cost <= T taken greedily from the top (each at least one row); None if more
+        than `parts` are needed."""
+        cuts, y0 = [], 0
+        while y0 < H:
+            if len(cuts) == parts:
+                return None
+            y1 = y0 + 1
+            lo, hi = y0 + 1, H   # the largest y1 with cost <= T (cost grows with y1)
+            while lo <= hi:
+                mid = (lo + hi) // 2
+                if band_cost(P, y0, mid, halo) <= T:
+                    y1, lo = mid, mid + 1
+                else:
+                    hi = mid - 1
+            cuts.append((y0, y1))
+            y0 = y1
+        return cuts
+
+    lo = max(band_cost(P, y, y + 1, halo) for y in range(H))
+    hi = band_cost(P, 0, H, halo)
+    best = greedy(hi)
+    for _ in range(64):   # bisection on the bottleneck cost
+        mid = 0.5 * (lo + hi)
+        g = greedy(mid)
+        if g is None:
+            lo = mid
+        else:
+            hi, best = mid, g
+        if hi - lo <= 1e-6 * hi:
+            break
+    bands = list(best)
+    # fewer bands than parts: split the costliest band in two (a sub-band costs no more)
+    while len(bands) < parts:
+        i = max((k for k in range(len(bands)) if bands[k][1] - bands[k][0] > 1),
+                key=lambda k: band_cost(P, bands[k][0], bands[k][1], halo))
+        y0, y1 = bands[i]
+        # the split row that balances the two halves
+        m = min(range(y0 + 1, y1), key=lambda y: max(band_cost(P, y0, y, halo), band_cost(P, y, y1, halo)))
+        bands[i:i + 1] = [(y0, m), (m, y1)]
+    return [(int(a), int(b)) for a, b in bands]
+
+
+def pipeline_pool(pool: int, rows: int, width: int, images: int, max_batch: int = 256, slack: float = 0.08) -> int:
     """Path-pool slots for one pipeline rendering `images` images of `rows` x `width` pixels.
 
     dcrt_tracer::AutoBatch cuts a render into equal batches of as many images as the pool

@@ -76,6 +76,22 @@ class WavefrontPathTracer:
         p = _abi.FilmPartition(world_size, rank, stripe_height, halo_rows)
         check(self._lib.dcrt_tracer_set_film_partition(self._h, C.byref(p)), "SetFilmPartition")
 
+    def set_film_bands(self, bands, halo_rows: int = 0) -> None:
+        """Own the rows of the (y0, y1) bands (ascending, disjoint), path-trace them plus halo_rows
+        beyond each and convolve only them (dcrt_tracer_set_film_bands)."""
+        flat = np.asarray([y for b in bands for y in b], np.uint32)
+        check(self._lib.dcrt_tracer_set_film_bands(self._h, flat.ctypes.data_as(C.POINTER(C.c_uint32)), len(bands),
+                                                   int(halo_rows)), "SetFilmBands")
+
+    def set_row_cost_probe(self, enable: bool) -> None:
+        """Count the rays cast per film row from now on (cleared when turned on)."""
+        check(self._lib.dcrt_tracer_set_row_cost_probe(self._h, 1 if enable else 0), "SetRowCostProbe")
+
+    def read_row_cost(self) -> np.ndarray:
+        out = np.empty(self.height, np.uint32)
+        check(self._lib.dcrt_tracer_read_row_cost(self._h, out.ctypes.data_as(C.POINTER(C.c_uint32))), "ReadRowCost")
+        return out
+
     def render(self, max_iterations: int = 0) -> None:
         check(self._lib.dcrt_tracer_render(self._h, int(max_iterations)), "Render")
 
@@ -250,28 +266,36 @@ def device_count() -> int:
 
 def make_pipelines(scene, pool: int, streams: int = 2, images: int = 1, iterations: int = 16, world: int = 1,
                    rank: int = 0, stripe: int = 64, mode: str = "wavefront", image_batch: int = 0, device: int = 0,
-                   debug_rng: bool = False) -> list:
-    """The concurrent wavefront pipelines bench.py renders with (one GPU: `streams` horizontal
-    bands; N GPUs: this rank's stripes dealt to its pipelines, partition.stream_partition), each
-    a tracer with its share of `pool` slots (grown to whole batches of `images` images,
-    partition.pipeline_pool), the filter's halo rows, its own stream. Their films have disjoint
-    supports: add_film_device sums them into the rank's film bit for bit."""
-    from .partition import halo_for_radius, pipeline_pool, render_rows, stream_partition
+                   debug_rng: bool = False, row_cost=None, fixed_pool: bool = False) -> list:
+    """The concurrent wavefront pipelines bench.py renders with, each a tracer with its share of
+    `pool` slots (grown to whole batches of `images` images, partition.pipeline_pool), the
+    filter's halo rows, its own stream. With `row_cost` (rays per film row, probe_row_cost) the
+    film is cut into world x streams contiguous equal-cost bands (partition.balanced_bands) and
+    pipeline s of rank r takes band r * streams + s; without it, one GPU splits the film into
+    `streams` equal horizontal bands and N GPUs deal this rank's round-robin stripes to its
+    pipelines (partition.stream_partition). Their films have disjoint supports: add_film_device
+    sums them into the rank's film bit for bit."""
+    from .partition import balanced_bands, band_render_rows, halo_for_radius, pipeline_pool, render_rows, stream_partition
     W, H = scene.resolution
     halo = max(1, halo_for_radius(scene.filter_params().radius, H))
     K = max(1, streams)
+    bands = balanced_bands(row_cost, world * K, halo) if row_cost is not None and world * K > 1 else None
     tracers = []
     try:
         for s_ in range(K):
-            part = stream_partition(H, world, rank, K, s_, stripe) if (K > 1 or world > 1) else None
-            rows = len(render_rows(H, *part, halo)) if part is not None else H
-            p = pipeline_pool(pool // K, rows, W, images) if not image_batch else pool // K
+            part = stream_partition(H, world, rank, K, s_, stripe) if (K > 1 or world > 1) and bands is None else None
+            band = [bands[rank * K + s_]] if bands is not None else None
+            rows = (len(band_render_rows(H, band, halo)) if band is not None
+                    else len(render_rows(H, *part, halo)) if part is not None else H)
+            p = pipeline_pool(pool // K, rows, W, images) if not (image_batch or fixed_pool) else pool // K
             t = WavefrontPathTracer(path_pool_size=p, iterations_per_render=iterations, device=device, debug_rng=debug_rng)
             tracers.append(t)
             t.on_scene_loaded(scene)
             t.set_mode(mode)
             t.set_image_batch(image_batch)
-            if part is not None:
+            if band is not None:
+                t.set_film_bands(band, halo)
+            elif part is not None:
                 t.set_film_partition(*part, halo)
     except BaseException:
         for t in tracers:
@@ -305,3 +329,19 @@ def render_images_concurrently(tracers, first_seed: int, count: int, filter_para
         raise errors[0]
     for t in tracers:
         t.synchronize()
+
+
+def probe_row_cost(scene, first_seed: int = 1 << 20, images: int = 1, pool: int = 1 << 22, device: int = 0) -> np.ndarray:
+    """Rays cast per film row over `images` images (seeds first_seed ..) of the whole film, from
+    the tracer's row-cost probe: exact and schedule-independent, so every rank that probes the
+    same scene gets the same vector and cuts the same balanced bands without communicating.
+    (The default seeds lie outside any render's: the probe's image is not one of the film's.)"""
+    t = WavefrontPathTracer(path_pool_size=pool, iterations_per_render=16, device=device)
+    try:
+        t.on_scene_loaded(scene)
+        t.set_row_cost_probe(True)
+        t.clear_film()
+        t.render_images(first_seed, images)
+        return t.read_row_cost().astype(np.int64)
+    finally:
+        t.destroy()

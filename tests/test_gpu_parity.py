@@ -362,6 +362,90 @@ def test_film_partition_sums_to_single_gpu(native_lib, golden_luts):
     assert same_bits(total, films[0]).all()
 
 
+def test_row_cost_probe_matches_oracle(native_lib, golden_luts, oracle_mod):
+    """The row-cost probe (MATERIAL's PROBE variant): rays cast per film row over two images --
+    every extension ray the wavefront shades plus every shadow ray it casts -- equal the oracle's
+    per-row counts exactly; on a tracer with film bands, the rows it path-traces (bands + halo)
+    carry their counts and the other rows none. Turning it off restores the shipped kernels."""
+    from directcomputeraytracing_amd import WavefrontPathTracer
+    W, H = 160, 96
+    s = cornell(W, H, 4)
+    flat = oracle_mod.flat_with_own_bvh(s)
+    ref = np.zeros(H, np.int64)
+    for seed in (3, 4):
+        fr = oracle_mod.frame_params(s, seed)
+        for y in range(H):
+            _, _, _, c = oracle_mod.render(flat, golden_luts, fr, oracle_mod.WAVEFRONT, rect=(0, y, W, 1))
+            ref[y] += c["extension_rays"] + c["shadow_rays"]
+    t = WavefrontPathTracer(path_pool_size=1 << 14)
+    try:
+        t.set_luts(golden_luts)
+        t.on_scene_loaded(s)
+        t.set_row_cost_probe(True)
+        t.clear_film()
+        t.render_images(3, 2)
+        rows = t.read_row_cost()
+        c = t.counters()
+        assert np.array_equal(rows.astype(np.int64), ref)
+        assert rows.sum() == c["extension_rays"] + c["shadow_rays"]
+        t.set_film_bands([(10, 37), (60, 61)], 2)     # the counters restart with the new rows
+        t.clear_film()
+        t.render_images(3, 2)
+        banded = t.read_row_cost().astype(np.int64)
+        traced = np.zeros(H, bool)
+        traced[8:39] = traced[58:63] = True
+        assert np.array_equal(banded[traced], ref[traced]) and not banded[~traced].any()
+        t.set_row_cost_probe(False)
+        t.set_film_partition(1, 0, 64)
+        t.clear_film()
+        t.render_images(3, 2)
+        with pytest.raises(Exception, match="probe is off"):
+            t.read_row_cost()
+    finally:
+        t.destroy()
+
+
+def test_balanced_bands_pipelines_sum_to_oracle_film(native_lib, golden_luts, oracle_mod):
+    """bench.py's default construction with cost-balanced bands (make_pipelines(row_cost=
+    probe_row_cost(scene))): three pipelines on one GPU, and a world of four ranks with two
+    pipelines each -- every rank's pipeline films summed, then the ranks summed -- give the
+    oracle's film bit for bit. The bands are uneven (equal cost, not equal height)."""
+    from directcomputeraytracing_amd import make_pipelines, probe_row_cost
+    from directcomputeraytracing_amd.partition import balanced_bands, halo_for_radius
+    W, H = 160, 96
+    s = cornell(W, H, 4)
+    filt = s.filter_params()
+    cost = probe_row_cost(s)
+    assert cost.sum() > W * H
+    heights = {b[1] - b[0] for b in balanced_bands(cost, 8, max(1, halo_for_radius(filt.radius, H)))}
+    assert len(heights) > 1
+    flat = oracle_mod.flat_with_own_bvh(s)
+    ref = np.zeros((H, W, 4), np.float32)
+    for seed in range(2):
+        p, v, _, _ = oracle_mod.render(flat, golden_luts, oracle_mod.frame_params(s, seed), oracle_mod.WAVEFRONT)
+        oracle_mod.sample_convolution(filt, p, v, ref)
+    for world, K in ((1, 3), (4, 2)):
+        total = np.zeros_like(ref)
+        for rank in range(world):
+            ts = make_pipelines(s, 1 << 15, streams=K, images=2, world=world, rank=rank, row_cost=cost)
+            try:
+                for t in ts:
+                    t.set_luts(golden_luts)
+                    t.clear_film()
+                render_images_concurrently_local(ts, 0, 2, filt)
+                for t in ts:
+                    total += t.read_film()
+            finally:
+                for t in ts:
+                    t.destroy()
+        assert same_bits(total, ref).all(), (world, K)
+
+
+def render_images_concurrently_local(ts, first, count, filt):
+    from directcomputeraytracing_amd import render_images_concurrently
+    render_images_concurrently(ts, first, count, filt)
+
+
 def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
     """render_images in batches (images sharing the path pool) == one image at a time:
     same film bits, and read_samples returns the last image's samples."""

@@ -112,7 +112,36 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_dir):
+def test_balanced_bands_cover_and_balance():
+    """partition.balanced_bands: `parts` contiguous bands covering every row once, in order; the
+    costliest band (with its halo rows) within one band-edge row of the best any contiguous cut
+    can do (total / parts lower bound); deterministic; degenerate sizes handled."""
+    from directcomputeraytracing_amd.partition import band_cost, band_owned_rows, band_render_rows, balanced_bands
+    rng = np.random.default_rng(3)
+    for H in (1, 7, 144, 1080, 2160):
+        for parts in (1, 2, 3, 8, 16, 24):
+            for halo in (1, 2):
+                cost = rng.uniform(50, 400, H) * (1 + 3 * (np.arange(H) / max(1, H)) ** 2)
+                bands = balanced_bands(cost, parts, halo)
+                assert bands == balanced_bands(cost, parts, halo)
+                assert len(bands) == min(parts, H) and bands[0][0] == 0 and bands[-1][1] == H
+                assert all(a < b for a, b in bands) and all(bands[i][1] == bands[i + 1][0] for i in range(len(bands) - 1))
+                P = np.concatenate([[0.0], np.cumsum(cost)])
+                worst = max(band_cost(P, a, b, halo) for a, b in bands)
+                bound = max(P[-1] / len(bands), max(band_cost(P, y, y + 1, halo) for y in range(H)))
+                assert worst <= bound + (2 * halo + 1) * cost.max() + 1e-6
+                own = sum(band_owned_rows(H, [b]).astype(int) for b in bands)
+                assert (own == 1).all()
+                for b in bands:
+                    rows = band_render_rows(H, [b], halo)
+                    assert rows[0] == max(0, b[0] - halo) and rows[-1] == min(H, b[1] + halo) - 1
+    # a skewed cost moves the cuts: equal-cost bands are not equal-height bands
+    cost = np.r_[np.full(500, 1.0), np.full(580, 10.0)]
+    b = balanced_bands(cost, 2, 1)
+    assert b[0][1] > 700
+
+
+def _worker(rank, world, port, out_dir, mode="stripes"):
     import sys
     sys.path.insert(0, str(ROOT))
     import torch
@@ -121,8 +150,19 @@ def _worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import oracle
     from directcomputeraytracing_amd import FILTER_BOX, FilterParams, Scene, scenes
-    from directcomputeraytracing_amd.partition import owned_row_ranges, render_rows, row_runs
+    from directcomputeraytracing_amd.partition import (balanced_bands, band_owned_rows, band_render_rows, owned_row_ranges,
+                                                       render_rows, row_runs)
     W, H, S = 96, 80, 16
+    if mode == "bands":
+        # uneven contiguous bands, as the row-cost probe cuts them (a synthetic skewed cost here):
+        # two per rank, like two pipelines of one GPU
+        cost = 1.0 + (np.arange(H) / H) ** 3 * 20.0
+        mine = balanced_bands(cost, 2 * world, 1)[2 * rank:2 * rank + 2]
+        rendered = band_render_rows(H, mine, 1)
+        owned = row_runs(np.nonzero(band_owned_rows(H, mine))[0])
+    else:
+        rendered = render_rows(H, world, rank, S, 1)
+        owned = owned_row_ranges(H, world, rank, S)
     s = Scene((W, H))
     scenes.setup_cornell(s, W, H, 3)
     luts = oracle.luts_from_arrays(dict(np.load(GOLDEN / "bxdf_luts.npz")))
@@ -132,10 +172,10 @@ def _worker(rank, world, port, out_dir):
         fr = s.frame_params(seed)
         pos = np.zeros((H, W, 2), np.float32)
         val = np.zeros((H, W, 4), np.float32)
-        for (y0, y1) in row_runs(render_rows(H, world, rank, S, 1)):
+        for (y0, y1) in row_runs(rendered):
             p, v, _, _ = oracle.render(s.flat(), luts, fr, oracle.WAVEFRONT, rect=(0, y0, W, y1 - y0), threads=1)
             pos[y0:y1], val[y0:y1] = p[y0:y1], v[y0:y1]
-        for (r0, r1) in owned_row_ranges(H, world, rank, S):
+        for (r0, r1) in owned:
             oracle.sample_convolution(filt, pos, val, film, rows=(r0, r1))
     t = torch.from_numpy(film)
     dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
@@ -144,10 +184,13 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_gloo_two_rank_film_reduce_is_bit_exact(tmp_path, oracle_mod, golden_luts):
+@pytest.mark.parametrize("mode", ["stripes", "bands"])
+def test_gloo_two_rank_film_reduce_is_bit_exact(tmp_path, oracle_mod, golden_luts, mode):
+    """Round-robin stripes, and uneven cost-balanced bands (partition.balanced_bands, two per rank):
+    the reduce(SUM) of the ranks' films is the one-rank film bit for bit."""
     import torch.multiprocessing as mp
     from directcomputeraytracing_amd import FILTER_BOX, FilterParams, Scene, scenes
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), mode), nprocs=2, join=True)
     reduced = np.load(tmp_path / "film_reduced.npy")
     W, H = 96, 80
     s = Scene((W, H))

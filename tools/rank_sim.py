@@ -28,12 +28,15 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines per rank (bench.py --streams)")
     ap.add_argument("--rank0-only", action="store_true", help="time rank 0's share only (sweeps)")
     ap.add_argument("--fixed-pool", action="store_true", help="pool // streams per pipeline (no pipeline_pool sizing)")
+    ap.add_argument("--partition", choices=["balanced", "stripes"], default="balanced",
+                    help="balanced: equal-cost contiguous bands from the row-cost probe (bench.py's default); "
+                         "stripes: round-robin stripes of --stripe rows")
     args = ap.parse_args()
-    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, render_images_concurrently, scenes
-    from directcomputeraytracing_amd.partition import halo_for_radius, pipeline_pool, render_rows, stream_partition
+    from directcomputeraytracing_amd import Scene, make_pipelines, probe_row_cost, render_images_concurrently, scenes
     scene = Scene((1920, 1080))
     scenes.setup_cornell(scene, 1920, 1080, 8)
     filt = scene.filter_params()
+    row_cost = probe_row_cost(scene) if args.partition == "balanced" else None
     base = None
     for n in [int(x) for x in args.gpus.split(",")]:
         times, rays, iters = [], [], []
@@ -42,19 +45,11 @@ def main():
             K = max(1, args.streams)
             ts = []
             try:
-                for s_ in range(K):
-                    part = stream_partition(1080, n, r, K, s_, args.stripe) if (n > 1 or K > 1) else None
-                    halo = max(1, halo_for_radius(filt.radius))
-                    rows = len(render_rows(1080, *part, halo)) if part is not None else 1080
-                    pool = args.pool // K
-                    if not args.image_batch and not args.fixed_pool:   # as bench.py sizes it
-                        pool = pipeline_pool(pool, rows, 1920, args.steps * n)
-                    t = WavefrontPathTracer(path_pool_size=pool, iterations_per_render=16)
-                    ts.append(t)
-                    t.on_scene_loaded(scene)
-                    t.set_image_batch(args.image_batch)
-                    if part is not None:
-                        t.set_film_partition(*part, halo)
+                # (bench.py's own construction; --fixed-pool: image batches of the whole pool share)
+                ts = make_pipelines(scene, args.pool, streams=K, images=args.steps * n, iterations=16, world=n, rank=r,
+                                    stripe=args.stripe, image_batch=args.image_batch, row_cost=row_cost,
+                                    fixed_pool=args.fixed_pool)
+                for t in ts:
                     t.clear_film()
 
                 def run(first, count):
@@ -76,7 +71,7 @@ def main():
         mx, mean = max(times), sum(times) / len(times)
         base = base or mx
         print(json.dumps({"n_gpus": n, "ms_per_step_max_rank": round(mx, 3), "ms_per_step_mean_rank": round(mean, 3),
-                          "weak_efficiency": round(base / mx, 3), "image_batch": args.image_batch, "pool": args.pool, "fixed_pool": args.fixed_pool, "streams": args.streams,
+                          "weak_efficiency": round(base / mx, 3), "partition": args.partition, "image_batch": args.image_batch, "pool": args.pool, "fixed_pool": args.fixed_pool, "streams": args.streams,
                           "mrays_per_step_mean_rank": round(sum(rays) / len(rays) / 1e6, 3),
                           "ns_per_ray_mean_rank": round(mean * 1e6 / (sum(rays) / len(rays)), 4),
                           "iterations_per_step_mean_rank": round(sum(iters) / len(iters), 2),
