@@ -66,8 +66,8 @@ def parse():
                          "row-cost probe (rays per film row of one probe image, identical on every rank); stripes = "
                          "equal-height round-robin stripes of --stripe rows")
     ap.add_argument("--streams", type=int, default=0,
-                    help="concurrent wavefront pipelines per GPU (film partitions on their own streams); 0: 3 for the "
-                         "one-GPU Cornell headline, 2 otherwise (profiles/r05_ab_pool.txt)")
+                    help="concurrent wavefront pipelines per GPU (film partitions on their own streams); 0: 3 for "
+                         "Cornell at every N, 2 otherwise (profiles/r05_ab_pool.txt, profiles/r06_rank_sim_partition.txt)")
     ap.add_argument("--image-batch", type=int, default=0, help="images per wavefront batch (0 = automatic)")
     ap.add_argument("--roofline-images", type=int, default=0,
                     help="images of the roofline leg (0 = the timed images, so its launches are the timed region's)")
@@ -247,12 +247,13 @@ def main():
         desc = scenes.setup_config(scene, args.config, args.scene_dir, multiscattering=not args.no_multiscattering)
         args.width, args.height = scene.resolution
         workload = f"{desc}, {{spp}} spp ({world} spp/step, film stripes across {world} GPU(s)), wavefront"
-    # pipelines per GPU: three on the one-GPU Cornell headline (its LDS-resident, VALU-bound cast and
-    # memory-bound MATERIAL overlap best three ways: -1 to -3 %), two elsewhere (coffee +2-3 % with
-    # three; a rank of N > 1 renders thin stripes, where a third pipeline adds halo rows)
+    # pipelines per GPU: three for Cornell at every N (its LDS-resident, VALU-bound cast and
+    # memory-bound MATERIAL overlap best three ways: -1 to -3 % at N = 1; with cost-balanced bands
+    # three match two at N = 8, profiles/r06_rank_sim_partition.txt), two elsewhere (coffee +2-3 %
+    # with three)
     args.streams_explicit = args.streams > 0   # (the configs[3] leg follows an explicit --streams)
     if args.streams <= 0:
-        args.streams = 3 if (args.config == "cornell" and world == 1) else 2
+        args.streams = 3 if args.config == "cornell" else 2
     args.pool = args.pool or scenes.default_pool(args.width, args.height, args.streams)
     # (the coffee scene without configs[2]'s multiscattering is its own workload)
     config_name = args.config + ("_noms" if args.config == "coffee" and args.no_multiscattering else "")
@@ -272,8 +273,9 @@ def main():
         return t
 
     # cost-balanced film bands: the rays per film row of one probe image, the same
-    # on every rank (exact, schedule-independent), cut into world x K contiguous equal-cost bands;
-    # pipeline s of rank r takes band r * K + s. Not timed (it precedes the warm-up).
+    # on every rank (exact, schedule-independent), cut into world x K contiguous equal-cost bands
+    # dealt round-robin: pipeline s of rank r takes band s * world + r (make_pipelines), so a cost
+    # trend down the image (time per ray is not uniform) evens out over the ranks. Not timed.
     K = max(1, args.streams)
     row_cost = None
     rank_bands = None
@@ -281,7 +283,7 @@ def main():
         from directcomputeraytracing_amd import probe_row_cost
         from directcomputeraytracing_amd.partition import balanced_bands
         row_cost = probe_row_cost(scene, device=device)
-        rank_bands = balanced_bands(row_cost, world * K, halo)[rank * K:(rank + 1) * K]
+        rank_bands = balanced_bands(row_cost, world * K, halo)[rank::world]
 
     # K concurrent pipelines per GPU (--streams): tracer s renders the rank's stripes dealt
     # to it (partition.stream_partition), on its own stream, from its own host thread; the

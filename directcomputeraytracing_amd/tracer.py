@@ -271,7 +271,8 @@ def make_pipelines(scene, pool: int, streams: int = 2, images: int = 1, iteratio
     `pool` slots (grown to whole batches of `images` images, partition.pipeline_pool), the
     filter's halo rows, its own stream. With `row_cost` (rays per film row, probe_row_cost) the
     film is cut into world x streams contiguous equal-cost bands (partition.balanced_bands) and
-    pipeline s of rank r takes band r * streams + s; without it, one GPU splits the film into
+    pipeline s of rank r takes band s * world + r -- dealt round-robin, so every rank holds one
+    band of each 1/streams of the film and a cost trend down the image evens out; without it, one GPU splits the film into
     `streams` equal horizontal bands and N GPUs deal this rank's round-robin stripes to its
     pipelines (partition.stream_partition). Their films have disjoint supports: add_film_device
     sums them into the rank's film bit for bit."""
@@ -284,7 +285,7 @@ def make_pipelines(scene, pool: int, streams: int = 2, images: int = 1, iteratio
     try:
         for s_ in range(K):
             part = stream_partition(H, world, rank, K, s_, stripe) if (K > 1 or world > 1) and bands is None else None
-            band = [bands[rank * K + s_]] if bands is not None else None
+            band = [bands[s_ * world + rank]] if bands is not None else None
             rows = (len(band_render_rows(H, band, halo)) if band is not None
                     else len(render_rows(H, *part, halo)) if part is not None else H)
             p = pipeline_pool(pool // K, rows, W, images) if not (image_batch or fixed_pool) else pool // K

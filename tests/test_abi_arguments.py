@@ -108,7 +108,8 @@ def test_tracer_calls_with_null_outputs_are_refused():
     assert len(rcs) >= 30
     ok_with_nulls = {"dcrt_tracer_render", "dcrt_tracer_reset_image", "dcrt_tracer_set_mode", "dcrt_tracer_set_image_batch",
                      "dcrt_tracer_set_instrumentation", "dcrt_tracer_reset_stats", "dcrt_tracer_synchronize",
-                     "dcrt_tracer_prepare_images", "dcrt_tracer_clear_film"}
+                     "dcrt_tracer_prepare_images", "dcrt_tracer_clear_film",
+                     "dcrt_tracer_set_row_cost_probe"}   # (an int switch: no pointer to refuse)
     bad = {n: rc for n, rc in rcs.items() if n not in ok_with_nulls and rc not in (-1, -3)}
     assert not bad, bad
     # without a scene: rendering reports NO_SCENE

@@ -1142,7 +1142,7 @@ def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle
     lamp 4K (configs[4], thin lens, triangle lights). Images 0..N-1 rendered concurrently, the two
     films summed on the device. The combined film must equal the oracle's film of the same images
     bit for bit, and the ray counts the oracle's (plus the halo rows both pipelines trace)."""
-    from directcomputeraytracing_amd import Scene, make_pipelines, render_images_concurrently, scenes
+    from directcomputeraytracing_amd import Scene, make_pipelines, probe_row_cost, render_images_concurrently, scenes
     s = Scene((1920, 1080))
     if config == "cornell":
         scenes.setup_cornell(s, 1920, 1080, 8)
@@ -1153,8 +1153,10 @@ def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle
     W, H = s.resolution
     assert (W, H) == ((3840, 2160) if config in ("spaceship", "spaceship_close", "lamp") else (1920, 1080))
     filt = s.filter_params()
-    K = 3 if config == "cornell" else 2   # (bench.py's default pipelines per GPU at world size 1)
-    ts = make_pipelines(s, scenes.default_pool(W, H, K), streams=K, images=images, iterations=16)
+    K = 3 if config == "cornell" else 2   # (bench.py's default pipelines per GPU)
+    # bench.py's default film tiling: cost-balanced bands from the row-cost probe
+    cost = probe_row_cost(s)
+    ts = make_pipelines(s, scenes.default_pool(W, H, K), streams=K, images=images, iterations=16, row_cost=cost)
     try:
         info = ts[0].info()
         if config == "cornell":
@@ -1181,11 +1183,11 @@ def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle
     ext_ref = shadow_ref = 0
     # the rows two pipelines path-trace (each renders the filter's halo rows beyond its band):
     # their rays are traced twice
-    from directcomputeraytracing_amd.partition import halo_for_radius, render_rows, stream_partition
+    from directcomputeraytracing_amd.partition import balanced_bands, band_render_rows, halo_for_radius
     halo = max(1, halo_for_radius(filt.radius, H))
     times = np.zeros(H, np.int64)
-    for k in range(K):
-        times[list(render_rows(H, *stream_partition(H, 1, 0, K, k, 64), halo))] += 1
+    for band in balanced_bands(cost, K, halo):
+        times[band_render_rows(H, [band], halo)] += 1
     assert (times >= 1).all() and times.max() <= 2
     twice = sorted(np.nonzero(times == 2)[0].tolist())
     assert 0 < len(twice) <= 4 * halo * (K - 1)
@@ -1206,19 +1208,20 @@ def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle
 
 def test_rank_share_full_size_bit_exact(native_lib, golden_luts, oracle_mod):
     """One rank's share of the N = 8 Cornell bench exactly as bench.py builds it on that rank
-    (make_pipelines: world 8, rank 3, the 256-row stripe target, two pipelines per rank of N > 1),
-    image 0 at 1920x1080 / 8 bounces: the rank's film equals the oracle's film on the rows the rank
-    owns and is zero elsewhere, and its ray counts are the oracle's over the rows its pipelines
-    path-trace (owned rows plus the filter's halo)."""
-    from directcomputeraytracing_amd import Scene, make_pipelines, render_images_concurrently, scenes
-    from directcomputeraytracing_amd.partition import halo_for_radius, owned_rows, render_rows, row_runs, stream_partition
-    W, H, world, rank, K, stripe = 1920, 1080, 8, 3, 2, 256
+    (make_pipelines: world 8, rank 3, three pipelines, the cost-balanced bands cut from the
+    row-cost probe and dealt round-robin), image 0 at 1920x1080 / 8 bounces: the rank's film
+    equals the oracle's film on the rows the rank owns and is zero elsewhere, and its ray counts
+    are the oracle's over the rows its pipelines path-trace (owned rows plus the filter's halo)."""
+    from directcomputeraytracing_amd import Scene, make_pipelines, probe_row_cost, render_images_concurrently, scenes
+    from directcomputeraytracing_amd.partition import balanced_bands, band_owned_rows, band_render_rows, halo_for_radius, row_runs
+    W, H, world, rank, K = 1920, 1080, 8, 3, 3
     s = Scene((W, H))
     scenes.setup_cornell(s, W, H, 8)
     filt = s.filter_params()
     halo = max(1, halo_for_radius(filt.radius, H))
+    cost = probe_row_cost(s)
     ts = make_pipelines(s, scenes.default_pool(W, H, K), streams=K, images=1, iterations=16, world=world, rank=rank,
-                        stripe=stripe)
+                        row_cost=cost)
     try:
         for t in ts:
             t.clear_film()
@@ -1233,18 +1236,17 @@ def test_rank_share_full_size_bit_exact(native_lib, golden_luts, oracle_mod):
     finally:
         for t in ts:
             t.destroy()
-    parts = [stream_partition(H, world, rank, K, k, stripe) for k in range(K)]
-    owned = np.zeros(H, bool)
-    for part in parts:
-        owned |= owned_rows(H, *part)
+    mine = balanced_bands(cost, world * K, halo)[rank::world]
+    assert len(mine) == K
+    owned = band_owned_rows(H, mine)
     assert 0 < owned.sum() < H // 4
     flat = oracle_mod.flat_with_own_bvh(s)
     fr = oracle_mod.frame_params(s, 0)
     pos = np.zeros((H, W, 2), np.float32)
     val = np.zeros((H, W, 4), np.float32)
     ext_ref = shadow_ref = 0
-    for part in parts:
-        for y0, y1 in row_runs(render_rows(H, *part, halo)):
+    for band in mine:
+        for y0, y1 in row_runs(band_render_rows(H, [band], halo)):
             p, v, _, c = oracle_mod.render(flat, golden_luts, fr, oracle_mod.WAVEFRONT, rect=(0, y0, W, y1 - y0))
             pos[y0:y1], val[y0:y1] = p[y0:y1], v[y0:y1]
             ext_ref += c["extension_rays"]

@@ -157,7 +157,7 @@ def _worker(rank, world, port, out_dir, mode="stripes"):
         # uneven contiguous bands, as the row-cost probe cuts them (a synthetic skewed cost here):
         # two per rank, like two pipelines of one GPU
         cost = 1.0 + (np.arange(H) / H) ** 3 * 20.0
-        mine = balanced_bands(cost, 2 * world, 1)[2 * rank:2 * rank + 2]
+        mine = balanced_bands(cost, 2 * world, 1)[rank::world]
         rendered = band_render_rows(H, mine, 1)
         owned = row_runs(np.nonzero(band_owned_rows(H, mine))[0])
     else:
