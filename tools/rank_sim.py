@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--pool", type=int, default=1 << 25)
     ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines per rank (bench.py --streams)")
     ap.add_argument("--rank0-only", action="store_true", help="time rank 0's share only (sweeps)")
+    ap.add_argument("--repeats", type=int, default=3, help="timed repeats per rank; its time is their median")
     ap.add_argument("--fixed-pool", action="store_true", help="pool // streams per pipeline (no pipeline_pool sizing)")
     ap.add_argument("--partition", choices=["balanced", "stripes"], default="balanced",
                     help="balanced: equal-cost contiguous bands from the row-cost probe (bench.py's default); "
@@ -59,9 +60,15 @@ def main():
                 for t in ts:
                     t.prepare_images(args.steps * n)
                     t.reset_stats()
-                t0 = time.perf_counter()
-                run(0, args.steps * n)
-                times.append((time.perf_counter() - t0) * 1e3 / args.steps)
+                reps = []
+                for _ in range(max(1, args.repeats)):   # (bench.py: the median of its repeats)
+                    for t in ts:
+                        t.clear_film()
+                        t.reset_stats()
+                    t0 = time.perf_counter()
+                    run(0, args.steps * n)
+                    reps.append((time.perf_counter() - t0) * 1e3 / args.steps)
+                times.append(sorted(reps)[len(reps) // 2])
                 cs = [t.counters() for t in ts]
                 rays.append(sum(c["extension_rays"] + c["shadow_rays"] for c in cs) / args.steps)
                 iters.append(max(c.get("iterations", 0) for c in cs) / args.steps)
@@ -71,7 +78,7 @@ def main():
         mx, mean = max(times), sum(times) / len(times)
         base = base or mx
         print(json.dumps({"n_gpus": n, "ms_per_step_max_rank": round(mx, 3), "ms_per_step_mean_rank": round(mean, 3),
-                          "weak_efficiency": round(base / mx, 3), "partition": args.partition, "image_batch": args.image_batch, "pool": args.pool, "fixed_pool": args.fixed_pool, "streams": args.streams,
+                          "weak_efficiency": round(base / mx, 3), "repeats": args.repeats, "partition": args.partition, "image_batch": args.image_batch, "pool": args.pool, "fixed_pool": args.fixed_pool, "streams": args.streams,
                           "mrays_per_step_mean_rank": round(sum(rays) / len(rays) / 1e6, 3),
                           "ns_per_ray_mean_rank": round(mean * 1e6 / (sum(rays) / len(rays)), 4),
                           "iterations_per_step_mean_rank": round(sum(iters) / len(iters), 2),
