@@ -233,6 +233,9 @@ SIGNATURES = [
     ("dcrt_tracer_read_row_cost", _I, [_P, C.POINTER(C.c_uint32)]),
     ("dcrt_tracer_render", _I, [_P, _U]),
     ("dcrt_tracer_render_images", _I, [_P, _U, _U, C.POINTER(FilterParams)]),
+    ("dcrt_tracer_render_images_strided", _I, [_P, _U, _U, _U, _I, C.POINTER(FilterParams)]),
+    ("dcrt_tracer_image_sample_ptrs", _I, [_P, _U, C.POINTER(_P), C.POINTER(_P)]),
+    ("dcrt_tracer_accumulate_images", _I, [_P, C.POINTER(_P), C.POINTER(_P), _U, C.POINTER(FilterParams)]),
     ("dcrt_tracer_set_mode", _I, [_P, _I]),
     ("dcrt_tracer_set_image_batch", _I, [_P, C.c_uint32]),
     ("dcrt_tracer_reset_image", _I, [_P]),

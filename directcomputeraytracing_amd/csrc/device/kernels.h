@@ -77,6 +77,7 @@ struct Globals {
     // block outright and the shard cursors are preset past those blocks (staticGrid =
     // CONTROL workgroups, 0 = off); cleared after that iteration.
     uint32_t staticFill, staticGrid;
+    uint32_t skipFilm;        // RenderImages without the film pass: the caller convolves the images (accumulate_images)
     unsigned long long extRays, shadowRays, iterations;
 };
 
@@ -148,7 +149,10 @@ struct FrameConstants {
     uint32_t refillLanes, parkLanes; // persistent traversal thresholds (lanes of a wave64)
     uint32_t virtualStart;           // batch starts use the virtual extension queue (kVirtualWord)
     uint32_t drainPaths;             // drain_kernel completes the live paths once at most this many remain (0: off)
+    uint32_t seedStride;             // image b of a batch has frame seed frameSeed + b * seedStride (interleaved pipelines)
 };
+// The frame seed of image `image` of the current batch (RenderImages: frameSeed is the batch's first)
+DEV uint32_t image_seed(const FrameConstants& fc, uint32_t image) { return fc.frameSeed + __umul24(image, fc.seedStride); }
 
 // SampleAperture + GenerateRay (RayTracingCommon.inc.hlsl:38-86).
 DEV void generate_ray(const FrameConstants& f, float fsx, float fsy, float a0, float a1, float a2, V3* origin, V3* direction)
@@ -338,7 +342,7 @@ DEV float2 pixel_sample(const FrameConstants& fc, uint32_t p)
     const uint32_t W = fc.resolution[0], wh = W * fc.resolution[1];
     const uint32_t image = p / wh, local = p - image * wh;
     const uint32_t py = local / W, px = local - py * W;
-    Rng r = rng_init(px, py, fc.frameSeed + image);
+    Rng r = rng_init(px, py, image_seed(fc, image));
     const float psx = next1(r);
     const float psy = next1(r);
     return make_float2(psx, psy);
@@ -355,7 +359,7 @@ DEV Rng new_path(const FrameConstants& fc, uint32_t p, V3* o, V3* d)
     const uint32_t W = fc.resolution[0], wh = W * fc.resolution[1];
     const uint32_t image = p / wh, local = p - image * wh;
     const uint32_t py = local / W, px = local - py * W;
-    Rng rng = rng_init(px, py, fc.frameSeed + image);
+    Rng rng = rng_init(px, py, image_seed(fc, image));
     const float psx = next1(rng), psy = next1(rng);
     const float a0 = next1(rng), a1 = next1(rng), a2 = next1(rng);
     if (RAY) {

@@ -143,6 +143,7 @@ __global__ void set_idle_kernel(PathPool pool, Counters* counters, Globals* g, u
         g->imageTarget = 1u;
         g->staticFill = 0u;
         g->staticGrid = 0u;
+        g->skipFilm = 0u;
     }
 }
 
@@ -291,8 +292,8 @@ __global__ __launch_bounds__(kControlBlock) void control_kernel(PathPool pool, F
     if (got) {
         uint32_t px = 0, py = 0, image = 0;
         if (block_pixel(*fc, film, block, lane, &px, &py, &image)) {
-            // NEW_PATH :211-237 (image `image` of the batch has frame seed frameSeed + image)
-            rng = rng_init(px, py, fc->frameSeed + image);
+            // NEW_PATH :211-237 (image `image` of the batch has frame seed image_seed(fc, image))
+            rng = rng_init(px, py, image_seed(*fc, image));
             const float psx = next1(rng), psy = next1(rng);
             const float fsx = (psx + (float)px) / (float)fc->resolution[0];
             const float fsy = (psy + (float)py) / (float)fc->resolution[1];
@@ -1205,7 +1206,7 @@ __global__ __launch_bounds__(256) void megakernel(DeviceScene sc, const FrameCon
         const uint32_t block = shard + claimed * kShards;
         uint32_t px = 0, py = 0, image = 0;
         if (!block_pixel(fc, film, block, lane, &px, &py, &image)) continue;
-        Rng rng = rng_init(px, py, fc.frameSeed + image);
+        Rng rng = rng_init(px, py, image_seed(fc, image));
         const float psx = next1(rng), psy = next1(rng);
         const float fsx = (psx + (float)px) / (float)fc.resolution[0];
         const float fsy = (psy + (float)py) / (float)fc.resolution[1];
@@ -1544,9 +1545,12 @@ __device__ __forceinline__ void film_pixel_window(const FilterConsts& c, uint32_
     *ye = (int)floorf(cy + r); *ye = *ye > (int)H - 1 ? (int)H - 1 : *ye;
 }
 
-__global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t images, const Globals* guard)
+// posList / valList (accumulate_images): image b's sample textures sit at posList[b] / valList[b]
+// (W*H each, e.g. other pipelines' slots) instead of at slot b of this film's.
+__global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t images, const Globals* guard,
+                                                   const float2* const* posList, const float4* const* valList)
 {
-    if (guard && !guard->imageComplete) return;
+    if (guard && (!guard->imageComplete || guard->skipFilm)) return;
     // the images of a completed batch, in order: per pixel the same additions as one
     // film pass per image
     const uint32_t count = guard ? guard->batchImages : images;
@@ -1581,8 +1585,8 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
         if (spanX > kFilmSpan || spanY > kFilmSpan) {
             // wide filters: the direct gather from memory
             for (uint32_t b = 0; b < count && mine; ++b) {
-                const float2* sPos = film.samplePosition + (size_t)b * total;
-                const float4* sVal = film.sampleValue + (size_t)b * total;
+                const float2* sPos = posList ? posList[b] : film.samplePosition + (size_t)b * total;
+                const float4* sVal = valList ? valList[b] : film.sampleValue + (size_t)b * total;
                 const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
                 float wsum = 0.0f;
                 V3 sum = mk(0.0f, 0.0f, 0.0f);
@@ -1601,8 +1605,8 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
             // staged span [txs, txe] x [tys, tye]: inside the film by construction
             const int span = spanX, ox = txs, oy = tys;
             for (uint32_t b = 0; b < count; ++b) {
-                const float2* sPos = film.samplePosition + (size_t)b * total;
-                const float4* sVal = film.sampleValue + (size_t)b * total;
+                const float2* sPos = posList ? posList[b] : film.samplePosition + (size_t)b * total;
+                const float4* sVal = valList ? valList[b] : film.sampleValue + (size_t)b * total;
                 __syncthreads();   // the previous image's tile is no longer read
                 for (int i = (int)threadIdx.x; i < spanX * spanY; i += (int)blockDim.x) {
                     const size_t q = (size_t)(oy + i / spanX) * W + (size_t)(ox + i % spanX);
@@ -1649,7 +1653,7 @@ __global__ void advance_image_kernel(FrameConstants* fc, Globals* g)
     g->imageComplete = 0u;
     g->imagesDone += g->batchImages;
     if (g->imagesDone < g->imageTarget) {
-        fc->frameSeed = g->seedBase + g->imagesDone;
+        fc->frameSeed = g->seedBase + g->imagesDone * fc->seedStride;
         g->batchImages = min(g->batchCap, g->imageTarget - g->imagesDone);
         g->totalBlocks = fc->blocksPerImage * g->batchImages;
         begin_batch_claims(g);
@@ -1659,9 +1663,10 @@ __global__ void advance_image_kernel(FrameConstants* fc, Globals* g)
 }
 
 __global__ void begin_images_kernel(Globals* g, const FrameConstants* fc, uint32_t count, uint32_t firstSeed, uint32_t batchCap,
-                                    uint32_t staticGrid)
+                                    uint32_t staticGrid, uint32_t skipFilm)
 {
     if (threadIdx.x != 0) return;
+    g->skipFilm = skipFilm;
     g->imagesDone = 0u;
     g->imageTarget = count;
     g->seedBase = firstSeed;

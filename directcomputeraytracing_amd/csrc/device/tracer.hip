@@ -382,6 +382,11 @@ struct dcrt_tracer {
     uint32_t sampleImages = 0;         // images the sample textures hold (batch capacity)
     uint32_t batchImages = 0;          // RenderImages batch size (0: automatic)
     uint32_t lastSlot = 0;             // sample slot of the last completed image
+    uint32_t seedStride = 1;           // RenderImages: image k has frame seed first + k * seedStride
+    bool keptSlots = false;            // the last RenderImages left image k's samples in slot k (no film pass)
+    uint32_t keptImages = 0;
+    void** dSourceLists = nullptr;     // accumulate_images: device copies of the caller's pointer lists
+    uint32_t sourceCap = 0;
     dcrt_film_partition partition{ 1, 0, 64, 0 };
     std::vector<uint32_t> bands;       // explicit film bands [y0, y1) pairs (dcrt_tracer_set_film_bands), or empty
 
@@ -470,7 +475,9 @@ struct dcrt_tracer {
     int UploadFilter(const dcrt_filter_params& f);
     int ReadCompletion(bool* complete);
     int Render(uint32_t maxIterations);
-    int RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_filter_params& filter);
+    int RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_filter_params& filter, uint32_t stride = 1,
+                     bool convolve = true);
+    int AccumulateImages(const void* const* pos, const void* const* val, uint32_t count, const dcrt_filter_params& filter);
     int Accumulate(const dcrt_filter_params& filter);
     void InvalidateGraph()
     {
@@ -506,6 +513,7 @@ dcrt_tracer::~dcrt_tracer()
     for (hipEvent_t e : events) (void)hipEventDestroy(e);
     for (hipEvent_t e : stopEvents) if (e) (void)hipEventDestroy(e);
     if (hFilter) (void)hipHostFree(hFilter);
+    if (dSourceLists) (void)hipFree(dSourceLists);
     if (hStop) (void)hipHostFree(hStop);
     FreeAll(&poolAllocs);
     FreeAll(&sceneAllocs);
@@ -1270,6 +1278,7 @@ int dcrt_tracer::BeginImage()
     fc.bladeVertexPos[0] = frame.blade_vertex_pos[0]; fc.bladeVertexPos[1] = frame.blade_vertex_pos[1];
     fc.apertureBaseAngle = frame.aperture_base_angle;
     fc.frameSeed = frame.frame_seed;
+    fc.seedStride = seedStride;
     fc.maxBounce = frame.max_bounce_count;
     fc.lightCount = frame.light_count;
     fc.envLightIndex = frame.environment_light_index;
@@ -1373,7 +1382,7 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     }
     if (sequenced) {
         hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
-                           (const Globals*)dGlobals);
+                           (const Globals*)dGlobals, (const float2* const*)nullptr, (const float4* const*)nullptr);
         hipLaunchKernelGGL(advance_image_kernel, dim3(1), dim3(64), 0, stream, dFrame, dGlobals);
     }
     HIPCHECK(hipGetLastError());
@@ -1422,7 +1431,9 @@ int dcrt_tracer::PrepareImages(uint32_t count)
     if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
     if (count == 0 || mode == 1) return DCRT_OK;
-    CHECKED(EnsureSamples(AutoBatch(count)));
+    // (also the slots of a render without the film pass, which keeps every image: slot k = image k)
+    const uint64_t keptCap = std::min<uint64_t>(kMaxImageBatch, ((uint64_t)1 << 31) / ((uint64_t)filmW * filmH));
+    CHECKED(EnsureSamples(std::max<uint32_t>(AutoBatch(count), count <= keptCap ? count : 0u)));
     if (!extTiming) {
         const uint32_t chunk = std::max<uint32_t>(2, iterationsPerRender & ~1u);
         CHECKED(BuildGraph(true, chunk));
@@ -1489,7 +1500,7 @@ int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
     if (!film.accum) { SetLastError("no film"); return DCRT_E_INVALID_ARG; }
     CHECKED(UploadFilter(f));
     hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
-                       (const Globals*)nullptr);
+                       (const Globals*)nullptr, (const float2* const*)nullptr, (const float4* const*)nullptr);
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
 }
@@ -1497,8 +1508,10 @@ int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
 // Images firstSeed .. firstSeed+count-1 back to back: the device detects each
 // image's completion, convolves it into the film and starts the next one, so the
 // host only enqueues graphs and polls a pinned "stopped" word two graphs behind.
-int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_filter_params& filter)
+int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_filter_params& filter, uint32_t stride, bool convolve)
 {
+    seedStride = std::max<uint32_t>(1u, stride);
+    keptSlots = false;
     Annotation an("RenderImages");
     if (!hasScene) { SetLastError("no scene uploaded"); return DCRT_E_NO_SCENE; }
     if (!hasFrame) { SetLastError("no frame parameters"); return DCRT_E_INVALID_ARG; }
@@ -1513,9 +1526,10 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     }
     lastSlot = 0;
     if (mode == 1) {   // MegakernelPathTracer::Render: one persistent launch + SampleConvolution per image
+        if (!convolve) { SetLastError("the megakernel mode convolves every image"); return DCRT_E_INVALID_ARG; }
         CHECKED(UploadFilter(filter));
         for (uint32_t img = 0; img < count; ++img) {
-            frame.frame_seed = firstSeed + img;
+            frame.frame_seed = firstSeed + img * seedStride;
             CHECKED(BeginImage());
             hipEvent_t e0 = nullptr, e1 = nullptr;
             if (extTiming) CHECKED(TimedPair(kTimedCast, &e0, &e1));
@@ -1523,7 +1537,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
             hipExtLaunchKernelGGL(mk, dim3(megaResident), dim3(castBlock), castLdsFull, stream, e0, e1, 0, scene,
                                   (const FrameConstants*)dFrame, film, dGlobals, (uint32_t)(film.debugRng != nullptr));
             hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
-                               (const Globals*)nullptr);
+                               (const Globals*)nullptr, (const float2* const*)nullptr, (const float4* const*)nullptr);
             HIPCHECK(hipGetLastError());
         }
         HIPCHECK(hipStreamSynchronize(stream));
@@ -1532,7 +1546,13 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
         imagesCompleted += count;
         return DCRT_OK;
     }
-    const uint32_t batch = AutoBatch(count);
+    uint32_t batch = AutoBatch(count);
+    if (!convolve) {
+        // every image keeps its samples (slot k = image k) for the caller's film pass: one batch
+        const uint64_t cap = std::min<uint64_t>(kMaxImageBatch, ((uint64_t)1 << 31) / ((uint64_t)filmW * filmH));
+        if (count > cap) { SetLastError("render_images without the film pass: too many images for one batch"); return DCRT_E_LIMIT; }
+        batch = count;
+    }
     CHECKED(EnsureSamples(batch));
     frame.frame_seed = firstSeed;
     CHECKED(UploadFilter(filter));
@@ -1540,7 +1560,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     // static batch-start claims: one per wave of CONTROL's virtual workgroups
     const uint32_t staticGrid = poolSize / kControlBlock;
     hipLaunchKernelGGL(begin_images_kernel, dim3(1), dim3(64), 0, stream, dGlobals, (const FrameConstants*)dFrame, count, firstSeed, batch,
-                       staticGrid);
+                       staticGrid, convolve ? 0u : 1u);
     HIPCHECK(hipGetLastError());
     // a path needs maxBounce + 3 iterations; cap the total so a broken scene cannot spin forever
     const uint64_t maxIterations = ((uint64_t)count + 2) * (frame.max_bounce_count + 8) * (1 + (filmW * (uint64_t)filmH) / poolSize) + 64;
@@ -1593,6 +1613,40 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
     newImage = true;
     imagesCompleted += count;
     lastSlot = (count - 1) % batch;
+    keptSlots = !convolve;
+    keptImages = keptSlots ? count : 0u;
+    return DCRT_OK;
+}
+
+// The film pass over `count` images whose sample textures (W*H each, this film's size) sit at
+// the caller's device pointers -- e.g. the slots of several pipelines that rendered interleaved
+// images (render_images without the film pass): image b of the list is convolved b-th, so the
+// film is the one-pipeline film bit for bit when the list is in image order.
+int dcrt_tracer::AccumulateImages(const void* const* pos, const void* const* val, uint32_t count, const dcrt_filter_params& f)
+{
+    Annotation an("SampleConvolution (image list)");
+    if (!film.accum) { SetLastError("no film"); return DCRT_E_INVALID_ARG; }
+    if (count == 0) return DCRT_OK;
+    if (count > sourceCap) {
+        HIPCHECK(hipStreamSynchronize(stream));
+        if (dSourceLists) (void)hipFree(dSourceLists);
+        dSourceLists = nullptr;
+        sourceCap = 0;
+        HIPCHECK(hipMalloc(&dSourceLists, (size_t)count * 2 * sizeof(void*)));
+        sourceCap = count;
+    }
+    std::vector<const void*> lists((size_t)count * 2);
+    for (uint32_t i = 0; i < count; ++i) {
+        if (!pos[i] || !val[i]) { SetLastError("null sample texture pointer"); return DCRT_E_INVALID_ARG; }
+        lists[i] = pos[i];
+        lists[count + i] = val[i];
+    }
+    CHECKED(UploadFilter(f));   // (synchronises: the list's staging below is reused safely)
+    HIPCHECK(hipMemcpyAsync(dSourceLists, lists.data(), lists.size() * sizeof(void*), hipMemcpyHostToDevice, stream));
+    hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, count,
+                       (const Globals*)nullptr, (const float2* const*)dSourceLists, (const float4* const*)(dSourceLists + count));
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(stream));   // (the host list is released on return)
     return DCRT_OK;
 }
 
@@ -1669,6 +1723,36 @@ DCRT_API int dcrt_tracer_render_images(dcrt_tracer* t, uint32_t first_seed, uint
     TRACER_GUARD(t);
     if (!f) return DCRT_E_INVALID_ARG;
     return t->RenderImages(first_seed, count, *f);
+}
+
+DCRT_API int dcrt_tracer_render_images_strided(dcrt_tracer* t, uint32_t first_seed, uint32_t seed_stride, uint32_t count,
+                                               int convolve, const dcrt_filter_params* f)
+{
+    TRACER_GUARD(t);
+    if (!f || seed_stride == 0) return DCRT_E_INVALID_ARG;
+    return t->RenderImages(first_seed, count, *f, seed_stride, convolve != 0);
+}
+
+DCRT_API int dcrt_tracer_image_sample_ptrs(dcrt_tracer* t, uint32_t image, void** pos, void** val)
+{
+    TRACER_GUARD(t);
+    if (!pos || !val) return DCRT_E_INVALID_ARG;
+    if (!t->keptSlots || image >= t->keptImages) {
+        SetLastError("no such image: its samples are kept only by render_images without the film pass");
+        return DCRT_E_INVALID_ARG;
+    }
+    const size_t o = (size_t)t->filmW * t->filmH * image;
+    *pos = (void*)(t->film.samplePosition + o);
+    *val = (void*)(t->film.sampleValue + o);
+    return DCRT_OK;
+}
+
+DCRT_API int dcrt_tracer_accumulate_images(dcrt_tracer* t, const void* const* d_positions, const void* const* d_values,
+                                           uint32_t image_count, const dcrt_filter_params* f)
+{
+    TRACER_GUARD(t);
+    if (!f || (image_count && (!d_positions || !d_values))) return DCRT_E_INVALID_ARG;
+    return t->AccumulateImages(d_positions, d_values, image_count, *f);
 }
 
 DCRT_API int dcrt_tracer_reset_image(dcrt_tracer* t)

@@ -141,6 +141,25 @@ def balanced_bands(row_cost, parts: int, halo: int = DEFAULT_HALO) -> list:
     return [(int(a), int(b)) for a, b in bands]
 
 
+def refine_row_cost(row_cost, rank_bands, rank_times, halo: int = DEFAULT_HALO) -> np.ndarray:
+    """Row costs corrected by measured time: rank r rendered rank_bands[r] (with halo) in
+    rank_times[r]; every row it owns is rescaled by r's time per unit of modelled cost. The
+    probe's rays are not time (time per ray grows down the Cornell image: more node visits and
+    triangle tests per ray), so one calibration run of the cut bands, gathered from all ranks,
+    re-cuts them at equal time. Deterministic given the gathered times: every rank computes the
+    same vector."""
+    c = np.maximum(np.asarray(row_cost, np.float64), 0.0)
+    P = np.concatenate([[0.0], np.cumsum(c)])
+    out = c.copy()
+    for bands, t in zip(rank_bands, rank_times):
+        modelled = sum(band_cost(P, y0, y1, halo) for y0, y1 in bands)
+        if modelled <= 0 or not t > 0:
+            continue
+        for y0, y1 in bands:
+            out[y0:y1] = c[y0:y1] * (float(t) / modelled)
+    return out * (P[-1] / max(out.sum(), 1e-300))   # (the same total as the input)
+
+
 def pipeline_pool(pool: int, rows: int, width: int, images: int, max_batch: int = 256, slack: float = 0.08) -> int:
     """Path-pool slots for one pipeline rendering `images` images of `rows` x `width` pixels.
 

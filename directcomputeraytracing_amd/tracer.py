@@ -95,9 +95,29 @@ class WavefrontPathTracer:
     def render(self, max_iterations: int = 0) -> None:
         check(self._lib.dcrt_tracer_render(self._h, int(max_iterations)), "Render")
 
-    def render_images(self, first_seed: int, count: int, filter_params: _abi.FilterParams | None = None) -> None:
+    def render_images(self, first_seed: int, count: int, filter_params: _abi.FilterParams | None = None,
+                      seed_stride: int = 1, convolve: bool = True) -> None:
+        """Images first_seed + k * seed_stride, k < count; convolve=False keeps every image's
+        samples (slot k) for accumulate_images instead of running the film pass."""
         f = filter_params or self.filter
-        check(self._lib.dcrt_tracer_render_images(self._h, int(first_seed), int(count), C.byref(f)), "RenderImages")
+        if seed_stride == 1 and convolve:
+            check(self._lib.dcrt_tracer_render_images(self._h, int(first_seed), int(count), C.byref(f)), "RenderImages")
+        else:
+            check(self._lib.dcrt_tracer_render_images_strided(self._h, int(first_seed), int(seed_stride), int(count),
+                                                              1 if convolve else 0, C.byref(f)), "RenderImagesStrided")
+
+    def image_sample_ptrs(self, image: int) -> tuple[int, int]:
+        pos, val = C.c_void_p(), C.c_void_p()
+        check(self._lib.dcrt_tracer_image_sample_ptrs(self._h, int(image), C.byref(pos), C.byref(val)), "ImageSamplePtrs")
+        return pos.value or 0, val.value or 0
+
+    def accumulate_images(self, positions, values, filter_params: _abi.FilterParams | None = None) -> None:
+        """SampleConvolution of the images whose sample textures sit at these device pointers, in order."""
+        f = filter_params or self.filter
+        n = len(positions)
+        P = (C.c_void_p * max(1, n))(*positions)
+        V = (C.c_void_p * max(1, n))(*values)
+        check(self._lib.dcrt_tracer_accumulate_images(self._h, P, V, n, C.byref(f)), "AccumulateImages")
 
     def prepare_images(self, count: int) -> None:
         """Allocate / capture what render_images(count) would on its first call."""
@@ -266,7 +286,8 @@ def device_count() -> int:
 
 def make_pipelines(scene, pool: int, streams: int = 2, images: int = 1, iterations: int = 16, world: int = 1,
                    rank: int = 0, stripe: int = 64, mode: str = "wavefront", image_batch: int = 0, device: int = 0,
-                   debug_rng: bool = False, row_cost=None, fixed_pool: bool = False) -> list:
+                   debug_rng: bool = False, row_cost=None, fixed_pool: bool = False, interleave: bool = False,
+                   bands_per_rank: int = 0) -> list:
     """The concurrent wavefront pipelines bench.py renders with, each a tracer with its share of
     `pool` slots (grown to whole batches of `images` images, partition.pipeline_pool), the
     filter's halo rows, its own stream. With `row_cost` (rays per film row, probe_row_cost) the
@@ -280,6 +301,9 @@ def make_pipelines(scene, pool: int, streams: int = 2, images: int = 1, iteratio
     W, H = scene.resolution
     halo = max(1, halo_for_radius(scene.filter_params().radius, H))
     K = max(1, streams)
+    if interleave:
+        return _make_interleaved(scene, pool, K, images, iterations, world, rank, stripe, mode, image_batch, device, debug_rng,
+                                 row_cost, fixed_pool, bands_per_rank or K, halo)
     bands = balanced_bands(row_cost, world * K, halo) if row_cost is not None and world * K > 1 else None
     tracers = []
     try:
@@ -305,29 +329,94 @@ def make_pipelines(scene, pool: int, streams: int = 2, images: int = 1, iteratio
     return tracers
 
 
-def render_images_concurrently(tracers, first_seed: int, count: int, filter_params=None) -> None:
-    """render_images on several tracers at once (one host thread each; the C ABI runs with
-    the GIL released and every tracer owns its stream), then synchronize them all. An
-    error in any tracer is raised here, after every thread has finished."""
+def _make_interleaved(scene, pool, K, images, iterations, world, rank, stripe, mode, image_batch, device, debug_rng, row_cost,
+                      fixed_pool, bands_per_rank, halo) -> list:
+    """make_pipelines(interleave=True): K tracers over the SAME rows -- the whole film on one GPU,
+    the rank's share of it on N (`bands_per_rank` cost-balanced bands dealt round-robin, or the
+    round-robin stripes without a row cost) -- that split the images instead of the rows
+    (render_images_concurrently deals image j to pipeline j mod K). No halo rows between the
+    pipelines of one GPU, and the pipelines carry statistically equal work."""
+    from .partition import balanced_bands, band_render_rows, pipeline_pool, render_rows
+    W, H = scene.resolution
+    bands = part = None
+    if world > 1:
+        if row_cost is not None:
+            B = max(1, bands_per_rank)
+            bands = balanced_bands(row_cost, world * B, halo)[rank::world]
+        else:
+            part = (world, rank, stripe)
+    rows = (len(band_render_rows(H, bands, halo)) if bands is not None
+            else len(render_rows(H, *part, halo)) if part is not None else H)
+    per = -(-images // K)
+    px = max(1, -(-rows // 8) * 8 * -(-W // 8) * 8)
+    p = pipeline_pool(pool // K, rows, W, per) if not (image_batch or fixed_pool) else pool // K
+    tracers = []
+    try:
+        for _ in range(K):
+            t = WavefrontPathTracer(path_pool_size=p, iterations_per_render=iterations, device=device, debug_rng=debug_rng)
+            tracers.append(t)
+            t.on_scene_loaded(scene)
+            t.set_mode(mode)
+            t.set_image_batch(image_batch)
+            if bands is not None:
+                t.set_film_bands(bands, halo)
+            elif part is not None:
+                t.set_film_partition(*part, halo)
+            t.interleaved = True
+            t.pool_images = max(1, p // px)
+            t.rank_bands = bands
+    except BaseException:
+        for t in tracers:
+            t.destroy()
+        raise
+    return tracers
+
+
+def _run_threads(tracers, fn) -> None:
+    """fn(index, tracer) on every tracer at once (one host thread each; the C ABI runs with the
+    GIL released and every tracer owns its stream). An error in any tracer is raised here,
+    after every thread has finished."""
     import threading
     errors = []
 
-    def run(t):
+    def run(i, t):
         try:
-            t.render_images(first_seed, count, filter_params)
+            fn(i, t)
         except BaseException as e:   # re-raised in the caller's thread
             errors.append(e)
 
     if len(tracers) == 1:
-        run(tracers[0])
+        run(0, tracers[0])
     else:
-        th = [threading.Thread(target=run, args=(t,)) for t in tracers]
+        th = [threading.Thread(target=run, args=(i, t)) for i, t in enumerate(tracers)]
         for x in th:
             x.start()
         for x in th:
             x.join()
     if errors:
         raise errors[0]
+
+
+def render_images_concurrently(tracers, first_seed: int, count: int, filter_params=None) -> None:
+    """render_images on several tracers at once, then synchronize them all. Pipelines built
+    with interleaved images (make_pipelines(interleave=True)) share their rows: tracer s renders
+    images s, s + K, ... of each chunk without the film pass, and tracer 0 then convolves the
+    chunk's images in image order from all K pipelines' sample textures (accumulate_images), so
+    its film is the one-pipeline film bit for bit and the others' stay empty."""
+    K = len(tracers)
+    if K > 1 and getattr(tracers[0], "interleaved", False):
+        # chunks the pipelines' pools hold whole (one batch each, with its virtual start)
+        chunk = K * max(1, min(getattr(t, "pool_images", 1) for t in tracers))
+        for c0 in range(0, count, chunk):
+            n = min(chunk, count - c0)
+            _run_threads(tracers, lambda s, t: t.render_images(first_seed + c0 + s, len(range(s, n, K)), filter_params,
+                                                               seed_stride=K, convolve=False) if s < n else None)
+            for t in tracers:
+                t.synchronize()
+            ptrs = [tracers[j % K].image_sample_ptrs(j // K) for j in range(n)]
+            tracers[0].accumulate_images([p for p, _ in ptrs], [v for _, v in ptrs], filter_params)
+        return
+    _run_threads(tracers, lambda i, t: t.render_images(first_seed, count, filter_params))
     for t in tracers:
         t.synchronize()
 

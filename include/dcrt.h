@@ -486,6 +486,22 @@ DCRT_API int dcrt_tracer_render(dcrt_tracer* tracer, uint32_t max_iterations);
  * image, in order, so the film is the same as with one image at a time. */
 DCRT_API int dcrt_tracer_render_images(dcrt_tracer* tracer, uint32_t first_seed, uint32_t image_count,
                                        const dcrt_filter_params* filter);
+/* render_images generalised for pipelines that share a film's rows by interleaving images:
+ * image k of the call has frame seed first_seed + k * seed_stride; with convolve == 0 the film
+ * pass is skipped and image k's samples stay in slot k (at most 256 images, one batch) for
+ * dcrt_tracer_image_sample_ptrs / dcrt_tracer_accumulate_images. No reference counterpart. */
+DCRT_API int dcrt_tracer_render_images_strided(dcrt_tracer* tracer, uint32_t first_seed, uint32_t seed_stride,
+                                               uint32_t image_count, int convolve, const dcrt_filter_params* filter);
+/* Device pointers of image `image`'s sample textures (W*H R32G32F / RGBA32F) after a
+ * render_images_strided call with convolve == 0. */
+DCRT_API int dcrt_tracer_image_sample_ptrs(dcrt_tracer* tracer, uint32_t image, void** out_position, void** out_value);
+/* SampleConvolution over image_count images whose sample textures sit at the given device
+ * pointers (host arrays of image_count pointers each; every texture W*H of this tracer's film,
+ * on its device), convolved in list order into this tracer's film (its own rows): the film of
+ * several pipelines' interleaved images, bit for bit the one-pipeline film when the list is in
+ * image order. Synchronous. */
+DCRT_API int dcrt_tracer_accumulate_images(dcrt_tracer* tracer, const void* const* d_positions, const void* const* d_values,
+                                           uint32_t image_count, const dcrt_filter_params* filter);
 /* Allocate / capture now what dcrt_tracer_render_images(image_count) would on its first
  * call (the batch's sample textures, the iteration graph), e.g. before a timed region.
  * No reference counterpart (the reference allocates at Create and scene load). */

@@ -441,6 +441,45 @@ def test_balanced_bands_pipelines_sum_to_oracle_film(native_lib, golden_luts, or
         assert same_bits(total, ref).all(), (world, K)
 
 
+@pytest.mark.parametrize("pool", [1 << 16, 1 << 14])
+def test_interleaved_pipelines_match_oracle_film(native_lib, golden_luts, oracle_mod, pool):
+    """Pipelines that split the IMAGES of a GPU's rows instead of the rows (make_pipelines(
+    interleave=True)): pipeline s renders images s, s + K, ... (seed stride K) without the film
+    pass, and pipeline 0 convolves every image in image order from the K pipelines' sample
+    textures (accumulate_images). One GPU with three pipelines, and four ranks of two pipelines
+    on one or two cost-balanced bands each: the film (summed over the ranks) is the oracle's bit
+    for bit, and the other pipelines' films stay empty. The small pool forces chunks of one
+    image per pipeline (several batches, each with its virtual start)."""
+    from directcomputeraytracing_amd import make_pipelines, probe_row_cost, render_images_concurrently
+    W, H, images = 160, 96, 5
+    s = cornell(W, H, 4)
+    filt = s.filter_params()
+    cost = probe_row_cost(s)
+    flat = oracle_mod.flat_with_own_bvh(s)
+    ref = np.zeros((H, W, 4), np.float32)
+    for seed in range(images):
+        p, v, _, _ = oracle_mod.render(flat, golden_luts, oracle_mod.frame_params(s, seed), oracle_mod.WAVEFRONT)
+        oracle_mod.sample_convolution(filt, p, v, ref)
+    for world, K, B in ((1, 3, 0), (4, 2, 1), (4, 2, 2)):
+        total = np.zeros_like(ref)
+        for rank in range(world):
+            ts = make_pipelines(s, pool * K, streams=K, images=images, world=world, rank=rank, row_cost=cost,
+                                interleave=True, bands_per_rank=B)
+            try:
+                for t in ts:
+                    t.set_luts(golden_luts)
+                    t.clear_film()
+                render_images_concurrently(ts, 0, images, filt)
+                total += ts[0].read_film()
+                for t in ts[1:]:
+                    assert not t.read_film().any()
+                assert sum(t.counters()["images_completed"] for t in ts) == images
+            finally:
+                for t in ts:
+                    t.destroy()
+        assert same_bits(total, ref).all(), (world, K, B)
+
+
 def render_images_concurrently_local(ts, first, count, filt):
     from directcomputeraytracing_amd import render_images_concurrently
     render_images_concurrently(ts, first, count, filt)

@@ -28,6 +28,11 @@ def main():
     ap.add_argument("--streams", type=int, default=2, help="concurrent pipelines per rank (bench.py --streams)")
     ap.add_argument("--rank0-only", action="store_true", help="time rank 0's share only (sweeps)")
     ap.add_argument("--repeats", type=int, default=3, help="timed repeats per rank; its time is their median")
+    ap.add_argument("--interleave", action="store_true", help="pipelines split the images of the rank's rows (bench --interleave)")
+    ap.add_argument("--bands-per-rank", type=int, default=0, help="interleaved: balanced bands per rank (0 = --streams)")
+    ap.add_argument("--calibrate", type=int, default=0,
+                    help="steps of a timed calibration run per rank before the timed runs; its rank times re-cut the "
+                         "bands at equal time (partition.refine_row_cost, bench --calibrate)")
     ap.add_argument("--fixed-pool", action="store_true", help="pool // streams per pipeline (no pipeline_pool sizing)")
     ap.add_argument("--partition", choices=["balanced", "stripes"], default="balanced",
                     help="balanced: equal-cost contiguous bands from the row-cost probe (bench.py's default); "
@@ -39,8 +44,33 @@ def main():
     filt = scene.filter_params()
     row_cost = probe_row_cost(scene) if args.partition == "balanced" else None
     base = None
+    from directcomputeraytracing_amd.partition import balanced_bands, halo_for_radius, refine_row_cost
+    halo = max(1, halo_for_radius(filt.radius, 1080))
+
+    def rank_bands(cost, n, K):
+        B = (args.bands_per_rank or K) if args.interleave else K
+        return [balanced_bands(cost, n * B, halo)[r::n] for r in range(n)]
+
     for n in [int(x) for x in args.gpus.split(",")]:
         times, rays, iters = [], [], []
+        cost_n = row_cost
+        if args.calibrate and row_cost is not None and n > 1:
+            # the calibration run: every rank's share of args.calibrate steps, timed once
+            K = max(1, args.streams)
+            calib = []
+            for r in range(n):
+                ts = make_pipelines(scene, args.pool, streams=K, images=args.calibrate * n, iterations=16, world=n, rank=r,
+                                    stripe=args.stripe, image_batch=args.image_batch, row_cost=row_cost,
+                                    fixed_pool=args.fixed_pool, interleave=args.interleave, bands_per_rank=args.bands_per_rank)
+                try:
+                    render_images_concurrently(ts, 20_000, n, filt)
+                    t0 = time.perf_counter()
+                    render_images_concurrently(ts, 30_000, args.calibrate * n, filt)
+                    calib.append(time.perf_counter() - t0)
+                finally:
+                    for t in ts:
+                        t.destroy()
+            cost_n = refine_row_cost(row_cost, rank_bands(row_cost, n, K), calib, halo)
         for r in range(1 if args.rank0_only else n):
             # the rank's K concurrent pipelines, as bench.py --streams K runs them
             K = max(1, args.streams)
@@ -48,8 +78,9 @@ def main():
             try:
                 # (bench.py's own construction; --fixed-pool: image batches of the whole pool share)
                 ts = make_pipelines(scene, args.pool, streams=K, images=args.steps * n, iterations=16, world=n, rank=r,
-                                    stripe=args.stripe, image_batch=args.image_batch, row_cost=row_cost,
-                                    fixed_pool=args.fixed_pool)
+                                    stripe=args.stripe, image_batch=args.image_batch, row_cost=cost_n,
+                                    fixed_pool=args.fixed_pool, interleave=args.interleave,
+                                    bands_per_rank=args.bands_per_rank)
                 for t in ts:
                     t.clear_film()
 
@@ -78,7 +109,7 @@ def main():
         mx, mean = max(times), sum(times) / len(times)
         base = base or mx
         print(json.dumps({"n_gpus": n, "ms_per_step_max_rank": round(mx, 3), "ms_per_step_mean_rank": round(mean, 3),
-                          "weak_efficiency": round(base / mx, 3), "repeats": args.repeats, "partition": args.partition, "image_batch": args.image_batch, "pool": args.pool, "fixed_pool": args.fixed_pool, "streams": args.streams,
+                          "weak_efficiency": round(base / mx, 3), "repeats": args.repeats, "partition": args.partition, "interleave": args.interleave, "bands_per_rank": args.bands_per_rank, "calibrate": args.calibrate, "image_batch": args.image_batch, "pool": args.pool, "fixed_pool": args.fixed_pool, "streams": args.streams,
                           "mrays_per_step_mean_rank": round(sum(rays) / len(rays) / 1e6, 3),
                           "ns_per_ray_mean_rank": round(mean * 1e6 / (sum(rays) / len(rays)), 4),
                           "iterations_per_step_mean_rank": round(sum(iters) / len(iters), 2),
