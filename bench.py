@@ -68,6 +68,15 @@ def parse():
     ap.add_argument("--streams", type=int, default=0,
                     help="concurrent wavefront pipelines per GPU (film partitions on their own streams); 0: 3 for "
                          "Cornell at every N, 2 otherwise (profiles/r05_ab_pool.txt, profiles/r06_rank_sim_partition.txt)")
+    ap.add_argument("--interleave", choices=["auto", "on", "off"], default="auto",
+                    help="on: the GPU's pipelines share the rank's rows and split the images (no halo between them, "
+                         "equal work per pipeline); off: each pipeline its own band; auto: on for N > 1")
+    ap.add_argument("--bands-per-rank", type=int, default=1,
+                    help="interleaved: cost-balanced bands per rank, dealt round-robin over the ranks")
+    ap.add_argument("--calibrate", type=int, default=1,
+                    help="N > 1 balanced: calibration rounds, each an untimed render of the timed workload whose "
+                         "per-rank times re-cut the bands at equal time (partition.refine_row_cost); 0 = the probe's "
+                         "ray counts alone")
     ap.add_argument("--image-batch", type=int, default=0, help="images per wavefront batch (0 = automatic)")
     ap.add_argument("--roofline-images", type=int, default=0,
                     help="images of the roofline leg (0 = the timed images, so its launches are the timed region's)")
@@ -235,7 +244,8 @@ def main():
         torch.cuda.set_device(device)
 
     import numpy as np
-    from directcomputeraytracing_amd import Scene, WavefrontPathTracer, make_pipelines, render_images_concurrently, scenes
+    from directcomputeraytracing_amd import (Scene, WavefrontPathTracer, make_pipelines, prepare_pipelines,
+                                             render_images_concurrently, scenes)
     luts_arrays = dict(np.load(ROOT / "tests" / "golden" / "bxdf_luts.npz"))
 
     scene = Scene((args.width, args.height))
@@ -277,21 +287,27 @@ def main():
     # dealt round-robin: pipeline s of rank r takes band s * world + r (make_pipelines), so a cost
     # trend down the image (time per ray is not uniform) evens out over the ranks. Not timed.
     K = max(1, args.streams)
+    interleave = args.interleave == "on" or (args.interleave == "auto" and world > 1)
+    B = max(1, args.bands_per_rank) if interleave else K      # bands per rank
     row_cost = None
     rank_bands = None
-    if args.partition == "balanced" and world * K > 1 and args.mode == "wavefront":
+    if args.partition == "balanced" and world * B > 1 and args.mode == "wavefront":
         from directcomputeraytracing_amd import probe_row_cost
         from directcomputeraytracing_amd.partition import balanced_bands
         row_cost = probe_row_cost(scene, device=device)
-        rank_bands = balanced_bands(row_cost, world * K, halo)[rank::world]
+        rank_bands = balanced_bands(row_cost, world * B, halo)[rank::world]
 
-    # K concurrent pipelines per GPU (--streams): tracer s renders the rank's stripes dealt
-    # to it (partition.stream_partition), on its own stream, from its own host thread; the
-    # K films have disjoint supports and are summed on the device (add_film_device).
+    # K concurrent pipelines per GPU (--streams), each on its own stream from its own host
+    # thread. N = 1: pipeline s renders cost-balanced band s (disjoint film supports, summed on
+    # the device by add_film_device). N > 1 (interleaved): the K pipelines share the rank's
+    # bands and split the images; pipeline 0 convolves them all in image order.
     # (a pipeline's pool just short of a whole number of batches grows by <= 8 %: one drain less)
-    tracers = make_pipelines(scene, args.pool, streams=K, images=args.steps * world, iterations=args.iterations,
-                             world=world, rank=rank, stripe=args.stripe, mode=args.mode, image_batch=args.image_batch,
-                             device=device, row_cost=row_cost)
+    def build_pipelines(cost):
+        return make_pipelines(scene, args.pool, streams=K, images=args.steps * world, iterations=args.iterations,
+                              world=world, rank=rank, stripe=args.stripe, mode=args.mode, image_batch=args.image_batch,
+                              device=device, row_cost=cost, interleave=interleave, bands_per_rank=B)
+
+    tracers = build_pipelines(row_cost)
     tracer = tracers[0]
 
     def render_all(first, count):
@@ -306,7 +322,10 @@ def main():
             dist.barrier()
 
     def combine_films():
-        # the K pipelines' films into tracer 0's (disjoint supports: bit-exact sum)
+        # the K pipelines' films into tracer 0's (disjoint supports: bit-exact sum); interleaved
+        # pipelines already convolved into tracer 0's film
+        if interleave:
+            return
         for t in tracers[1:]:
             t.synchronize()
             tracer.add_film_device(t.film_device_ptr())
@@ -330,7 +349,7 @@ def main():
         for t in tracers:
             t.synchronize()
         tracers[0].copy_film_device(snap_dev.data_ptr())
-        for t in tracers[1:]:
+        for t in ([] if interleave else tracers[1:]):
             t.copy_film_device(snap_tmp.data_ptr())
             snap_dev.add_(snap_tmp)
             # the next pipeline's copy (on its own stream) overwrites snap_tmp: wait for the add
@@ -355,10 +374,47 @@ def main():
         t.clear_film()
     if args.warmup:
         render_all(10_000, args.warmup)
+
     images = args.steps * world            # weak scaling: each step is one image per GPU-equivalent
-    for t in tracers:
-        t.prepare_images(images)           # sample textures of the timed batches + graph: not timed work
+    prepare_pipelines(tracers, images)     # sample textures of the timed batches + graph: not timed work
     snapshots = bool(args.snapshot_spp and args.snapshot_spp < images)
+
+    calibration = None
+    if dist is not None and row_cost is not None and args.calibrate > 0:
+        # time per ray is not uniform over the film (deeper traversals lower in the Cornell
+        # image), so the probe's ray counts leave the ranks a few % apart. Calibration rounds:
+        # untimed renders of the timed workload (other seeds), the median rank times gathered, the
+        # bands re-cut at equal time (partition.refine_row_cost -- every rank computes the same
+        # cut from the same gathered times) and the pipelines rebuilt and prepared on it
+        import torch
+        from directcomputeraytracing_amd.partition import balanced_bands, refine_row_cost
+        calibration = {"rounds": args.calibrate, "rank_ms_per_step": []}
+        for _ in range(args.calibrate):
+            runs_s = []
+            for rep in range(3):                   # (the median of three: a single run is +-1.5 %)
+                barrier_sync()
+                t0 = time.perf_counter()
+                render_all(20_000 + rep * images, images)
+                for t in tracers:
+                    t.synchronize()
+                runs_s.append(time.perf_counter() - t0)
+            mine = torch.tensor([float(np.median(runs_s))], dtype=torch.float64, device="cuda" if on_device else "cpu")
+            gathered = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(gathered, mine)
+            calib_s = [float(g.item()) for g in gathered]
+            calibration["rank_ms_per_step"].append([round(x * 1e3 / args.steps, 3) for x in calib_s])
+            all_bands = balanced_bands(row_cost, world * B, halo)
+            row_cost = refine_row_cost(row_cost, [all_bands[r::world] for r in range(world)], calib_s, halo)
+            rank_bands = balanced_bands(row_cost, world * B, halo)[rank::world]
+            for t in tracers:
+                t.destroy()
+            tracers = build_pipelines(row_cost)
+            tracer = tracers[0]
+            for t in tracers:
+                t.clear_film()
+            if args.warmup:
+                render_all(10_000, args.warmup)
+            prepare_pipelines(tracers, images)
 
     def timed_run():
         """One timed repeat of exactly K steps: (wall s, this rank's render s, reduce s)."""
@@ -481,8 +537,10 @@ def main():
                    "parallelism": (f"film {'cost-balanced bands' if rank_bands is not None else 'stripes'} x{world}"
                                    if world > 1 else "single GPU")
                                   + (f", {K} concurrent pipelines per GPU" if K > 1 else "")
+                                  + (f" (image-interleaved over the rank's {B} band(s))" if interleave and K > 1 else "")
                                   + (" (cost-balanced bands)" if rank_bands is not None and world == 1 else ""),
                    "partition": args.partition if rank_bands is not None else ("stripes" if world * K > 1 else "none"),
+                   "interleave": interleave, "bands_per_rank": B if rank_bands is not None else None,
                    "rays": int(rays)},
         "roofline": roof,
         "pipeline_roofline": pipeline_roofline(pmc, pmc_src, images / world / elapsed, pipe_achieved, pipe_bytes_R / R),
@@ -505,7 +563,8 @@ def main():
                                          + ("RCCL over xGMI" if on_device else args.dist_backend),
                                "film_bytes": args.width * args.height * 16,
                                "rank0_rows_owned": owned, "rank0_rows_rendered": rendered,
-                               "rank0_halo_overhead": round(rendered / max(1, owned) - 1.0, 4)}
+                               "rank0_halo_overhead": round(rendered / max(1, owned) - 1.0, 4),
+                               "calibration": calibration}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         label = "1920x1080 8-bounce Cornell" if args.config == "cornell" else f"{args.config} config"
         result["cpu_baseline"] = cpu_baseline(scene, luts_arrays, args.cpu_seconds, label)

@@ -10,7 +10,7 @@ from ._abi import (DCRTError, FEATURE_ALLOW_ANYHIT, FEATURE_DEFAULT, FEATURE_GGX
                    FILTER_MITCHELL, FILTER_TRIANGLE, FilterParams, FrameParams, LIB_PATH, load_library)
 from .scene import Scene  # noqa: F401
 from ._abi import PostFxParams  # noqa: F401
-from .tracer import (HIT_DTYPE, RAY_DTYPE, WavefrontPathTracer, device_count, make_pipelines, make_rays, probe_row_cost,  # noqa: F401
+from .tracer import (HIT_DTYPE, RAY_DTYPE, WavefrontPathTracer, device_count, make_pipelines, make_rays, prepare_pipelines, probe_row_cost,  # noqa: F401
                      render_images_concurrently, save_bmp, srgb_thresholds)
 
 __version__ = "0.1.0"

@@ -421,6 +421,18 @@ def render_images_concurrently(tracers, first_seed: int, count: int, filter_para
         t.synchronize()
 
 
+def prepare_pipelines(tracers, count: int) -> None:
+    """prepare_images on every pipeline for a render_images_concurrently of `count` images: the
+    whole count on banded pipelines, the largest per-pipeline share of a chunk on interleaved
+    ones (each keeps only the images it renders)."""
+    K = len(tracers)
+    if K > 1 and getattr(tracers[0], "interleaved", False):
+        chunk = min(count, K * max(1, min(getattr(t, "pool_images", 1) for t in tracers)))
+        count = -(-chunk // K)
+    for t in tracers:
+        t.prepare_images(count)
+
+
 def probe_row_cost(scene, first_seed: int = 1 << 20, images: int = 1, pool: int = 1 << 22, device: int = 0) -> np.ndarray:
     """Rays cast per film row over `images` images (seeds first_seed ..) of the whole film, from
     the tracer's row-cost probe: exact and schedule-independent, so every rank that probes the

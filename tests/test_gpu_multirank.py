@@ -46,6 +46,9 @@ def test_two_rank_bench_film_equals_single_rank(tmp_path):
     assert all(x > 0 for x in m["per_rank_render_ms"]) and all(x >= 0 for x in m["per_rank_reduce_ms"])
     assert m["rank0_rows_rendered"] >= m["rank0_rows_owned"] > 0 and m["rank0_halo_overhead"] >= 0
     assert d["repeats"] == 5 and len(d["repeat_ms_per_spp"]) == 5
+    # N > 1 default: image-interleaved pipelines over one calibrated cost-balanced band per rank
+    assert d["config"]["interleave"] is True and d["config"]["partition"] == "balanced"
+    assert len(m["calibration"]["rank_ms_per_step"]) == 1 and len(m["calibration"]["rank_ms_per_step"][0]) == 2
     a, b = np.load(single), np.load(multi)
     # 2 images on 2 ranks vs 1 image on 1 rank: compare the 1-rank film of the same 2 images
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *common, "--steps", "2", "--save-film", str(single)],
@@ -119,6 +122,9 @@ def test_bench_default_line_fields(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert d["repeats"] == 5 and len(d["repeat_ms_per_spp"]) == 5
+    # N > 1 default: image-interleaved pipelines over one calibrated cost-balanced band per rank
+    assert d["config"]["interleave"] is True and d["config"]["partition"] == "balanced"
+    assert len(m["calibration"]["rank_ms_per_step"]) == 1 and len(m["calibration"]["rank_ms_per_step"][0]) == 2
     assert abs(d["ms_per_spp"] - sorted(d["repeat_ms_per_spp"])[2]) < 1e-3
     roof = d["roofline"]
     assert roof["frac_algorithmic"] > 0 and roof["bound"].startswith("lds/valu") and roof["scene_in_lds"]

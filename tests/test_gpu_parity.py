@@ -1247,52 +1247,58 @@ def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle
 
 def test_rank_share_full_size_bit_exact(native_lib, golden_luts, oracle_mod):
     """One rank's share of the N = 8 Cornell bench exactly as bench.py builds it on that rank
-    (make_pipelines: world 8, rank 3, three pipelines, the cost-balanced bands cut from the
-    row-cost probe and dealt round-robin), image 0 at 1920x1080 / 8 bounces: the rank's film
-    equals the oracle's film on the rows the rank owns and is zero elsewhere, and its ray counts
-    are the oracle's over the rows its pipelines path-trace (owned rows plus the filter's halo)."""
-    from directcomputeraytracing_amd import Scene, make_pipelines, probe_row_cost, render_images_concurrently, scenes
-    from directcomputeraytracing_amd.partition import balanced_bands, band_owned_rows, band_render_rows, halo_for_radius, row_runs
-    W, H, world, rank, K = 1920, 1080, 8, 3, 3
+    (make_pipelines: world 8, rank 3, three image-interleaved pipelines over the rank's one
+    cost-balanced band, cut from the row-cost probe after a calibration re-cut by rank times --
+    here a synthetic 8 % trend down the image), images 0-2 at 1920x1080 / 8 bounces (one per
+    pipeline): the rank's film equals the oracle's film on the rows it owns, convolved in image
+    order, and is zero elsewhere; its ray counts are the oracle's over the rows it path-traces
+    (owned rows plus the filter's halo)."""
+    from directcomputeraytracing_amd import (Scene, make_pipelines, prepare_pipelines, probe_row_cost,
+                                             render_images_concurrently, scenes)
+    from directcomputeraytracing_amd.partition import (balanced_bands, band_owned_rows, band_render_rows, halo_for_radius,
+                                                       refine_row_cost, row_runs)
+    W, H, world, rank, K, images = 1920, 1080, 8, 3, 3, 3
     s = Scene((W, H))
     scenes.setup_cornell(s, W, H, 8)
     filt = s.filter_params()
     halo = max(1, halo_for_radius(filt.radius, H))
-    cost = probe_row_cost(s)
-    ts = make_pipelines(s, scenes.default_pool(W, H, K), streams=K, images=1, iterations=16, world=world, rank=rank,
-                        row_cost=cost)
+    probe = probe_row_cost(s)
+    first = balanced_bands(probe, world, halo)
+    cost = refine_row_cost(probe, [[b] for b in first], [1.0 + 0.01 * r for r in range(world)], halo)
+    ts = make_pipelines(s, scenes.default_pool(W, H, K), streams=K, images=images, iterations=16, world=world, rank=rank,
+                        row_cost=cost, interleave=True, bands_per_rank=1)
     try:
+        prepare_pipelines(ts, images)
         for t in ts:
             t.clear_film()
             t.reset_stats()
-        render_images_concurrently(ts, 0, 1, filt)
-        for t in ts[1:]:
-            ts[0].add_film_device(t.film_device_ptr())
+        render_images_concurrently(ts, 0, images, filt)
         ts[0].synchronize()
         film = ts[0].read_film()
+        assert all(not t.read_film().any() for t in ts[1:])
         ext = sum(t.counters()["extension_rays"] for t in ts)
         shadow = sum(t.counters()["shadow_rays"] for t in ts)
     finally:
         for t in ts:
             t.destroy()
-    mine = balanced_bands(cost, world * K, halo)[rank::world]
-    assert len(mine) == K
+    mine = balanced_bands(cost, world, halo)[rank::world]
+    assert len(mine) == 1 and mine != [first[rank]], "the calibrated cut is not the probe's"
     owned = band_owned_rows(H, mine)
     assert 0 < owned.sum() < H // 4
     flat = oracle_mod.flat_with_own_bvh(s)
-    fr = oracle_mod.frame_params(s, 0)
-    pos = np.zeros((H, W, 2), np.float32)
-    val = np.zeros((H, W, 4), np.float32)
+    ref = np.zeros_like(film)
     ext_ref = shadow_ref = 0
-    for band in mine:
-        for y0, y1 in row_runs(band_render_rows(H, [band], halo)):
+    for image in range(images):
+        fr = oracle_mod.frame_params(s, image)
+        pos = np.zeros((H, W, 2), np.float32)
+        val = np.zeros((H, W, 4), np.float32)
+        for y0, y1 in row_runs(band_render_rows(H, mine, halo)):
             p, v, _, c = oracle_mod.render(flat, golden_luts, fr, oracle_mod.WAVEFRONT, rect=(0, y0, W, y1 - y0))
             pos[y0:y1], val[y0:y1] = p[y0:y1], v[y0:y1]
             ext_ref += c["extension_rays"]
             shadow_ref += c["shadow_rays"]
-    ref = np.zeros_like(film)
-    for y0, y1 in row_runs(np.nonzero(owned)[0]):
-        oracle_mod.sample_convolution(filt, pos, val, ref, rows=(y0, y1))
+        for y0, y1 in row_runs(np.nonzero(owned)[0]):
+            oracle_mod.sample_convolution(filt, pos, val, ref, rows=(y0, y1))
     assert not film[~owned].any(), "the rank wrote rows it does not own"
     bad = np.count_nonzero(~same_bits(film[owned], ref[owned]).all(-1))
     assert bad == 0, f"{bad} owned film pixels differ"

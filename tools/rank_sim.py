@@ -31,14 +31,16 @@ def main():
     ap.add_argument("--interleave", action="store_true", help="pipelines split the images of the rank's rows (bench --interleave)")
     ap.add_argument("--bands-per-rank", type=int, default=0, help="interleaved: balanced bands per rank (0 = --streams)")
     ap.add_argument("--calibrate", type=int, default=0,
-                    help="steps of a timed calibration run per rank before the timed runs; its rank times re-cut the "
-                         "bands at equal time (partition.refine_row_cost, bench --calibrate)")
+                    help="calibration rounds: each renders every rank's share once, untimed by the result, and its rank "
+                         "times re-cut the bands at equal time (partition.refine_row_cost, bench --calibrate)")
+    ap.add_argument("--calib-repeats", type=int, default=3, help="calibration: median of this many runs per rank")
     ap.add_argument("--fixed-pool", action="store_true", help="pool // streams per pipeline (no pipeline_pool sizing)")
     ap.add_argument("--partition", choices=["balanced", "stripes"], default="balanced",
                     help="balanced: equal-cost contiguous bands from the row-cost probe (bench.py's default); "
                          "stripes: round-robin stripes of --stripe rows")
     args = ap.parse_args()
-    from directcomputeraytracing_amd import Scene, make_pipelines, probe_row_cost, render_images_concurrently, scenes
+    from directcomputeraytracing_amd import (Scene, make_pipelines, prepare_pipelines, probe_row_cost,
+                                             render_images_concurrently, scenes)
     scene = Scene((1920, 1080))
     scenes.setup_cornell(scene, 1920, 1080, 8)
     filt = scene.filter_params()
@@ -54,58 +56,66 @@ def main():
     for n in [int(x) for x in args.gpus.split(",")]:
         times, rays, iters = [], [], []
         cost_n = row_cost
-        if args.calibrate and row_cost is not None and n > 1:
-            # the calibration run: every rank's share of args.calibrate steps, timed once
-            K = max(1, args.streams)
-            calib = []
-            for r in range(n):
-                ts = make_pipelines(scene, args.pool, streams=K, images=args.calibrate * n, iterations=16, world=n, rank=r,
-                                    stripe=args.stripe, image_batch=args.image_batch, row_cost=row_cost,
-                                    fixed_pool=args.fixed_pool, interleave=args.interleave, bands_per_rank=args.bands_per_rank)
-                try:
-                    render_images_concurrently(ts, 20_000, n, filt)
-                    t0 = time.perf_counter()
-                    render_images_concurrently(ts, 30_000, args.calibrate * n, filt)
-                    calib.append(time.perf_counter() - t0)
-                finally:
-                    for t in ts:
-                        t.destroy()
-            cost_n = refine_row_cost(row_cost, rank_bands(row_cost, n, K), calib, halo)
-        for r in range(1 if args.rank0_only else n):
-            # the rank's K concurrent pipelines, as bench.py --streams K runs them
-            K = max(1, args.streams)
-            ts = []
+        K = max(1, args.streams)
+        ranks = list(range(1 if args.rank0_only else n))
+
+        def build(cost):
+            # every rank's K pipelines at once (a few GB each: the 288 GB of HBM hold all eight
+            # ranks), so the repeats can go round-robin over the ranks and a slow drift of the
+            # GPU's clock lands on every rank alike instead of reading as imbalance
+            shares = []
             try:
-                # (bench.py's own construction; --fixed-pool: image batches of the whole pool share)
-                ts = make_pipelines(scene, args.pool, streams=K, images=args.steps * n, iterations=16, world=n, rank=r,
-                                    stripe=args.stripe, image_batch=args.image_batch, row_cost=cost_n,
-                                    fixed_pool=args.fixed_pool, interleave=args.interleave,
-                                    bands_per_rank=args.bands_per_rank)
-                for t in ts:
-                    t.clear_film()
+                for r in ranks:
+                    shares.append(make_pipelines(scene, args.pool, streams=K, images=args.steps * n, iterations=16, world=n,
+                                                 rank=r, stripe=args.stripe, image_batch=args.image_batch, row_cost=cost,
+                                                 fixed_pool=args.fixed_pool, interleave=args.interleave,
+                                                 bands_per_rank=args.bands_per_rank))
+                for ts in shares:
+                    for t in ts:
+                        t.clear_film()
+                    render_images_concurrently(ts, 10_000, n, filt)
+                    prepare_pipelines(ts, args.steps * n)
+            except BaseException:
+                destroy(shares)
+                raise
+            return shares
 
-                def run(first, count):
-                    render_images_concurrently(ts, first, count, filt)
-
-                run(10_000, n)
+        def destroy(shares):
+            for ts in shares:
                 for t in ts:
-                    t.prepare_images(args.steps * n)
-                    t.reset_stats()
-                reps = []
-                for _ in range(max(1, args.repeats)):   # (bench.py: the median of its repeats)
+                    t.destroy()
+
+        def time_ranks(shares, first, repeats):
+            reps = [[] for _ in shares]
+            for _ in range(max(1, repeats)):
+                for i, ts in enumerate(shares):
                     for t in ts:
                         t.clear_film()
                         t.reset_stats()
                     t0 = time.perf_counter()
-                    run(0, args.steps * n)
-                    reps.append((time.perf_counter() - t0) * 1e3 / args.steps)
-                times.append(sorted(reps)[len(reps) // 2])
+                    render_images_concurrently(ts, first, args.steps * n, filt)
+                    reps[i].append((time.perf_counter() - t0) * 1e3 / args.steps)
+            return [sorted(x)[len(x) // 2] for x in reps]   # (bench.py: the median of its repeats)
+
+        cost_n = row_cost
+        for _round in range(args.calibrate if (row_cost is not None and n > 1 and not args.rank0_only) else 0):
+            # a calibration round (bench.py --calibrate): the median rank times of the prepared
+            # workload on other seeds re-cut the bands at equal time
+            shares = build(cost_n)
+            try:
+                calib = time_ranks(shares, 30_000, args.calib_repeats)
+            finally:
+                destroy(shares)
+            cost_n = refine_row_cost(cost_n, rank_bands(cost_n, n, K), calib, halo)
+        shares = build(cost_n)
+        try:
+            times = time_ranks(shares, 0, args.repeats)
+            for ts in shares:
                 cs = [t.counters() for t in ts]
                 rays.append(sum(c["extension_rays"] + c["shadow_rays"] for c in cs) / args.steps)
                 iters.append(max(c.get("iterations", 0) for c in cs) / args.steps)
-            finally:
-                for t in ts:
-                    t.destroy()
+        finally:
+            destroy(shares)
         mx, mean = max(times), sum(times) / len(times)
         base = base or mx
         print(json.dumps({"n_gpus": n, "ms_per_step_max_rank": round(mx, 3), "ms_per_step_mean_rank": round(mean, 3),
