@@ -270,9 +270,13 @@ bool RequiredTraversalStack(const dcrt_flat_scene& s, uint32_t* out)
 // hold -- then every subtree below them depth-first by child pairs. Each root gets a padded
 // slot, so every pair starts at an even index (one 64-B aligned line). Traversal follows the
 // tree, not the indices: hits, node counts and stack depths are those of the flat order.
+// quads (the default; DCRT_NODE_QUADS=0: off): below the top levels the children pairs of a node's two children
+// sit side by side in one 128-B aligned line (a padded half where a child is a leaf), so the
+// fetch that expands one child brings its sibling's children into L2 with it; otherwise a
+// node's left child's pair follows the node's own pair depth-first.
 // Call after RequiredTraversalStack (which checks every reference); false if a node would be
 // placed twice (a child shared between parents).
-bool PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bvh_node>* out)
+bool PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bvh_node>* out, bool quads = false)
 {
     constexpr uint32_t kNone = UINT32_MAX;
     const dcrt_bvh_node* nd = s.bvh_nodes;
@@ -309,6 +313,22 @@ bool PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bv
     }
     for (const uint32_t root : level) {
         stack.assign(1, root);
+        if (quads) {
+            // stack: nodes whose children are placed; expanding one places its children's pairs
+            if (!placeChildren(root)) return false;
+            while (!stack.empty()) {
+                const uint32_t p = stack.back();
+                stack.pop_back();
+                const uint32_t c0 = p + 1, c1 = nd[p].right_child_or_prim_index;
+                if (isLeaf(c0) && isLeaf(c1)) continue;
+                while (order.size() & 3u) order.push_back(kNone);   // one 128-B line
+                if (!isLeaf(c0) && !placeChildren(c0)) return false;
+                if (!isLeaf(c1) && !placeChildren(c1)) return false;
+                if (!isLeaf(c1)) stack.push_back(c1);
+                if (!isLeaf(c0)) stack.push_back(c0);   // the left subtree first
+            }
+            continue;
+        }
         while (!stack.empty()) {
             const uint32_t p = stack.back();
             stack.pop_back();
@@ -892,7 +912,10 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         if (castPair) {
             uint32_t topNodes = 4096;
             if (const char* e = std::getenv("DCRT_TOP_NODES")) topNodes = (uint32_t)std::atoi(e);   // A/B experiments
-            if (!PairLayout(s, topNodes, &pairNodes)) { SetLastError("malformed BVH: a node with two parents"); return DCRT_E_INVALID_ARG; }
+            // quads (profiles/r06_ab_log.md: spaceship -1.6 %, close framing -0.1 / -1.4 %)
+            bool quads = true;
+            if (const char* e = std::getenv("DCRT_NODE_QUADS")) quads = std::atoi(e) != 0;   // A/B experiments
+            if (!PairLayout(s, topNodes, &pairNodes, quads)) { SetLastError("malformed BVH: a node with two parents"); return DCRT_E_INVALID_ARG; }
             nodeCount = (uint32_t)pairNodes.size();
         }
         std::vector<dcrt_bvh_node> devNodes = castPair ? std::move(pairNodes) : std::vector<dcrt_bvh_node>(s.bvh_nodes, s.bvh_nodes + nodeCount);
