@@ -122,9 +122,8 @@ def test_bench_default_line_fields(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert d["repeats"] == 5 and len(d["repeat_ms_per_spp"]) == 5
-    # N > 1 default: image-interleaved pipelines over one calibrated cost-balanced band per rank
-    assert d["config"]["interleave"] is True and d["config"]["partition"] == "balanced"
-    assert len(m["calibration"]["rank_ms_per_step"]) == 1 and len(m["calibration"]["rank_ms_per_step"][0]) == 2
+    # N = 1: three pipelines over cost-balanced bands, not interleaved
+    assert d["config"]["interleave"] is False and d["config"]["partition"] == "balanced"
     assert abs(d["ms_per_spp"] - sorted(d["repeat_ms_per_spp"])[2]) < 1e-3
     roof = d["roofline"]
     assert roof["frac_algorithmic"] > 0 and roof["bound"].startswith("lds/valu") and roof["scene_in_lds"]
