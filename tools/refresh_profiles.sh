@@ -9,7 +9,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-r04}
 mkdir -p gpurun_out/profiles profiles
-IFS=';' read -ra ITEMS <<< "${WORKLOADS:-cornell 20 c20;cornell 64 c64;spaceship 16 s16}"
+# (prof_config runs one pipeline: --pool gives it the bench's whole pool -- three Cornell
+# pipelines of 2^24, two coffee ones -- so the recorded workload key is the bench's)
+IFS=';' read -ra ITEMS <<< "${WORKLOADS:-cornell 20 c20 --pool 50331648;cornell 64 c64 --pool 50331648;spaceship 16 s16}"
 for w in "${ITEMS[@]}"; do
   set -- $w
   cfg=$1 steps=$2 key=$3; shift 3
