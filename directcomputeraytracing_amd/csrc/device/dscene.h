@@ -144,6 +144,18 @@ DEV float4 lds_load4(const float4* genericLds, uint32_t i)
     const LoadF4 v = p[i];
     return make_float4(v.x, v.y, v.z, v.w);
 }
+DEV uint64_t global_load_u64(const uint64_t* g, size_t i)
+{
+    const __attribute__((address_space(1))) uint64_t* p = (const __attribute__((address_space(1))) uint64_t*)(uintptr_t)g;
+    return p[i];
+}
+typedef float LoadF2 __attribute__((ext_vector_type(2)));
+DEV float2 global_load2(const float2* g, size_t i)
+{
+    const __attribute__((address_space(1))) LoadF2* p = (const __attribute__((address_space(1))) LoadF2*)(uintptr_t)g;
+    const LoadF2 v = p[i];
+    return make_float2(v.x, v.y);
+}
 DEV float4 global_load4(const float4* g, size_t i)
 {
     const __attribute__((address_space(1))) LoadF4* p = (const __attribute__((address_space(1))) LoadF4*)(uintptr_t)g;

@@ -1548,7 +1548,8 @@ __device__ __forceinline__ void film_pixel_window(const FilterConsts& c, uint32_
 // posList / valList (accumulate_images): image b's sample textures sit at posList[b] / valList[b]
 // (W*H each, e.g. other pipelines' slots) instead of at slot b of this film's.
 __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t images, const Globals* guard,
-                                                   const float2* const* posList, const float4* const* valList)
+                                                   const float2* const* __restrict__ posList,
+                                                   const float4* const* __restrict__ valList)
 {
     if (guard && (!guard->imageComplete || guard->skipFilm)) return;
     // the images of a completed batch, in order: per pixel the same additions as one
@@ -1558,8 +1559,9 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
     const uint32_t W = film.width, H = film.height;
     const uint32_t total = W * H;
     const uint32_t tilesX = (W + kFilmTile - 1) / kFilmTile, tiles = tilesX * ((H + kFilmTile - 1) / kFilmTile);
-    __shared__ float2 tPos[kFilmSpan * kFilmSpan];
-    __shared__ float4 tVal[kFilmSpan * kFilmSpan];
+    // two tile buffers: image b is convolved from buffer b & 1 while image b + 1's loads are in flight
+    __shared__ float2 tPos[2][kFilmSpan * kFilmSpan];
+    __shared__ float4 tVal[2][kFilmSpan * kFilmSpan];
     for (uint32_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
         const int x0 = (int)(tile % tilesX) * kFilmTile, y0 = (int)(tile / tilesX) * kFilmTile;
         const uint32_t px = (uint32_t)x0 + (threadIdx.x % kFilmTile), py = (uint32_t)y0 + (threadIdx.x / kFilmTile);
@@ -1604,31 +1606,75 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
         } else {
             // staged span [txs, txe] x [tys, tye]: inside the film by construction
             const int span = spanX, ox = txs, oy = tys;
-            for (uint32_t b = 0; b < count; ++b) {
-                const float2* sPos = posList ? posList[b] : film.samplePosition + (size_t)b * total;
-                const float4* sVal = valList ? valList[b] : film.sampleValue + (size_t)b * total;
-                __syncthreads();   // the previous image's tile is no longer read
-                for (int i = (int)threadIdx.x; i < spanX * spanY; i += (int)blockDim.x) {
-                    const size_t q = (size_t)(oy + i / spanX) * W + (size_t)(ox + i % spanX);
-                    tPos[i] = sPos[q];
-                    tVal[i] = sVal[q];
+            // Software-pipelined over the images of a batch: image b + 1's tile is loaded into
+            // registers while image b is convolved from its LDS buffer, and one barrier per image
+            // separates the two buffers' writes from their reads. The barrier is s_barrier after
+            // the LDS stores drain (lgkmcnt), not __syncthreads: that one's fence would also wait
+            // for the next image's loads. (A buffer written at image b + 1 was last read at image
+            // b - 1, which every thread finished before passing image b's barrier.)
+            // (three staging elements per thread: kFilmSpan^2 <= 3 x 256; plain variables, so the
+            // in-flight tile stays in registers)
+            static_assert(kFilmSpan * kFilmSpan <= 3 * 256, "three staging elements per thread");
+            const int nStage = spanX * spanY;
+            const int i0 = (int)threadIdx.x, i1 = i0 + 256, i2 = i0 + 512;
+            const bool s0 = i0 < nStage, s1 = i1 < nStage, s2 = i2 < nStage;
+            const size_t oFirst = (size_t)oy * W + (size_t)ox;
+            const size_t o0 = s0 ? (size_t)(oy + i0 / spanX) * W + (size_t)(ox + i0 % spanX) : oFirst;
+            const size_t o1 = s1 ? (size_t)(oy + i1 / spanX) * W + (size_t)(ox + i1 % spanX) : oFirst;
+            const size_t o2 = s2 ? (size_t)(oy + i2 / spanX) * W + (size_t)(ox + i2 % spanX) : oFirst;
+            float2 nP0{}, nP1{}, nP2{};
+            float4 nV0{}, nV1{}, nV2{};
+            // image b's sample textures: this film's slot b, or a list entry (accumulate_images),
+            // read one image ahead with a vector load (the index made opaque to the uniformity
+            // analysis: a scalar load would share lgkmcnt with the LDS traffic, whose waits would
+            // then drain it too). The two sources run as two instances of the loop, so neither
+            // carries the other's selects and register hazards.
+            uint32_t lane0 = 0u;
+            asm volatile("" : "+v"(lane0));
+            auto run = [&](auto srcPos, auto srcVal) __attribute__((always_inline)) {
+                // (unconditional loads: a thread without a third element loads the span's first
+                // one again, so no branch splits the loads and their waits stay exact)
+                auto stage_load = [&](const float2* lp, const float4* lv) __attribute__((always_inline)) {
+                    nP0 = global_load2(lp, o0); nV0 = global_load4(lv, o0);
+                    nP1 = global_load2(lp, o1); nV1 = global_load4(lv, o1);
+                    nP2 = global_load2(lp, o2); nV2 = global_load4(lv, o2);
+                };
+                if (count > 0) stage_load(srcPos(0u), srcVal(0u));
+                const float2* nextPos = count > 1 ? srcPos(1u) : nullptr;
+                const float4* nextVal = count > 1 ? srcVal(1u) : nullptr;
+                for (uint32_t b = 0; b < count; ++b) {
+                    const uint32_t buf = b & 1u;
+                    if (s0) { tPos[buf][i0] = nP0; tVal[buf][i0] = nV0; }
+                    if (s1) { tPos[buf][i1] = nP1; tVal[buf][i1] = nV1; }
+                    if (s2) { tPos[buf][i2] = nP2; tVal[buf][i2] = nV2; }
+                    if (b + 1 < count) {
+                        stage_load(nextPos, nextVal);
+                        if (b + 2 < count) { nextPos = srcPos(b + 2u); nextVal = srcVal(b + 2u); }
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                    if (mine) {
+                        const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
+                        float wsum = 0.0f;
+                        V3 sum = mk(0.0f, 0.0f, 0.0f);
+                        for (int y = ys; y <= ye; ++y)
+                            for (int x = xs; x <= xe; ++x) {
+                                const int i = (y - oy) * span + (x - ox);
+                                const float2 sp = tPos[buf][i];
+                                const float4 sv = tVal[buf][i];
+                                const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
+                                sum = sum + mk(sv.x, sv.y, sv.z) * w;
+                                wsum = wsum + w;
+                            }
+                        v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
+                    }
                 }
-                __syncthreads();
-                if (mine) {
-                    const float cx = (float)px + 0.5f, cy = (float)py + 0.5f;
-                    float wsum = 0.0f;
-                    V3 sum = mk(0.0f, 0.0f, 0.0f);
-                    for (int y = ys; y <= ye; ++y)
-                        for (int x = xs; x <= xe; ++x) {
-                            const int i = (y - oy) * span + (x - ox);
-                            const float2 sp = tPos[i];
-                            const float4 sv = tVal[i];
-                            const float w = evaluate_filter(c, cx - (sp.x + (float)x), cy - (sp.y + (float)y));
-                            sum = sum + mk(sv.x, sv.y, sv.z) * w;
-                            wsum = wsum + w;
-                        }
-                    v.x = v.x + sum.x; v.y = v.y + sum.y; v.z = v.z + sum.z; v.w = v.w + wsum;
-                }
+            };
+            if (posList) {
+                run([&](uint32_t b) __attribute__((always_inline)) { return (const float2*)global_load_u64((const uint64_t*)posList, b + lane0); },
+                    [&](uint32_t b) __attribute__((always_inline)) { return (const float4*)global_load_u64((const uint64_t*)valList, b + lane0); });
+            } else {
+                run([&](uint32_t b) __attribute__((always_inline)) { return film.samplePosition + (size_t)b * total; },
+                    [&](uint32_t b) __attribute__((always_inline)) { return film.sampleValue + (size_t)b * total; });
             }
         }
         if (mine) film.accum[(size_t)py * W + px] = v;

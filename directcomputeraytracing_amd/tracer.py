@@ -413,8 +413,13 @@ def render_images_concurrently(tracers, first_seed: int, count: int, filter_para
                                                                seed_stride=K, convolve=False) if s < n else None)
             for t in tracers:
                 t.synchronize()
-            ptrs = [tracers[j % K].image_sample_ptrs(j // K) for j in range(n)]
-            tracers[0].accumulate_images([p for p, _ in ptrs], [v for _, v in ptrs], filter_params)
+            # image k of a pipeline's call sits in its sample slot k: slot 0's pointers plus k
+            # whole-film strides (one ABI call per pipeline, not one per image)
+            W, H = tracers[0].width, tracers[0].height
+            base = [t.image_sample_ptrs(0) for t in tracers[:min(K, n)]]
+            pos = [base[j % K][0] + (j // K) * W * H * 8 for j in range(n)]
+            val = [base[j % K][1] + (j // K) * W * H * 16 for j in range(n)]
+            tracers[0].accumulate_images(pos, val, filter_params)
         return
     _run_threads(tracers, lambda i, t: t.render_images(first_seed, count, filter_params))
     for t in tracers:

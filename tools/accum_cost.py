@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--rank", type=int, default=3)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--per-image-calls", action="store_true", help="one image_sample_ptrs call per image (round-6 first form)")
     args = ap.parse_args()
     from directcomputeraytracing_amd import Scene, make_pipelines, prepare_pipelines, probe_row_cost, scenes
     from directcomputeraytracing_amd.tracer import _run_threads
@@ -43,14 +44,25 @@ def main():
                 for t in ts:
                     t.synchronize()
                 b = time.perf_counter()
-                ptrs = [ts[j % K].image_sample_ptrs(j // K) for j in range(m)]
-                ts[0].accumulate_images([p for p, _ in ptrs], [v for _, v in ptrs], filt)
+                if args.per_image_calls:
+                    ptrs = [ts[j % K].image_sample_ptrs(j // K) for j in range(m)]
+                    pos, val = [p for p, _ in ptrs], [v for _, v in ptrs]
+                else:   # (render_images_concurrently's arithmetic)
+                    W, H = ts[0].width, ts[0].height
+                    base = [t.image_sample_ptrs(0) for t in ts[:min(K, m)]]
+                    pos = [base[j % K][0] + (j // K) * W * H * 8 for j in range(m)]
+                    val = [base[j % K][1] + (j // K) * W * H * 16 for j in range(m)]
+                    assert all((pos[j], val[j]) == ts[j % K].image_sample_ptrs(j // K) for j in (0, m - 1, m // 2))
+                b2 = time.perf_counter()
+                ts[0].accumulate_images(pos, val, filt)
                 c = time.perf_counter()
                 t_render += b - a
                 t_acc += c - b
+                t_ptrs = b2 - b
             total = time.perf_counter() - t0
             print(f"rep {rep}: {n} image slices, chunk {chunk}: render {t_render * 1e3:.2f} ms, ordered film pass "
-                  f"{t_acc * 1e3:.2f} ms ({t_acc / total * 100:.1f} % of {total * 1e3:.2f} ms)", flush=True)
+                  f"{t_acc * 1e3:.2f} ms ({t_acc / total * 100:.1f} % of {total * 1e3:.2f} ms; pointer lists "
+                  f"{t_ptrs * 1e3:.2f} ms of it)", flush=True)
     finally:
         for t in ts:
             t.destroy()
