@@ -681,8 +681,10 @@ DEV bool trav_visit_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uin
 // Phase B: the parked leaf's work. TLAS leaf: move the ray into the instance and
 // continue at its BLAS root. BLAS leaf: test triangles [ref, ref + count), then pop.
 // LANE_ANY: any-hit is a per-lane choice (s.anyHit), for the merged ray-cast kernel
+// FLAT (the entry-free node order of the cache-only IDENT kernel, tracer.hip EntryFreeLayout): no
+// TLAS leaves -- a leaf is a BLAS triangle leaf whose count field holds its instance + 1
 template <bool ANY_HIT, bool INSTR, bool OPACITY = false, bool LANE_ANY = false, bool ALL_CACHED = false, bool IDENT = false,
-          bool RING = false>
+          bool RING = false, bool FLAT = false>
 DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     s.parked = false;
@@ -693,13 +695,13 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
         leafMisc = asu(b.w);
     }
     const uint32_t primOrInst = (leafMisc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
-    if (IDENT && (leafMisc & 0x4u)) {   // (every instance the identity: see trav_visit)
+    if (!FLAT && IDENT && (leafMisc & 0x4u)) {   // (every instance the identity: see trav_visit)
         s.inst = primOrInst;
         s.node = leafRef | 0x80000000u;
         if (INSTR) ++st.blas;
         return false;
     }
-    if (leafMisc & 0x4u) {
+    if (!FLAT && (leafMisc & 0x4u)) {
         const float4* M;
         uint32_t identity;
         if (ALL_CACHED) {
@@ -772,11 +774,11 @@ DEV bool trav_leaf(const DeviceScene& sc, TravState& s, bool watertight, uint32_
             s.tMax = t;
             s.hit.t = t; s.hit.u = u; s.hit.v = v;
             s.hit.tri = (p & 0x7FFFFFFFu) | (bf ? 0x80000000u : 0u);
-            s.hit.inst = s.inst;
+            s.hit.inst = FLAT ? primOrInst - 1u : s.inst;
         }
         return false;
     };
-    if (sc.singlePrimLeaves) {   // (uniform: straight-line code, no loop)
+    if (FLAT || sc.singlePrimLeaves) {   // (uniform: straight-line code, no loop)
         if (test(leafRef)) return true;
     } else {
         const uint32_t end = leafRef + primOrInst;

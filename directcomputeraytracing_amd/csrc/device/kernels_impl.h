@@ -778,7 +778,8 @@ __device__ __forceinline__ void ring_maintain(const DeviceScene& sc, TravState& 
 }
 
 template <bool ANY_HIT, bool INSTR, bool OPACITY, bool LANE_ANY = false, bool ALL_CACHED = false, bool PAIR = false,
-          int LAYOUT = kLayoutScene, bool IDENT = false, bool RING = false, typename Lookup, typename Fetch, typename Emit>
+          int LAYOUT = kLayoutScene, bool IDENT = false, bool RING = false, bool FLAT = false, typename Lookup, typename Fetch,
+          typename Emit>
 __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t n, uint32_t features, uint32_t kRefillLanes,
                                                  uint32_t kParkLanes, uint32_t* lds, uint32_t shift, Lookup lookup, Fetch fetch,
                                                  Emit emit, TraversalStats& st, int waveTag = -1)
@@ -866,7 +867,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             for (int k = 0; k < kVisitsPerCheck; ++k) {
                 if (ls == kRun) {
                     const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair<false, LAYOUT, RING>(sc, s, lds, shift)
-                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, (ALL_CACHED || IDENT) && !OPACITY && DCRT_INLINE_ENTRY, IDENT, RING>(sc, s, lds, shift, st);
+                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, !FLAT && (ALL_CACHED || IDENT) && !OPACITY && DCRT_INLINE_ENTRY, IDENT, RING>(sc, s, lds, shift, st);
                     if (fin) ls = kFin;
                     else if (s.parked) ls = kPark;
                 }
@@ -891,7 +892,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
         // phase B: the parked lanes' leaf work, shared by many lanes at once
         if (__ballot(ls == kPark) != 0ull) DCRT_PHASE_COUNT(5);
         if (ls == kPark)
-            ls = trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED, IDENT, RING>(sc, s, watertight, lds, shift, st) ? kFin : kRun;
+            ls = trav_leaf<ANY_HIT, INSTR, OPACITY, LANE_ANY, ALL_CACHED, IDENT, RING, FLAT>(sc, s, watertight, lds, shift, st) ? kFin : kRun;
         DCRT_PHASE(2);
     }
     DCRT_PHASE_FLUSH();
@@ -1042,7 +1043,8 @@ __global__ __launch_bounds__(256) DCRT_CAST_OCCUPANCY void shadow_kernel(PathPoo
 #endif
 // RING: the traversal stack as an LDS window over a per-lane global column (ring_maintain), for
 // scenes whose whole stack would cost LDS occupancy (tracer.hip UploadScene).
-template <bool INSTR, bool OPACITY, bool ALL_CACHED, bool PAIR, bool IDENT = false, bool RING = false>
+// FLAT: the cache-only IDENT kernel over the entry-free node order (tracer.hip EntryFreeLayout)
+template <bool INSTR, bool OPACITY, bool ALL_CACHED, bool PAIR, bool IDENT = false, bool RING = false, bool FLAT = false>
 __global__ __launch_bounds__(256)
 #ifndef DCRT_GLOBAL_CAST_WAVES_PER_EU
 #define DCRT_GLOBAL_CAST_WAVES_PER_EU DCRT_CAST_WAVES_PER_EU   // (the global-memory, non-pair kernel; A/B)
@@ -1073,7 +1075,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? (IDENT ? D
         const FrameConstants& f = *fc;
         const uint32_t* pixels = sgpr_ptr((const uint32_t*)pool.pixel);
         uint32_t rays = 0;
-        persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT, RING>(
+        persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT, RING, FLAT>(
             sc, virt, f.features, f.refillLanes, f.parkLanes, stackMem + threadIdx.x, block_shift(),
             [&](uint32_t i) __attribute__((always_inline)) { return i; },
             [&](uint32_t i, uint32_t v, TravState& s) __attribute__((always_inline)) {
@@ -1100,7 +1102,7 @@ __attribute__((amdgpu_waves_per_eu(ALL_CACHED && !OPACITY && !INSTR ? (IDENT ? D
     } else {
     // (node order: the pair kernels run on pair-ordered scenes, the other non-counting ones on
     // PackBVH-ordered ones -- tracer.hip takes both from castPair -- the counting ones on either)
-    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT, RING>(
+    persistent_trace<false, INSTR, OPACITY, true, ALL_CACHED, PAIR, kLayout, IDENT, RING, FLAT>(
         sc, nExt + nShadow, fc->features, fc->refillLanes, fc->parkLanes, stackMem + threadIdx.x, block_shift(),
         [&](uint32_t i) __attribute__((always_inline)) {
             // either kind: its record's position in its queue (no load)
@@ -1921,6 +1923,7 @@ template __global__ void cast_kernel<true, true, true, false>(PathPool, DeviceSc
 template __global__ void cast_kernel<false, false, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void cast_kernel<false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void cast_kernel<false, false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
+template __global__ void cast_kernel<false, false, true, false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void cast_kernel<true, false, true, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void cast_kernel<false, false, false, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);
 template __global__ void cast_kernel<true, false, false, false, true>(PathPool, DeviceScene, const FrameConstants*, Counters*, Counters*, Globals*, unsigned long long*);

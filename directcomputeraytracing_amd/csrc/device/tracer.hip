@@ -17,6 +17,7 @@
 #include <mutex>
 #include <string>
 #include <type_traits>
+#include <limits>
 #include <vector>
 
 #include "../../../include/dcrt.h"
@@ -170,8 +171,9 @@ using CastFn = void (*)(PathPool, DeviceScene, const FrameConstants*, Counters*,
 // x pair-expanding traversal (the non-counting kernels of scenes not in the LDS cache) x the
 // world ray in every space (IDENT) x the spilling stack window (RING: non-counting, opaque,
 // global-memory kernels)
-CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair, bool ident = false, bool ring = false)
+CastFn CastKernel(bool instr, bool opacity, bool allCached, bool pair, bool ident = false, bool ring = false, bool flat = false)
 {
+    if (flat && ident && allCached && !opacity && !instr && !ring) return cast_kernel<false, false, true, false, true, false, true>;
     if (ring && !instr && !opacity && !allCached) {
         if (pair) return cast_kernel<false, false, false, true, false, true>;
         return ident ? cast_kernel<false, false, false, false, true, true> : cast_kernel<false, false, false, false, false, true>;
@@ -348,6 +350,63 @@ bool PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bv
     return true;
 }
 
+// The entry-free node order of the cache-only IDENT kernel (cast_kernel<..., FLAT>; every instance's
+// inverse exactly the identity, single-triangle leaves). A TLAS leaf becomes an interior node (misc 3:
+// its near child is taken by negMask bit 3, the front-to-back flag) whose children are an empty node
+// and a copy of its instance's BLAS; the BLAS triangle leaves carry instance + 1 in their count field.
+// The kernel then has no BLAS-entry step in its node visit: the TLAS leaf's box is tested as before,
+// the BLAS root is visited next (or after the empty node, which no ray hits: all its planes are +inf,
+// so its slab interval is empty or starts at +inf), and hits, their order and their tMax are the
+// reference's bit for bit -- the empty node adds a visit and a stack entry, no triangle test. (The
+// counting kernels keep PackBVH's order and their counts are the reference's.) False if a leaf holds
+// more than one triangle; `extraDepth` is the stack entries the empty nodes add (1).
+bool EntryFreeLayout(const dcrt_flat_scene& s, std::vector<dcrt_bvh_node>* out)
+{
+    const dcrt_bvh_node* nd = s.bvh_nodes;
+    const uint32_t n = s.bvh_node_count;
+    out->clear();
+    out->reserve((size_t)n + 2u * s.instance_count);
+    bool ok = true;
+    // (explicit stack: (node, instance + 1 or 0 in the TLAS, the slot whose `right` field takes it))
+    struct Item { uint32_t node, inst1, parent; };
+    std::vector<Item> todo{{0u, 0u, UINT32_MAX}};
+    while (!todo.empty() && ok) {
+        const Item it = todo.back();
+        todo.pop_back();
+        if (it.node >= n) { ok = false; break; }
+        const uint32_t idx = (uint32_t)out->size();
+        if (it.parent != UINT32_MAX) (*out)[it.parent].right_child_or_prim_index = idx;
+        dcrt_bvh_node v = nd[it.node];
+        if (it.inst1 == 0u && (v.misc & 0x4u)) {
+            // TLAS leaf -> interior node: left child the empty node, right child the BLAS copy
+            const uint32_t inst = (v.misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
+            if (inst + 1u > DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT) { ok = false; break; }
+            const uint32_t blas = v.right_child_or_prim_index;
+            v.misc = 3u;
+            out->push_back(v);
+            dcrt_bvh_node empty{};
+            const float inf = std::numeric_limits<float>::infinity();
+            empty.bbox_min[0] = empty.bbox_min[1] = empty.bbox_min[2] = inf;
+            empty.bbox_max[0] = empty.bbox_max[1] = empty.bbox_max[2] = inf;
+            empty.misc = 0u;
+            out->push_back(empty);
+            todo.push_back({blas, inst + 1u, idx});
+        } else if (v.misc >= 4u) {
+            // BLAS triangle leaf (a TLAS-level triangle leaf cannot exist)
+            if (it.inst1 == 0u || ((v.misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT) != 1u) { ok = false; break; }
+            v.misc = (v.misc & 0x7u) | (it.inst1 << 3);
+            out->push_back(v);
+        } else {
+            // interior: the left child (node + 1) right behind it, the right child after its subtree
+            out->push_back(v);
+            todo.push_back({v.right_child_or_prim_index, it.inst1, idx});
+            todo.push_back({it.node + 1u, it.inst1, UINT32_MAX});
+        }
+        if (out->size() > (size_t)n * 4u + 64u) { ok = false; break; }   // (a malformed tree: refuse)
+    }
+    return ok && !out->empty();
+}
+
 }  // namespace
 
 struct dcrt_tracer {
@@ -386,6 +445,9 @@ struct dcrt_tracer {
     size_t castLdsFull = 0;            // the layout of every kernel but the ring cast: stackSize + 2 rows + the cache
     uint32_t ringRows = 0;             // the ring cast kernel's LDS stack window (0: whole stack in LDS)
     DeviceScene sceneRing{};           // the scene as the ring cast kernel sees it (stackRows = ringRows, spill column)
+    bool castFlat = false;             // the cache-only IDENT cast runs on the entry-free node order (EntryFreeLayout)
+    DeviceScene sceneFlat{};           // the scene as that kernel sees it (its nodes, one more stack row)
+    size_t castLdsFlat = 0;
     uint32_t castPerCU = 0;            // resident cast workgroups per CU
     bool castAllCached = false;        // the scene fits the LDS cache: cast_kernel<., ., true, .>
     bool castPair = false;             // trav_visit_pair: the scene outgrows an XCD's L2 (UploadScene)
@@ -1020,13 +1082,43 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         // front of the same cache
         castLdsFull = castLds + (launchLds - stackLds);
         castLds = launchLds;
+        // The entry-free node order for the cache-only IDENT kernel (EntryFreeLayout: no BLAS-entry
+        // step per node visit), where its nodes, the triangles and one more stack row still fit
+        // the LDS the IDENT kernel runs at (DCRT_FLAT_CAST=0: off, A/B and tests)
+        castFlat = false;
+        bool flatWanted = true;
+        if (const char* e = std::getenv("DCRT_FLAT_CAST")) flatWanted = std::atoi(e) != 0;
+        if (flatWanted && castAllCached && castIdent && mergedCasts && d.singlePrimLeaves) {
+            std::vector<dcrt_bvh_node> flat;
+            if (EntryFreeLayout(s, &flat)) {
+                const size_t flatLds = (size_t)(d.stackSize + 3u) * castBlock * 4 + flat.size() * 32 + (size_t)s.triangle_count * 144;
+                int identPerCU = 0, flatPerCU = 0;
+                CHECKED(castOccupancy(CastKernel(false, false, true, false, true, false), castLds, &identPerCU));
+                CHECKED(castOccupancy(CastKernel(false, false, true, false, true, false, true), flatLds, &flatPerCU));
+                if (flatPerCU >= identPerCU && flatLds <= 65536) {
+                    dcrt_bvh_node* fn = nullptr;
+                    CHECKED(upload(&fn, flat.data(), flat.size()));
+                    HIPCHECK(hipStreamSynchronize(stream));   // (flat ends with this block)
+                    sceneFlat = scene;
+                    sceneFlat.nodes = (const float4*)fn;
+                    sceneFlat.nodeCount = (uint32_t)flat.size();
+                    sceneFlat.cachedNodes = (uint32_t)flat.size();
+                    sceneFlat.cachedInstances = 0u;
+                    sceneFlat.stackSize = d.stackSize + 1u;
+                    sceneFlat.stackRows = d.stackSize + 3u;
+                    castLdsFlat = flatLds;
+                    castFlat = true;
+                }
+            }
+        }
     }
     {
         // The persistent traversal kernels run exactly one resident wave of workgroups.
         hipDeviceProp_t prop;
         HIPCHECK(hipGetDeviceProperties(&prop, device));
         int perCU = 0;
-        CHECKED(castOccupancy(CastKernel(false, false, castAllCached, castPair, castIdent, ringRows != 0), castLds, &perCU));
+        if (castFlat) CHECKED(castOccupancy(CastKernel(false, false, true, false, true, false, true), castLdsFlat, &perCU));
+        else CHECKED(castOccupancy(CastKernel(false, false, castAllCached, castPair, castIdent, ringRows != 0), castLds, &perCU));
         if (const char* b = std::getenv("DCRT_CAST_BLOCKS_PER_CU")) {   // tuning experiments
             const int v = std::atoi(b);
             if (v >= 1 && v < perCU) perCU = v;
@@ -1383,9 +1475,10 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
     if (mergedCasts) {
         const bool ring = ringRows != 0 && !instrCounters && !opacity;   // (the ring kernel; the counting and
                                                                         // any-hit kernels keep the whole stack)
-        auto cast = CastKernel(instrCounters, opacity, castAllCached, castPair, castIdent, ring);
-        hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), ring ? castLds : castLdsFull, stream, e0, e1, 0, pool,
-                              ring ? sceneRing : scene,
+        const bool flat = castFlat && !instrCounters && !opacity;
+        auto cast = CastKernel(instrCounters, opacity, castAllCached, castPair, castIdent, ring, flat);
+        hipExtLaunchKernelGGL(cast, dim3(castGrid), dim3(castBlock), flat ? castLdsFlat : ring ? castLds : castLdsFull, stream, e0,
+                              e1, 0, pool, flat ? sceneFlat : ring ? sceneRing : scene,
                               (const FrameConstants*)dFrame, cnt, next, dGlobals, dInstr);
     } else {
         auto ext = instrCounters ? (opacity ? extension_kernel<true, true> : extension_kernel<true, false>)
@@ -1947,8 +2040,8 @@ DCRT_API int dcrt_tracer_get_info(dcrt_tracer* t, dcrt_tracer_info* out)
     out->material_grid = t->materialGrid;
     out->cast_grid = t->castResident;
     out->material_lds = t->materialLds;
-    out->cast_identity = t->castIdent ? 1u : 0u;
-    out->stack_lds_rows = t->hasScene ? (t->ringRows ? t->ringRows : t->scene.stackRows) : 0u;
+    out->cast_identity = t->castIdent ? (t->castFlat ? 2u : 1u) : 0u;
+    out->stack_lds_rows = t->hasScene ? (t->ringRows ? t->ringRows : t->castFlat ? t->sceneFlat.stackRows : t->scene.stackRows) : 0u;
     out->ring_rows = t->hasScene ? t->ringRows : 0u;
     out->cast_waves_per_cu = t->castPerCU * (t->castBlock / 64u);
     return DCRT_OK;

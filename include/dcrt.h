@@ -287,7 +287,8 @@ typedef struct dcrt_tracer_info {
     uint32_t cast_grid;           /* persistent cast-kernel workgroups (resident on the chip) */
     uint32_t material_lds;        /* bytes of MATERIAL's LDS scene copy (0: not used)      */
     uint32_t cast_identity;       /* 1: the cache-only cast kernel without instance space
-                                     (every instance's inverse exactly the identity)       */
+                                     (every instance's inverse exactly the identity); 2: the
+                                     same over the entry-free node order (no BLAS-entry step) */
     uint32_t stack_lds_rows;      /* LDS stack rows per lane of the launched cast kernel: traversal_stack + 2,
                                      or ring_rows                                          */
     uint32_t ring_rows;           /* 0, or the LDS window (rows) of a spilling traversal stack: deeper

@@ -518,22 +518,25 @@ def test_image_batches_match_single_images(native_lib, golden_luts, oracle_mod):
 def test_identity_cast_kernel_bit_exact(native_lib, golden_luts, monkeypatch, cached):
     """The cast kernel without instance space (every instance's inverse exactly the identity, as
     for every OBJ shape: IDENT in dscene.h) against the kernel that keeps it (DCRT_IDENT_CAST=0),
-    as the cache-only kernel and (DCRT_NO_LDS_CACHE=1) as the global-memory one: the same samples,
-    RNG state, film and ray counts bit for bit, and the instrumented traversal counts (node
-    visits, triangle tests, BLAS entries) equal."""
+    as the cache-only kernel and (DCRT_NO_LDS_CACHE=1) as the global-memory one -- and the cache-only
+    one over the entry-free node order (FLAT, tracer.hip EntryFreeLayout: cast_identity 2) against
+    it over PackBVH's (DCRT_FLAT_CAST=0): the same samples, RNG state, film and ray counts bit for
+    bit, and the instrumented traversal counts (node visits, triangle tests, BLAS entries) equal."""
     from directcomputeraytracing_amd import FILTER_BOX, FilterParams, WavefrontPathTracer
     monkeypatch.setenv("DCRT_NO_LDS_CACHE", "0" if cached else "1")
     s = cornell(96, 64, 6)
     filt = FilterParams(FILTER_BOX, 1.0, 1.5, 1 / 3, 1 / 3, 3)
     runs = {}
-    for ident in ("1", "0"):
-        monkeypatch.setenv("DCRT_IDENT_CAST", ident)
+    for ident in ("1", "0", "1-noflat"):
+        monkeypatch.setenv("DCRT_IDENT_CAST", ident[0])
+        monkeypatch.setenv("DCRT_FLAT_CAST", "0" if ident.endswith("noflat") else "1")
         t = WavefrontPathTracer(path_pool_size=1 << 14, debug_rng=True)
         try:
             t.set_luts(golden_luts)
             t.on_scene_loaded(s)
             info = t.info()
-            assert info["scene_in_lds"] == (1 if cached else 0) and info["cast_identity"] == (1 if ident == "1" else 0)
+            want = 0 if ident == "0" else (2 if cached and ident == "1" else 1)
+            assert info["scene_in_lds"] == (1 if cached else 0) and info["cast_identity"] == want, info
             _assert_cast_grid_resident(info)
             t.clear_film()
             t.render_images(0, 3, filt)
@@ -545,10 +548,11 @@ def test_identity_cast_kernel_bit_exact(native_lib, golden_luts, monkeypatch, ca
             runs[ident] = (film, samples, rng, c, {k: st[k] for k in st if k.endswith(("visits", "tests", "entries"))})
         finally:
             t.destroy()
-    (fa, (pa, va), ra, ca, sa), (fb, (pb, vb), rb, cb, sb) = runs["1"], runs["0"]
-    assert np.array_equal(ra, rb) and same_bits(pa, pb).all() and same_bits(va, vb).all() and same_bits(fa, fb).all()
-    assert ca["extension_rays"] == cb["extension_rays"] and ca["shadow_rays"] == cb["shadow_rays"]
-    assert sa == sb and sa["ext_node_visits"] > 0
+    for other in ("0", "1-noflat"):
+        (fa, (pa, va), ra, ca, sa), (fb, (pb, vb), rb, cb, sb) = runs["1"], runs[other]
+        assert np.array_equal(ra, rb) and same_bits(pa, pb).all() and same_bits(va, vb).all() and same_bits(fa, fb).all()
+        assert ca["extension_rays"] == cb["extension_rays"] and ca["shadow_rays"] == cb["shadow_rays"]
+        assert sa == sb and sa["ext_node_visits"] > 0
 
 
 @pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
@@ -887,7 +891,7 @@ def test_stack_ring_and_split_casts_bit_exact(native_lib, golden_luts, oracle_mo
         assert info["pair_traversal"] == (1 if kernel == "pair" else 0)
         assert info["ring_rows"] == (0 if kernel == "split" else 8)
         if kernel == "ident":
-            assert info["cast_identity"] == (1 if scene_name == "cornell" else 0)
+            assert info["cast_identity"] == (1 if scene_name == "cornell" else 0)   # (the ring kernel: not cache-only)
     finally:
         t.destroy()
 
@@ -1199,7 +1203,7 @@ def test_bench_configuration_full_size_bit_exact(native_lib, golden_luts, oracle
     try:
         info = ts[0].info()
         if config == "cornell":
-            assert info["scene_in_lds"] == 1 and info["cast_identity"] == 1
+            assert info["scene_in_lds"] == 1 and info["cast_identity"] == 2   # (IDENT over the entry-free order)
         elif config == "coffee":
             assert info["scene_in_lds"] == 0 and info["pair_traversal"] == 0
         elif config.startswith("spaceship"):

@@ -102,7 +102,7 @@ def test_random_scenes_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatc
         info = t.info()
         assert info["pair_traversal"] == (1 if cache == "pair" else 0)
         if cache == "lds" and kind == "obj":   # (the XML scenes' soup is partly cached: nodes in LDS, the rest global)
-            assert info["scene_in_lds"] == 1 and info["cast_identity"] == 1
+            assert info["scene_in_lds"] == 1 and info["cast_identity"] in (1, 2)
         if cache == "ring8":
             assert info["ring_rows"] == 8
     finally:
