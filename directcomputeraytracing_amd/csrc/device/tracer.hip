@@ -351,7 +351,9 @@ bool PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bv
 }
 
 // The entry-free node order of the cache-only IDENT kernel (cast_kernel<..., FLAT>; every instance's
-// inverse exactly the identity, single-triangle leaves). A TLAS leaf becomes an interior node (misc 3:
+// inverse exactly the identity, single-triangle leaves). A TLAS leaf whose box is its BLAS root's bit
+// for bit is replaced by (a copy of) that root: the root's visit would repeat the leaf's box test with
+// the same world ray and tMax (IDENT), so skipping it changes no hit. Any other TLAS leaf becomes an interior node (misc 3:
 // its near child is taken by negMask bit 3, the front-to-back flag) whose children are an empty node
 // and a copy of its instance's BLAS; the BLAS triangle leaves carry instance + 1 in their count field.
 // The kernel then has no BLAS-entry step in its node visit: the TLAS leaf's box is tested as before,
@@ -377,6 +379,19 @@ bool EntryFreeLayout(const dcrt_flat_scene& s, std::vector<dcrt_bvh_node>* out)
         const uint32_t idx = (uint32_t)out->size();
         if (it.parent != UINT32_MAX) (*out)[it.parent].right_child_or_prim_index = idx;
         dcrt_bvh_node v = nd[it.node];
+        if (it.inst1 == 0u && (v.misc & 0x4u)) {
+            const uint32_t inst = (v.misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
+            const uint32_t blas = v.right_child_or_prim_index;
+            if (blas < n && inst + 1u <= DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT &&
+                std::memcmp(v.bbox_min, nd[blas].bbox_min, sizeof(v.bbox_min)) == 0 &&
+                std::memcmp(v.bbox_max, nd[blas].bbox_max, sizeof(v.bbox_max)) == 0) {
+                // the BLAS root's box is the TLAS leaf's bit for bit (an identity instance's bounds
+                // usually are): its visit would repeat the leaf's test with the same ray and tMax,
+                // so the root takes the leaf's place and the ray enters with no visit of its own
+                todo.push_back({blas, inst + 1u, it.parent});
+                continue;
+            }
+        }
         if (it.inst1 == 0u && (v.misc & 0x4u)) {
             // TLAS leaf -> interior node: left child the empty node, right child the BLAS copy
             const uint32_t inst = (v.misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
