@@ -90,6 +90,7 @@ struct DeviceScene {
     uint32_t cachedInstances;     // 0, or instanceCount: every inverse transform + identity flag, after the triangles
     uint32_t singlePrimLeaves;    // 1: every BLAS leaf holds exactly one triangle (BVHAccel.cpp's builder always does)
     uint32_t pairLayout;          // node order: 0 PackBVH's (flat scene), 1 child pairs (kLayoutPairs)
+    uint32_t skipRoot;            // 1: trav_skip_root at a ray's start (the non-counting trav_visit kernels)
     // MATERIAL's LDS scene copy (material_kernel<CAPS, true>, small scenes): the material and
     // light counts it copies (0 when the variant is not used)
     uint32_t ldsMaterials, ldsLights;
@@ -599,6 +600,47 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         s.leafMisc = misc;
     }
     return done;
+}
+
+// A ray whose origin lies strictly inside the root's box (every ray of a scene that encloses its
+// camera) hits that box: per axis one slab plane lies below the origin and one above, so the signs
+// of (plane - o) are exact and every axis' interval holds 0 -- t0 <= 0 < t1 up to signed zeros and
+// infinities, hence t1 >= t0, t0 < tMax (tMax > 0, or t0 < 0 = tMax) and t1 >= tMin = 0. Its first
+// visit is then the root's descend, done here at the ray's start without the box test: the near
+// child (split axis' direction sign) next, the far one pushed -- trav_visit's outcome bit for bit.
+// (Non-counting kernels: the counting ones visit the root as the reference does.)
+template <bool ALL_CACHED, int LAYOUT, bool IDENT>
+DEV void trav_skip_root(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift)
+{
+    // (and on down the near children while their boxes hold the origin strictly: each of those
+    // visits is the same sure hit; sc.skipRoot levels at most, nodes of the LDS cache only)
+    const uint32_t stride = stack_stride<ALL_CACHED>(shift);
+    const V3 o = IDENT ? s.o : s.lo();
+    const bool positive = s.tMax > 0.0f;
+    uint32_t node = 0u;
+    bool go = positive;
+    for (uint32_t level = 0; level < sc.skipRoot; ++level) {
+        const uint32_t idx = node & 0x7FFFFFFFu;
+        if (!ALL_CACHED && idx >= sc.cachedNodes) go = false;
+        if (__ballot(go) == 0ull) break;
+        float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = a;
+        if (go) {
+            const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
+            a = c[idx * 2];
+            b = c[idx * 2 + 1];
+        }
+        const uint32_t misc = asu(b.w);
+        go = go & (o.x > a.x) & (o.x < a.w) & (o.y > a.y) & (o.y < b.x) & (o.z > a.z) & (o.z < b.y) & (misc < 4u);
+        if (go) {
+            const bool neg = __builtin_amdgcn_ubfe(s.negMask, misc, 1u) != 0u;
+            uint32_t left, right;
+            node_children<LAYOUT>(sc, node, asu(b.z), &left, &right);
+            stack_at(lds, s.sp + stride) = neg ? left : right;
+            s.sp += stride;
+            node = neg ? right : left;
+            s.node = node;
+        }
+    }
 }
 
 // Phase A with one dependent fetch per hit interior node instead of one per visited node

@@ -850,6 +850,9 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             if (free && k < end && idx < n) {
                 item = fetch(idx, lookup(idx), s);
                 if (!f2b) s.negMask = 0u;
+                if constexpr (!INSTR && !PAIR && !RING && !OPACITY) {
+                    if (sc.skipRoot && item != kNoItem) trav_skip_root<ALL_CACHED, LAYOUT, IDENT>(sc, s, lds, shift);
+                }
                 // (kNoItem: the queue item has no ray -- a hole of a virtual batch start)
                 ls = item != kNoItem ? kRun : kIdle;
             }

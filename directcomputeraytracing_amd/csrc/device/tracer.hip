@@ -1072,6 +1072,9 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         d.nodes = (const float4*)nodes;
         d.nodeCount = nodeCount;
         d.pairLayout = castPair ? 1u : 0u;
+        // trav_skip_root: levels of sure hits taken at a ray's start without their box tests
+        d.skipRoot = 1u;
+        if (const char* e = std::getenv("DCRT_SKIP_ROOT")) d.skipRoot = (uint32_t)std::max(0, std::min(16, std::atoi(e)));   // (A/B, tests)
         const size_t cacheBytes = [&] { return (size_t)d.cachedNodes * 32 + (size_t)d.cachedTris * (castAllCached ? 144 : 48) + (size_t)d.cachedInstances * 64; }();
         size_t launchLds = stackLds + cacheBytes;
         // The budget above divides 160 KiB evenly among the workgroups the registers allow; the

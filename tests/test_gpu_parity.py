@@ -1320,6 +1320,11 @@ KNOB_CASES = [
     ("top_nodes_64", "spaceship", {"DCRT_PAIR_TRAVERSAL": "1", "DCRT_TOP_NODES": "64"}),
     ("tune_8_4", "cornell", {"DCRT_TRAVERSAL_TUNE": "8,4"}),
     ("tune_64_64", "cornell", {"DCRT_TRAVERSAL_TUNE": "64,64", "DCRT_NO_LDS_CACHE": "1"}),
+    # trav_skip_root: off, and 16 levels of sure hits (cache-only, entry-free order / global-memory kernel)
+    ("skip_root_off", "cornell", {"DCRT_SKIP_ROOT": "0"}),
+    ("skip_root_16", "cornell", {"DCRT_SKIP_ROOT": "16"}),
+    ("skip_root_16_global", "xml_mix", {"DCRT_SKIP_ROOT": "16", "DCRT_PAIR_TRAVERSAL": "0"}),
+    ("flat_cast_off", "cornell", {"DCRT_FLAT_CAST": "0"}),
 ]
 
 
