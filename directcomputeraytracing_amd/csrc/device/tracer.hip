@@ -359,9 +359,9 @@ bool PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bv
 // The kernel then has no BLAS-entry step in its node visit: the TLAS leaf's box is tested as before,
 // the BLAS root is visited next (or after the empty node, which no ray hits: all its planes are +inf,
 // so its slab interval is empty or starts at +inf), and hits, their order and their tMax are the
-// reference's bit for bit -- the empty node adds a visit and a stack entry, no triangle test. (The
-// counting kernels keep PackBVH's order and their counts are the reference's.) False if a leaf holds
-// more than one triangle; `extraDepth` is the stack entries the empty nodes add (1).
+// reference's bit for bit -- the empty node adds a visit and a stack entry (the kernel's stack has
+// one row more), no triangle test. (The counting kernels keep PackBVH's order and their counts are
+// the reference's.) False if a leaf holds more than one triangle.
 bool EntryFreeLayout(const dcrt_flat_scene& s, std::vector<dcrt_bvh_node>* out)
 {
     const dcrt_bvh_node* nd = s.bvh_nodes;
