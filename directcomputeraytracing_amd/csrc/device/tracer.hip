@@ -362,7 +362,7 @@ bool PairLayout(const dcrt_flat_scene& s, uint32_t topNodes, std::vector<dcrt_bv
 // reference's bit for bit -- the empty node adds a visit and a stack entry (the kernel's stack has
 // one row more), no triangle test. (The counting kernels keep PackBVH's order and their counts are
 // the reference's.) False if a leaf holds more than one triangle.
-bool EntryFreeLayout(const dcrt_flat_scene& s, std::vector<dcrt_bvh_node>* out)
+bool EntryFreeLayout(const dcrt_flat_scene& s, std::vector<dcrt_bvh_node>* out, bool merge = true)
 {
     const dcrt_bvh_node* nd = s.bvh_nodes;
     const uint32_t n = s.bvh_node_count;
@@ -382,7 +382,7 @@ bool EntryFreeLayout(const dcrt_flat_scene& s, std::vector<dcrt_bvh_node>* out)
         if (it.inst1 == 0u && (v.misc & 0x4u)) {
             const uint32_t inst = (v.misc >> 3) & DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT;
             const uint32_t blas = v.right_child_or_prim_index;
-            if (blas < n && inst + 1u <= DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT &&
+            if (merge && blas < n && inst + 1u <= DCRT_BVHNODE_MISC_MASK_PRIMITIVE_COUNT &&
                 std::memcmp(v.bbox_min, nd[blas].bbox_min, sizeof(v.bbox_min)) == 0 &&
                 std::memcmp(v.bbox_max, nd[blas].bbox_max, sizeof(v.bbox_max)) == 0) {
                 // the BLAS root's box is the TLAS leaf's bit for bit (an identity instance's bounds
@@ -1108,7 +1108,9 @@ int dcrt_tracer::UploadScene(const dcrt_flat_scene& s)
         if (const char* e = std::getenv("DCRT_FLAT_CAST")) flatWanted = std::atoi(e) != 0;
         if (flatWanted && castAllCached && castIdent && mergedCasts && d.singlePrimLeaves) {
             std::vector<dcrt_bvh_node> flat;
-            if (EntryFreeLayout(s, &flat)) {
+            bool merge = true;   // (DCRT_FLAT_MERGE=0: every TLAS leaf over an empty node -- tests)
+            if (const char* e = std::getenv("DCRT_FLAT_MERGE")) merge = std::atoi(e) != 0;
+            if (EntryFreeLayout(s, &flat, merge)) {
                 const size_t flatLds = (size_t)(d.stackSize + 3u) * castBlock * 4 + flat.size() * 32 + (size_t)s.triangle_count * 144;
                 int identPerCU = 0, flatPerCU = 0;
                 CHECKED(castOccupancy(CastKernel(false, false, true, false, true, false), castLds, &identPerCU));

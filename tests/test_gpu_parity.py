@@ -792,18 +792,22 @@ def test_xml_scene_mesh_lights_bit_exact(gpu_tracer, golden_luts, oracle_mod):
     list(_render_and_compare(gpu_tracer, oracle_mod, golden_luts, s, [0, 7]))
 
 
-@pytest.mark.parametrize("cache", ["lds", "global", "pair"])
+@pytest.mark.parametrize("cache", ["lds", "lds-nomerge", "global", "pair"])
 @pytest.mark.parametrize("features", [0x05, 0x0F, 0x07])
 @pytest.mark.parametrize("scene_name", ["cornell", "xml_mix"])
 def test_traversal_variants_wavefront_bit_exact(native_lib, golden_luts, oracle_mod, monkeypatch, scene_name, features, cache):
     """The merged cast kernel's traversal variants through the whole wavefront path:
     Moller-Trumbore (WATERTIGHT off), BVH_NO_FRONT_TO_BACK_TRAVERSAL, both; the cache-only
     kernel (scene, permuted triangle copies and instance transforms in LDS: both scenes
-    fit), the global-memory kernel (DCRT_NO_LDS_CACHE) and the global-memory kernel with the
-    pair-expanding traversal (trav_visit_pair). xml_mix has transformed rectangle instances
-    (instance-space rays in the BLAS)."""
+    fit; Cornell's over the entry-free node order, its TLAS leaves merged with their BLAS roots
+    or -- lds-nomerge -- every one over an empty node), the global-memory kernel
+    (DCRT_NO_LDS_CACHE) and the global-memory kernel with the pair-expanding traversal
+    (trav_visit_pair). xml_mix has transformed rectangle instances (instance-space rays in the
+    BLAS)."""
     from conftest import GOLDEN
     from directcomputeraytracing_amd import Scene, WavefrontPathTracer
+    if cache == "lds-nomerge":
+        monkeypatch.setenv("DCRT_FLAT_MERGE", "0")
     if cache in ("global", "pair"):
         monkeypatch.setenv("DCRT_NO_LDS_CACHE", "1")
     monkeypatch.setenv("DCRT_PAIR_TRAVERSAL", "1" if cache == "pair" else "0")
@@ -817,6 +821,8 @@ def test_traversal_variants_wavefront_bit_exact(native_lib, golden_luts, oracle_
     try:
         list(_render_and_compare(t, oracle_mod, golden_luts, s, [0, 3]))
         assert t.info()["pair_traversal"] == (1 if cache == "pair" else 0)
+        if scene_name == "cornell" and cache.startswith("lds"):
+            assert t.info()["cast_identity"] == 2   # (the entry-free order)
     finally:
         t.destroy()
 
@@ -1325,6 +1331,7 @@ KNOB_CASES = [
     ("skip_root_16", "cornell", {"DCRT_SKIP_ROOT": "16"}),
     ("skip_root_16_global", "xml_mix", {"DCRT_SKIP_ROOT": "16", "DCRT_PAIR_TRAVERSAL": "0"}),
     ("flat_cast_off", "cornell", {"DCRT_FLAT_CAST": "0"}),
+    ("flat_no_merge", "cornell", {"DCRT_FLAT_MERGE": "0"}),
 ]
 
 
