@@ -643,6 +643,25 @@ DEV void trav_skip_root(const DeviceScene& sc, TravState& s, uint32_t* lds, uint
     }
 }
 
+// trav_skip_root for the pair traversal (trav_visit_pair): the root's sure hit leaves the lane
+// about to expand the root -- both children fetched and tested at its first step -- as the root's
+// own visit step would (take the root, an interior node: expand)
+DEV void trav_skip_root_pair(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift)
+{
+    if (sc.cachedNodes == 0u) return;
+    const float4* c = scene_cache(sc, lds - threadIdx.x, shift);
+    const float4 a = c[0], b = c[1];
+    const V3 o = s.lo();
+    const uint32_t misc = asu(b.w);
+    const bool inside = (o.x > a.x) & (o.x < a.w) & (o.y > a.y) & (o.y < b.x) & (o.z > a.z) & (o.z < b.y) & (misc < 4u) &
+                        (s.tMax > 0.0f);
+    if (inside) {
+        s.expand = true;
+        s.expNeg = __builtin_amdgcn_ubfe(s.negMask, misc, 1u) != 0u;
+        s.expRight = asu(b.z) | (s.node & 0x80000000u);
+    }
+}
+
 // Phase A with one dependent fetch per hit interior node instead of one per visited node
 // (the non-instrumented kernels; the counting kernels keep trav_visit). A node reached by
 // a pop or a BLAS entry is visited as in trav_visit (its box tested with the current tMax);

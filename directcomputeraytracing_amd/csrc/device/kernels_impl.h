@@ -852,6 +852,8 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
                 if (!f2b) s.negMask = 0u;
                 if constexpr (!INSTR && !PAIR && !RING && !OPACITY) {
                     if (sc.skipRoot && item != kNoItem) trav_skip_root<ALL_CACHED, LAYOUT, IDENT>(sc, s, lds, shift);
+                } else if constexpr (!INSTR && PAIR && !ALL_CACHED && !OPACITY) {
+                    if (sc.skipRoot && item != kNoItem) trav_skip_root_pair(sc, s, lds, shift);
                 }
                 // (kNoItem: the queue item has no ray -- a hole of a virtual batch start)
                 ls = item != kNoItem ? kRun : kIdle;
