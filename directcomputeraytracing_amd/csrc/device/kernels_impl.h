@@ -1537,9 +1537,14 @@ __device__ __forceinline__ float evaluate_filter(const FilterConsts& c, float px
 // halo are staged in LDS once (instead of every pixel fetching its (2r+1)^2 window from
 // memory), then every pixel gathers its window from LDS. Per pixel the arithmetic and its
 // order are those of the direct gather (images in order, window rows then columns).
-constexpr int kFilmTile = 16;
+#ifndef DCRT_FILM_TILE
+#define DCRT_FILM_TILE 16
+#endif
+constexpr int kFilmTile = DCRT_FILM_TILE;   // (a workgroup per kFilmTile^2-pixel tile, one thread per pixel)
+constexpr int kFilmThreads = kFilmTile * kFilmTile;
 constexpr int kFilmMaxHalo = 4;
 constexpr int kFilmSpan = kFilmTile + 2 * kFilmMaxHalo;
+constexpr int kFilmStage = (kFilmSpan * kFilmSpan + kFilmThreads - 1) / kFilmThreads;   // staging elements per thread
 
 __device__ __forceinline__ void film_pixel_window(const FilterConsts& c, uint32_t px, uint32_t py, uint32_t W, uint32_t H,
                                                   int* xs, int* xe, int* ys, int* ye)
@@ -1554,7 +1559,7 @@ __device__ __forceinline__ void film_pixel_window(const FilterConsts& c, uint32_
 
 // posList / valList (accumulate_images): image b's sample textures sit at posList[b] / valList[b]
 // (W*H each, e.g. other pipelines' slots) instead of at slot b of this film's.
-__global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts* fcon, uint32_t images, const Globals* guard,
+__global__ __launch_bounds__(kFilmThreads) void film_kernel(Film film, const FilterConsts* fcon, uint32_t images, const Globals* guard,
                                                    const float2* const* __restrict__ posList,
                                                    const float4* const* __restrict__ valList)
 {
@@ -1619,18 +1624,19 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
             // the LDS stores drain (lgkmcnt), not __syncthreads: that one's fence would also wait
             // for the next image's loads. (A buffer written at image b + 1 was last read at image
             // b - 1, which every thread finished before passing image b's barrier.)
-            // (three staging elements per thread: kFilmSpan^2 <= 3 x 256; plain variables, so the
-            // in-flight tile stays in registers)
-            static_assert(kFilmSpan * kFilmSpan <= 3 * 256, "three staging elements per thread");
+            // (kFilmStage staging elements per thread, in registers: the loops below unroll)
             const int nStage = spanX * spanY;
-            const int i0 = (int)threadIdx.x, i1 = i0 + 256, i2 = i0 + 512;
-            const bool s0 = i0 < nStage, s1 = i1 < nStage, s2 = i2 < nStage;
             const size_t oFirst = (size_t)oy * W + (size_t)ox;
-            const size_t o0 = s0 ? (size_t)(oy + i0 / spanX) * W + (size_t)(ox + i0 % spanX) : oFirst;
-            const size_t o1 = s1 ? (size_t)(oy + i1 / spanX) * W + (size_t)(ox + i1 % spanX) : oFirst;
-            const size_t o2 = s2 ? (size_t)(oy + i2 / spanX) * W + (size_t)(ox + i2 % spanX) : oFirst;
-            float2 nP0{}, nP1{}, nP2{};
-            float4 nV0{}, nV1{}, nV2{};
+            size_t off[kFilmStage];
+            float2 nP[kFilmStage];
+            float4 nV[kFilmStage];
+#pragma unroll
+            for (int k = 0; k < kFilmStage; ++k) {
+                const int i = (int)threadIdx.x + k * kFilmThreads;
+                off[k] = i < nStage ? (size_t)(oy + i / spanX) * W + (size_t)(ox + i % spanX) : oFirst;
+                nP[k] = make_float2(0.0f, 0.0f);
+                nV[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
             // image b's sample textures: this film's slot b, or a list entry (accumulate_images),
             // read one image ahead with a vector load (the index made opaque to the uniformity
             // analysis: a scalar load would share lgkmcnt with the LDS traffic, whose waits would
@@ -1642,18 +1648,25 @@ __global__ __launch_bounds__(256) void film_kernel(Film film, const FilterConsts
                 // (unconditional loads: a thread without a third element loads the span's first
                 // one again, so no branch splits the loads and their waits stay exact)
                 auto stage_load = [&](const float2* lp, const float4* lv) __attribute__((always_inline)) {
-                    nP0 = global_load2(lp, o0); nV0 = global_load4(lv, o0);
-                    nP1 = global_load2(lp, o1); nV1 = global_load4(lv, o1);
-                    nP2 = global_load2(lp, o2); nV2 = global_load4(lv, o2);
+#pragma unroll
+                    for (int k = 0; k < kFilmStage; ++k) {
+                        nP[k] = global_load2(lp, off[k]);
+                        nV[k] = global_load4(lv, off[k]);
+                    }
                 };
                 if (count > 0) stage_load(srcPos(0u), srcVal(0u));
                 const float2* nextPos = count > 1 ? srcPos(1u) : nullptr;
                 const float4* nextVal = count > 1 ? srcVal(1u) : nullptr;
                 for (uint32_t b = 0; b < count; ++b) {
                     const uint32_t buf = b & 1u;
-                    if (s0) { tPos[buf][i0] = nP0; tVal[buf][i0] = nV0; }
-                    if (s1) { tPos[buf][i1] = nP1; tVal[buf][i1] = nV1; }
-                    if (s2) { tPos[buf][i2] = nP2; tVal[buf][i2] = nV2; }
+#pragma unroll
+                    for (int k = 0; k < kFilmStage; ++k) {
+                        const int i = (int)threadIdx.x + k * kFilmThreads;
+                        if (i < nStage) {
+                            tPos[buf][i] = nP[k];
+                            tVal[buf][i] = nV[k];
+                        }
+                    }
                     if (b + 1 < count) {
                         stage_load(nextPos, nextVal);
                         if (b + 2 < count) { nextPos = srcPos(b + 2u); nextVal = srcVal(b + 2u); }

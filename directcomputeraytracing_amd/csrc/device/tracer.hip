@@ -585,7 +585,11 @@ struct dcrt_tracer {
         }
     }
     // film_kernel: one 16x16 tile per workgroup (grid-stride beyond the cap)
-    uint32_t FilmGrid() const { return std::max<uint32_t>(1u, std::min<uint32_t>(((filmW + 15) / 16) * ((filmH + 15) / 16), 8u * kMaxPersistentBlocks)); }
+    uint32_t FilmGrid() const
+    {
+        const uint32_t T = (uint32_t)kFilmTile;
+        return std::max<uint32_t>(1u, std::min<uint32_t>(((filmW + T - 1) / T) * ((filmH + T - 1) / T), 8u * kMaxPersistentBlocks * (256u / kFilmThreads)));
+    }
     uint32_t castResident = 0;         // persistent cast grid: resident workgroups on the whole chip
     uint32_t castResidentOpacity = 0;  // the same for the ALLOW_ANYHIT_SHADER variant
     uint32_t megaResident = 0;         // persistent megakernel grid
@@ -1517,7 +1521,7 @@ int dcrt_tracer::LaunchIteration(uint32_t par, bool timed, bool sequenced)
                            dGlobals, (const SampleOut*)dSampleOut);
     }
     if (sequenced) {
-        hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
+        hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(kFilmThreads), 0, stream, film, (const FilterConsts*)dFilter, 1u,
                            (const Globals*)dGlobals, (const float2* const*)nullptr, (const float4* const*)nullptr);
         hipLaunchKernelGGL(advance_image_kernel, dim3(1), dim3(64), 0, stream, dFrame, dGlobals);
     }
@@ -1635,7 +1639,7 @@ int dcrt_tracer::Accumulate(const dcrt_filter_params& f)
     Annotation an("SampleConvolution");
     if (!film.accum) { SetLastError("no film"); return DCRT_E_INVALID_ARG; }
     CHECKED(UploadFilter(f));
-    hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
+    hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(kFilmThreads), 0, stream, film, (const FilterConsts*)dFilter, 1u,
                        (const Globals*)nullptr, (const float2* const*)nullptr, (const float4* const*)nullptr);
     HIPCHECK(hipGetLastError());
     return DCRT_OK;
@@ -1672,7 +1676,7 @@ int dcrt_tracer::RenderImages(uint32_t firstSeed, uint32_t count, const dcrt_fil
             auto mk = (frame.features & DCRT_FEATURE_ALLOW_ANYHIT) ? megakernel<true> : megakernel<false>;
             hipExtLaunchKernelGGL(mk, dim3(megaResident), dim3(castBlock), castLdsFull, stream, e0, e1, 0, scene,
                                   (const FrameConstants*)dFrame, film, dGlobals, (uint32_t)(film.debugRng != nullptr));
-            hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, 1u,
+            hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(kFilmThreads), 0, stream, film, (const FilterConsts*)dFilter, 1u,
                                (const Globals*)nullptr, (const float2* const*)nullptr, (const float4* const*)nullptr);
             HIPCHECK(hipGetLastError());
         }
@@ -1779,7 +1783,7 @@ int dcrt_tracer::AccumulateImages(const void* const* pos, const void* const* val
     }
     CHECKED(UploadFilter(f));   // (synchronises: the list's staging below is reused safely)
     HIPCHECK(hipMemcpyAsync(dSourceLists, lists.data(), lists.size() * sizeof(void*), hipMemcpyHostToDevice, stream));
-    hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(256), 0, stream, film, (const FilterConsts*)dFilter, count,
+    hipLaunchKernelGGL(film_kernel, dim3(FilmGrid()), dim3(kFilmThreads), 0, stream, film, (const FilterConsts*)dFilter, count,
                        (const Globals*)nullptr, (const float2* const*)dSourceLists, (const float4* const*)(dSourceLists + count));
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(stream));   // (the host list is released on return)
