@@ -519,14 +519,7 @@ constexpr uint32_t kMiscIdentityLeaf = 1u;
 // BLAS entries and exits change nothing but the node and instance, and only the triangle tests
 // take the instance-space ray, formed where they need it (o + 0, d + 0: the same bits as the
 // identity transform). The nine registers of the instance-space ray are then free.
-// FLAT (the entry-free node order, tracer.hip EntryFreeLayout): an interior node's `right` field
-// carries two flags above the child index -- bit 31: its left child, bit 30: its right child is a
-// leaf whose box is this node's bit for bit (a quad's two triangles, say). Descending into such a
-// near child parks at it at once: its own visit would repeat this node's box test with the same
-// ray and tMax (no leaf lies between the two tests) and park there.
-constexpr uint32_t kFlatEqLeft = 0x80000000u, kFlatEqRight = 0x40000000u, kFlatChildMask = 0x3FFFFFFFu;
-template <bool INSTR, bool ALL_CACHED = false, int LAYOUT = kLayoutScene, bool ENTER = false, bool IDENT = false, bool RING = false,
-          bool FLAT = false>
+template <bool INSTR, bool ALL_CACHED = false, int LAYOUT = kLayoutScene, bool ENTER = false, bool IDENT = false, bool RING = false>
 DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift, TraversalStats& st)
 {
     if (INSTR) ++st.nodes;
@@ -555,8 +548,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
     }
     const bool hit = IDENT ? ray_aabb_raw(s.o, s.invW, s.tMin, s.tMax, a, b) : ray_aabb(s, a, b);
     const uint32_t misc = asu(b.w);
-    const uint32_t rightRaw = asu(b.z);
-    const uint32_t right = FLAT ? rightRaw & kFlatChildMask : rightRaw;
+    const uint32_t right = asu(b.z);
     // leaf: TLAS-leaf bit (4) or a primitive count (bits 3 and up); parked = hit && leaf
     // is formed as hit ^ descend below (a mask operation, not a second compare of misc)
     const bool descend = hit & (misc < 4u);
@@ -603,7 +595,6 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
         s.negMask = neg_mask(s.d, s.negMask);
     }
     s.parked = hit ^ (descend | enter);
-    if (FLAT) s.parked = s.parked | (descend & ((rightRaw & (neg ? kFlatEqRight : kFlatEqLeft)) != 0u));
     if (!ALL_CACHED) {   // (ALL_CACHED: phase B reads them from the LDS copy of the node)
         s.leafRef = right;
         s.leafMisc = misc;
@@ -618,7 +609,7 @@ DEV bool trav_visit(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t
 // visit is then the root's descend, done here at the ray's start without the box test: the near
 // child (split axis' direction sign) next, the far one pushed -- trav_visit's outcome bit for bit.
 // (Non-counting kernels: the counting ones visit the root as the reference does.)
-template <bool ALL_CACHED, int LAYOUT, bool IDENT, bool FLAT = false>
+template <bool ALL_CACHED, int LAYOUT, bool IDENT>
 DEV void trav_skip_root(const DeviceScene& sc, TravState& s, uint32_t* lds, uint32_t shift)
 {
     // (and on down the near children while their boxes hold the origin strictly: each of those
@@ -643,7 +634,7 @@ DEV void trav_skip_root(const DeviceScene& sc, TravState& s, uint32_t* lds, uint
         if (go) {
             const bool neg = __builtin_amdgcn_ubfe(s.negMask, misc, 1u) != 0u;
             uint32_t left, right;
-            node_children<LAYOUT>(sc, node, FLAT ? asu(b.z) & kFlatChildMask : asu(b.z), &left, &right);
+            node_children<LAYOUT>(sc, node, asu(b.z), &left, &right);
             stack_at(lds, s.sp + stride) = neg ? left : right;
             s.sp += stride;
             node = neg ? right : left;

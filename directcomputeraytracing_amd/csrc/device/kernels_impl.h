@@ -851,7 +851,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
                 item = fetch(idx, lookup(idx), s);
                 if (!f2b) s.negMask = 0u;
                 if constexpr (!INSTR && !PAIR && !RING && !OPACITY) {
-                    if (sc.skipRoot && item != kNoItem) trav_skip_root<ALL_CACHED, LAYOUT, IDENT, FLAT>(sc, s, lds, shift);
+                    if (sc.skipRoot && item != kNoItem) trav_skip_root<ALL_CACHED, LAYOUT, IDENT>(sc, s, lds, shift);
                 } else if constexpr (!INSTR && PAIR && !ALL_CACHED && !OPACITY) {
                     if (sc.skipRoot && item != kNoItem) trav_skip_root_pair(sc, s, lds, shift);
                 }
@@ -872,7 +872,7 @@ __device__ __forceinline__ void persistent_trace(const DeviceScene& sc, uint32_t
             for (int k = 0; k < kVisitsPerCheck; ++k) {
                 if (ls == kRun) {
                     const bool fin = PAIR && !INSTR && !ALL_CACHED ? trav_visit_pair<false, LAYOUT, RING>(sc, s, lds, shift)
-                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, !FLAT && (ALL_CACHED || IDENT) && !OPACITY && DCRT_INLINE_ENTRY, IDENT, RING, FLAT>(sc, s, lds, shift, st);
+                                                                   : trav_visit<INSTR, ALL_CACHED, LAYOUT, !FLAT && (ALL_CACHED || IDENT) && !OPACITY && DCRT_INLINE_ENTRY, IDENT, RING>(sc, s, lds, shift, st);
                     if (fin) ls = kFin;
                     else if (s.parked) ls = kPark;
                 }

@@ -419,22 +419,7 @@ bool EntryFreeLayout(const dcrt_flat_scene& s, std::vector<dcrt_bvh_node>* out, 
         }
         if (out->size() > (size_t)n * 4u + 64u) { ok = false; break; }   // (a malformed tree: refuse)
     }
-    if (!ok || out->empty() || out->size() > kFlatChildMask) return false;
-    // the equal-box leaf flags of the interior nodes (kFlatEqLeft / kFlatEqRight, dscene.h)
-    const bool eqFlags = [] { const char* e = std::getenv("DCRT_FLAT_EQ_LEAF"); return !e || std::atoi(e) != 0; }();
-    for (size_t i = 0; eqFlags && i < out->size(); ++i) {
-        dcrt_bvh_node& v = (*out)[i];
-        if (v.misc >= 4u) continue;
-        const uint32_t l = (uint32_t)i + 1u, r = v.right_child_or_prim_index;
-        auto eqLeaf = [&](uint32_t c) {
-            const dcrt_bvh_node& w = (*out)[c];
-            return w.misc >= 4u && std::memcmp(w.bbox_min, v.bbox_min, sizeof(v.bbox_min)) == 0 &&
-                   std::memcmp(w.bbox_max, v.bbox_max, sizeof(v.bbox_max)) == 0;
-        };
-        const bool el = l < out->size() && eqLeaf(l), er = r < out->size() && eqLeaf(r);
-        v.right_child_or_prim_index = r | (el ? kFlatEqLeft : 0u) | (er ? kFlatEqRight : 0u);
-    }
-    return true;
+    return ok && !out->empty();
 }
 
 }  // namespace

@@ -1332,7 +1332,6 @@ KNOB_CASES = [
     ("skip_root_16_global", "xml_mix", {"DCRT_SKIP_ROOT": "16", "DCRT_PAIR_TRAVERSAL": "0"}),
     ("flat_cast_off", "cornell", {"DCRT_FLAT_CAST": "0"}),
     ("flat_no_merge", "cornell", {"DCRT_FLAT_MERGE": "0"}),
-    ("flat_no_eq_leaf", "cornell", {"DCRT_FLAT_EQ_LEAF": "0"}),
 ]
 
 
